@@ -1,0 +1,170 @@
+"""Synthetic duplex-UMI inputs for the five BASELINE.json configs.
+
+Two generators with the same distribution:
+
+* ``family_records`` builds pysam-style records (for BAM files, the end-to-end
+  CLI path and the reference-run golden vectors);
+* ``packed_config`` builds a device batch directly in the packed columnar
+  layout (for the bench at 10 M+ reads, where per-record Python is too slow).
+
+Family layout follows the fgbio GroupReadsByUmi output the reference expects
+(DuplexUMIConsensusReads.py:132-154, :1185-1217): reads of one MI family are
+contiguous; A1/B2 map forward at P, B1/A2 reverse at P+I-L; MI is ``k/A`` on
+A1/A2 and ``k/B`` on B1/B2; RX is ``U1-U2`` on A and ``U2-U1`` on B.
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+
+from .records import AlignedSegment
+
+_ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
+# flags: paired|proper + strand/mate + read1/read2
+FLAG_A1, FLAG_B2, FLAG_B1, FLAG_A2 = 99, 163, 83, 147
+
+
+@dataclasses.dataclass
+class SynthConfig:
+    name: str
+    n_families: int
+    read_len: int = 150
+    sub_size: str = "poisson5"       # poisson5 | fixed8 | zipf | loguniform | poisson4p1
+    fixed_size: int = 8
+    zipf_s: float = 1.5
+    zipf_max: int = 100
+    logu_lo: int = 100
+    logu_hi: int = 1000
+    indel_frac: float = 0.0          # reads carrying one I or D of 1-3 bp at offset 20-130
+    softclip_frac: float = 0.0       # reads carrying a 1-10 bp soft clip
+    low_mapq_frac: float = 0.02
+    seed: int = 1
+    n_loci: int = 0                  # >0: families share these loci (deep panel)
+
+
+CONFIGS = {
+    "C1": SynthConfig("C1", 1000, sub_size="poisson5", seed=1),
+    "C2": SynthConfig("C2", 312_500, sub_size="fixed8", fixed_size=8, low_mapq_frac=0.0, seed=2),
+    "C3": SynthConfig("C3", 0, sub_size="zipf", indel_frac=0.05, softclip_frac=0.03, seed=3),
+    "C4": SynthConfig("C4", 1000, sub_size="loguniform", n_loci=20, seed=4),
+    "C5": SynthConfig("C5", 0, sub_size="poisson4p1", seed=5),
+}
+
+
+def _sub_sizes(rng, cfg, n):
+    if cfg.sub_size == "fixed8":
+        return np.full(n, cfg.fixed_size, dtype=np.int64)
+    if cfg.sub_size == "poisson5":
+        return np.clip(rng.poisson(5, n), 1, 12)
+    if cfg.sub_size == "poisson4p1":
+        return rng.poisson(4, n) + 1
+    if cfg.sub_size == "zipf":
+        k = np.arange(1, cfg.zipf_max + 1)
+        p = k ** -cfg.zipf_s
+        p /= p.sum()
+        return rng.choice(k, size=n, p=p)
+    if cfg.sub_size == "loguniform":
+        return np.exp(rng.uniform(np.log(cfg.logu_lo), np.log(cfg.logu_hi), n)).astype(np.int64)
+    raise ValueError(cfg.sub_size)
+
+
+def _quals(rng, n):
+    u = rng.random(n)
+    q = np.where(u < 0.80, 37, np.where(u < 0.92, 25, 12)).astype(np.uint8)
+    return q
+
+
+def _mutate(rng, tmpl, q):
+    """Substitute bases at the phred error rate 10^(-Q/10)."""
+    err = rng.random(len(tmpl)) < 10.0 ** (-q.astype(np.float64) / 10.0)
+    out = tmpl.copy()
+    if err.any():
+        shift = rng.integers(1, 4, err.sum())
+        idx = np.searchsorted(_ACGT, out[err])
+        out[err] = _ACGT[(idx + shift) % 4]
+    return out
+
+
+def _one_read(rng, cfg, tmpl_fwd, start, L, reverse):
+    """Bases/quals/cigar of one read copied from the family template."""
+    q = _quals(rng, L)
+    if not (q >= 20).any():
+        q[rng.integers(0, L)] = 37
+    cigar = [(0, L)]
+    shift = 0
+    seq = tmpl_fwd[start:start + L].copy()
+    if cfg.indel_frac and rng.random() < cfg.indel_frac:
+        off = int(rng.integers(20, min(131, L - 5)))
+        ln = int(rng.integers(1, 4))
+        if rng.random() < 0.5:   # insertion: ln extra bases inside the read
+            ins = _ACGT[rng.integers(0, 4, ln)]
+            seq = np.concatenate([seq[:off], ins, seq[off:L - ln]])
+            cigar = [(0, off), (1, ln), (0, L - off - ln)]
+        else:                    # deletion: skip ln template bases
+            seq = np.concatenate([seq[:off], tmpl_fwd[start + off + ln:start + L + ln]])
+            cigar = [(0, off), (2, ln), (0, L - off)]
+    if cfg.softclip_frac and rng.random() < cfg.softclip_frac:
+        sc = int(rng.integers(1, 11))
+        if rng.random() < 0.5:
+            ops = [(4, sc)] + cigar
+            ops[1] = (0, ops[1][1] - sc)
+            shift = sc
+        else:
+            ops = cigar[:-1] + [(0, cigar[-1][1] - sc), (4, sc)]
+        cigar = ops
+    seq = _mutate(rng, seq, q)
+    return seq, q, cigar, shift
+
+
+def family_records(rng, cfg: SynthConfig, fam_id: int, tid=0, locus=None):
+    """Records of one duplex family in BAM order (pairs adjacent)."""
+    L = cfg.read_len
+    n4 = _sub_sizes(rng, cfg, 4)
+    ins = int(np.clip(rng.normal(300, 30), 200, 500))
+    P = int(locus if locus is not None else rng.integers(1000, 100_000_000))
+    tmpl = _ACGT[rng.integers(0, 4, ins + 20)]
+    u1 = "".join(chr(c) for c in _ACGT[rng.integers(0, 4, 8)])
+    u2 = "".join(chr(c) for c in _ACGT[rng.integers(0, 4, 8)])
+    recs = []
+    # subfamily -> (flag, strand tag, reverse?, rx)
+    spec = [(FLAG_A1, "A", False), (FLAG_B2, "B", False), (FLAG_B1, "B", True), (FLAG_A2, "A", True)]
+    for k, (flag, strand, rev) in enumerate(spec):
+        for j in range(int(n4[k])):
+            start = 0 if not rev else ins - L
+            seq, q, cig, shift = _one_read(rng, cfg, tmpl, start, L, rev)
+            r = AlignedSegment()
+            r.query_name = f"mol{fam_id}_{k}_{j}"
+            r.flag = flag
+            r.reference_id = tid
+            r.reference_start = P + start + shift
+            mq = int(rng.integers(20, 61))
+            if rng.random() < cfg.low_mapq_frac:
+                mq = int(rng.integers(0, 20))
+            r.mapping_quality = mq
+            r.cigartuples = cig
+            r.query_sequence = seq.tobytes().decode()
+            r.query_qualities = q.tolist()
+            r.next_reference_id = tid
+            r.next_reference_start = P + (ins - L if not rev else 0)
+            r.template_length = ins if not rev else -ins
+            rx = f"{u1}-{u2}" if strand == "A" else f"{u2}-{u1}"
+            r.set_tags([("MI", f"{fam_id}/{strand}"), ("RX", rx)])
+            recs.append(r)
+    return recs
+
+
+def write_config_bam(path, cfg: SynthConfig, n_families=None, seed=None):
+    """Write a synthetic duplex BAM (families contiguous, coordinate-agnostic)."""
+    from .bam import AlignmentFile, BamHeader
+    rng = np.random.default_rng(cfg.seed if seed is None else seed)
+    hdr = BamHeader("@HD\tVN:1.6\tSO:unsorted\n@SQ\tSN:chr1\tLN:248956422\n", ["chr1"], [248956422])
+    n = cfg.n_families if n_families is None else n_families
+    with AlignmentFile(path, "wb", header=hdr) as out:
+        for f in range(n):
+            locus = None
+            if cfg.n_loci:
+                locus = 1_000_000 + 10_000 * (f % cfg.n_loci)
+            for r in family_records(rng, cfg, f, locus=locus):
+                out.write(r)
+    return path

@@ -1,0 +1,118 @@
+"""Consensus record builder: the record/tag half of ``make_consensus_read``.
+
+Given the numeric results of one consensus (from the device batch or any other
+backend) this builds the exact record the reference writes:
+
+* name/flag/rname helpers   get_consensus_id / get_consensus_flag (DuplexUMIConsensusReads.py:892-968)
+* single-strand tags        add_tags, method="single_strand" (:1054-1073)
+* duplex tags               add_tags, method="double_strand" (:1076-1120)
+* record assembly order     make_consensus_read (:1372-1384)
+* mate fields               fix_paired_end_fields (:1390-1419)
+
+``sd``/``se``/``cd``/``ce`` are the Python ``str()`` of a list of numpy ints as
+numpy 1.x printed it (``"[1, 2, 3]"``): the reference needs numpy < 1.24
+(``np.float`` at :686), whose scalars repr as plain integers.
+"""
+from __future__ import annotations
+
+from .records import AlignedSegment
+
+
+def int_list_str(vals) -> str:
+    return "[" + ", ".join(str(int(v)) for v in vals) + "]"
+
+
+def family_code(read) -> str:
+    return read.get_tag("MI").split("/")[0]
+
+
+def consensus_id(read, method: str) -> str:
+    """get_consensus_id (:892-933)."""
+    code = family_code(read)
+    if method == "single_strand":
+        if not read.is_reverse and read.is_read1:
+            sub = "A1"
+        elif read.is_reverse and read.is_read2:
+            sub = "A2"
+        elif read.is_reverse and read.is_read1:
+            sub = "B1"
+        else:
+            sub = "B2"
+        return "consensus_family" + code + "_" + sub
+    pe = "1" if not read.is_reverse else "2"
+    return "consensus_family" + code + "_paired-end" + pe
+
+
+def consensus_flag(read, method: str) -> int:
+    """get_consensus_flag (:936-968)."""
+    if method == "single_strand":
+        return read.flag
+    return 99 if not read.is_reverse else 147
+
+
+def _base_record(core, read0, method):
+    r = AlignedSegment()
+    r.query_name = consensus_id(read0, method)
+    r.flag = consensus_flag(read0, method)
+    r.reference_id = read0.reference_id
+    r.reference_start = int(core["pos"])
+    r.mapping_quality = int(core["mapq"])
+    r.cigartuples = [(int(op), int(n)) for op, n in core["cigar"]]
+    r.query_sequence = core["seq"]
+    r.query_qualities = [int(q) for q in core["qual"]]
+    return r
+
+
+def single_strand_record(core, reads) -> AlignedSegment:
+    """Record of one single-strand consensus; ``reads`` are the (downsampled,
+    preprocessed) input records in reference order; ``core`` holds pos, mapq,
+    cigar, seq, qual, d, D, M, e, E."""
+    read0 = reads[0]
+    r = _base_record(core, read0, "single_strand")
+    r.set_tags((("MI", read0.get_tag("MI")),
+                ("RX", read0.get_tag("RX")),
+                ("sQ", [int(x.mapping_quality) for x in reads]),
+                ("sd", int_list_str(core["d"])),
+                ("sD", int(core["D"])),
+                ("sM", int(core["M"])),
+                ("se", int_list_str(core["e"])),
+                ("sE", float(core["E"]))))
+    return r
+
+
+def duplex_record(core, ss_a: AlignedSegment, ss_b: AlignedSegment) -> AlignedSegment:
+    """Record of one duplex consensus built from two single-strand records."""
+    r = _base_record(core, ss_a, "double_strand")
+
+    def aq(rec):
+        q = rec.query_qualities
+        return "".join(chr(x + 33) for x in q) if q is not None else ""
+
+    r.set_tags((("MI", ss_a.get_tag("MI").split("/")[0]),
+                ("RX", ss_a.get_tag("RX")),
+                ("aQ", list(ss_a.get_tag("sQ"))),
+                ("bQ", list(ss_b.get_tag("sQ"))),
+                ("cQ", [ss_a.mapping_quality, ss_b.mapping_quality]),
+                ("ad", ss_a.get_tag("sd")), ("bd", ss_b.get_tag("sd")), ("cd", int_list_str(core["d"])),
+                ("aD", ss_a.get_tag("sD")), ("bD", ss_b.get_tag("sD")), ("cD", int(core["D"])),
+                ("aM", ss_a.get_tag("sM")), ("bM", ss_b.get_tag("sM")), ("cM", int(core["M"])),
+                ("ae", ss_a.get_tag("se")), ("be", ss_b.get_tag("se")), ("ce", int_list_str(core["e"])),
+                ("aE", ss_a.get_tag("sE")), ("bE", ss_b.get_tag("sE")), ("cE", float(core["E"])),
+                ("ac", ss_a.query_sequence), ("bc", ss_b.query_sequence),
+                ("aq", aq(ss_a)), ("bq", aq(ss_b))))
+    return r
+
+
+def fix_paired_end_fields(pe1: AlignedSegment, pe2: AlignedSegment):
+    """fix_paired_end_fields (:1390-1419)."""
+    tids = [pe1.reference_id, pe2.reference_id]
+    pos = [pe1.reference_start, pe2.reference_start]
+    read_length = pe2.query_alignment_length
+    pe1.next_reference_id = tids[1]
+    pe2.next_reference_id = tids[0]
+    pe1.next_reference_start = pos[1]
+    pe2.next_reference_start = pos[0]
+    tlen = pos[1] + read_length - pos[0]
+    pe1.template_length = tlen
+    pe2.template_length = -tlen
+    return [pe1, pe2]
