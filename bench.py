@@ -1,0 +1,170 @@
+"""Benchmark: consensus bases/s of the duplex-consensus hot path on MI355X.
+
+Workload (BASELINE.json configs[1]): per GPU a synthetic
+duplex batch of 10 M reads = 312,500 MI families x 4 subfamilies x 8 reads,
+2x150 bp ``150M`` reads, no indels, qualities {Q37 .80, Q25 .12, Q12 .08}.
+One step = the whole hot path over that batch with inputs resident in HBM:
+per-read preprocessing (k_prep), 1.25 M single-strand consensus
+(k_consensus<false>) and 625 k duplex consensus (k_consensus<true>).
+
+value = duplex consensus bases emitted by all ranks per second (weak scaling:
+each rank owns its own families, no data-path collective; max time over
+ranks).  roofline = the single-strand kernel's algorithmic bytes
+ / its HIP-event-timed average launch / 8 TB/s.
+cpu_baseline = the C restatement (oracle/, kind "port") on a bounded sample
+of the same workload on this host.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--families F]
+(N > 1 is launched by torch.distributed.run, one process per GPU.)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+METRIC = "consensus bases/sec (whole node) + SSCS kernel HBM GB/s vs peak, 1/2/4/8 GPUs"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def sscs_algorithmic_bytes(packed):
+    """sum_r(2 len_r + 4 n_cig_r + 4 + 1) + T*(2 + 4) + 16 per
+    subfamily, with T the subfamily's alignment width (here T_ub == T: no
+    clipping, no indels)."""
+    per_read = 2 * packed.seq_len.astype(np.int64) + 4 * packed.cig_n.astype(np.int64) + 5
+    reads_b = int(per_read.sum())
+    cols = int(packed.ss_col_off[-1])
+    n_sub = len(packed.ss_col_off) - 1
+    return reads_b + 6 * cols + 16 * n_sub
+
+
+def cpu_baseline(args, n_sample_fam):
+    from duplexumiconsensusreads_amd import synth
+    from duplexumiconsensusreads_amd.params import ConsensusParams
+    from oracle import dcr_oracle_c
+    threads = min(16, os.cpu_count() or 1)
+    sample = synth.packed_fixed_size(n_sample_fam, seed=args.seed)
+    t0 = time.perf_counter()
+    ss, ds, _ = dcr_oracle_c.run(sample, ConsensusParams(), n_threads=threads, want_info=False)
+    dt = time.perf_counter() - t0
+    bases = int(ds.len.sum())
+    return {"value": bases / dt, "unit": "consensus bases/s", "cores": threads, "kind": "port",
+            "sample": f"{n_sample_fam} families ({sample.n_reads} reads) of the same C2 workload, "
+                      f"C restatement oracle/dcr_oracle.c, {threads} threads, {dt:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--families", type=int, default=312_500, help="families per GPU (C2: 312,500)")
+    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--cpu-sample", type=int, default=65_536, help="families in the CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    from duplexumiconsensusreads_amd import _lib, synth
+    from duplexumiconsensusreads_amd.device import DeviceBatch
+    from duplexumiconsensusreads_amd.params import ConsensusParams
+
+    t0 = time.perf_counter()
+    packed = synth.packed_fixed_size(args.families, seed=args.seed + 1000 * rank)
+    log(f"[rank {rank}] generated {packed.n_reads} reads in {time.perf_counter() - t0:.1f} s")
+    dev = f"cuda:{local}"
+    db = DeviceBatch(packed, device=dev)
+    ctx = _lib.Context(ConsensusParams(), device=local)
+    ctx.reserve(db.batch_struct)
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        ctx.run_device(db.batch_struct, db.ss_struct, db.ds_struct)
+    ctx.sync()
+    # correctness guard on the bench batch itself: every record must be OK
+    st_ss = db.out["ss"]["status"][:4 * packed.n_fam]
+    st_ds = db.out["ds"]["status"][:2 * packed.n_fam]
+    n_bad = int((st_ss != 0).sum().item() + (st_ds != 0).sum().item())
+    bases = int(db.out["ds"]["len"].view(torch.int32)[:2 * packed.n_fam].sum().item())
+
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    ss_ms = prep_ms = ds_ms = 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.run_device(db.batch_struct, db.ss_struct, db.ds_struct)
+        tm = ctx.last_timing()          # waits on this step's events only
+        ss_ms += tm["single_strand"]
+        prep_ms += tm["prep"]
+        ds_ms += tm["duplex"]
+    ctx.sync()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        b = torch.tensor([bases, n_bad], dtype=torch.int64, device=dev)
+        tdist.all_reduce(b, op=tdist.ReduceOp.SUM)
+        total_bases, n_bad = int(b[0].item()), int(b[1].item())
+    else:
+        total_bases = bases
+
+    if rank == 0:
+        ms_step = elapsed * 1000.0 / args.steps
+        value = total_bases * args.steps / elapsed
+        ss_avg_ms = ss_ms / args.steps
+        alg = sscs_algorithmic_bytes(packed)
+        achieved = alg / (ss_avg_ms / 1000.0) / 1e9
+        res = {
+            "metric": METRIC, "value": value, "unit": "consensus bases/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": "C2 (BASELINE.json configs[1]): 10M-read synthetic duplex batch per GPU, "
+                                   "312,500 MI families x 4 subfamilies x 8 reads, 2x150bp, no indels",
+                       "families_per_gpu": packed.n_fam, "reads_per_gpu": packed.n_reads,
+                       "input_bytes_per_gpu": packed.nbytes(),
+                       "kernel_ms": {"prep": prep_ms / args.steps, "single_strand": ss_avg_ms,
+                                     "duplex": ds_ms / args.steps},
+                       "records_not_ok": n_bad,
+                       "parallelism": f"family-sharded x{world}, no data-path collective"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_consensus<false> (single-strand)",
+                         "algorithmic_bytes_per_launch": alg},
+        }
+        if not args.no_cpu and world == 1:
+            res["cpu_baseline"] = cpu_baseline(args, args.cpu_sample)
+        else:
+            res["cpu_baseline"] = None
+        print(json.dumps(res), flush=True)
+    ctx.close()
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,142 @@
+"""ctypes binding of libdcr.so (the C-ABI in include/dcr.h).
+
+This is the product path: it loads the in-tree HIP library built for gfx950
+and fails loudly if it is missing or the device is not an MI355X.  There is
+no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .batch import DcrBatch, DcrOut, DcrReadInfo, OutArrays, PackedBatch
+from .params import ConsensusParams, DcrParams, build_dcr_params
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdcr.so")
+
+EXPORTS = {
+    "dcr_abi_version": (ctypes.c_int, []),
+    "dcr_last_error": (ctypes.c_char_p, []),
+    "dcr_create": (ctypes.c_void_p, [ctypes.c_int, ctypes.c_void_p]),
+    "dcr_destroy": (None, [ctypes.c_void_p]),
+    "dcr_set_params": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "dcr_reserve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "dcr_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
+    "dcr_run_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "dcr_run_batch_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p]),
+    "dcr_sync": (ctypes.c_int, [ctypes.c_void_p]),
+    "dcr_read_info_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
+    "dcr_last_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+}
+
+_lib = None
+
+
+class DcrError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libdcr.so (raises if absent: build it with __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        # torch ships its own libamdhip64.so.7 (same soname as /opt/rocm's):
+        # load it first so libdcr and torch's allocator share one HIP runtime
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        if not os.path.exists(LIB_PATH):
+            raise DcrError(f"{LIB_PATH} not built — run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.dcr_abi_version() != 1:
+            raise DcrError("libdcr.so ABI mismatch")
+        _lib = lib
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise DcrError(f"libdcr error {rc}: {load().dcr_last_error().decode()}")
+
+
+class Context:
+    """One GPU context (``dcr_ctx``): stream, parameters, workspace."""
+
+    def __init__(self, params: ConsensusParams = ConsensusParams(), device: int = 0):
+        lib = load()
+        self.params = params
+        self._p = build_dcr_params(params)
+        self.device = device
+        self._ctx = lib.dcr_create(device, ctypes.byref(self._p))
+        if not self._ctx:
+            raise DcrError(f"dcr_create failed: {lib.dcr_last_error().decode()}")
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            load().dcr_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_params(self, params: ConsensusParams):
+        self.params = params
+        self._p = build_dcr_params(params)
+        _check(load().dcr_set_params(self._ctx, ctypes.byref(self._p)))
+
+    @property
+    def stream(self):
+        return load().dcr_stream(self._ctx)
+
+    # -- host-pointer path ------------------------------------------------
+    def run_host(self, packed: PackedBatch, want_info=True):
+        ss = OutArrays(4 * packed.n_fam, packed.ss_cols)
+        ds = OutArrays(2 * packed.n_fam, packed.ds_cols)
+        b = packed.as_struct()
+        so, do = ss.as_struct(), ds.as_struct()
+        _check(load().dcr_run_batch_host(self._ctx, ctypes.byref(b), ctypes.byref(so), ctypes.byref(do)))
+        info = self.read_info(packed.n_reads) if want_info else None
+        return ss, ds, info
+
+    def read_info(self, n):
+        arr = (DcrReadInfo * max(n, 1))()
+        _check(load().dcr_read_info_host(self._ctx, ctypes.cast(arr, ctypes.c_void_p), n))
+        return {k: np.array([getattr(x, k) for x in arr[:n]])
+                for k in ("seq_start", "len", "n_cig", "status", "has_ins")}
+
+    # -- device-pointer path (inputs resident in HBM) ----------------------
+    def reserve(self, batch_struct: DcrBatch):
+        _check(load().dcr_reserve(self._ctx, ctypes.byref(batch_struct)))
+
+    def run_device(self, batch_struct: DcrBatch, ss: DcrOut, ds: DcrOut):
+        """Asynchronous on the context stream."""
+        _check(load().dcr_run_batch(self._ctx, ctypes.byref(batch_struct), ctypes.byref(ss), ctypes.byref(ds)))
+
+    def sync(self):
+        _check(load().dcr_sync(self._ctx))
+
+    def last_timing(self):
+        ms = (ctypes.c_float * 4)()
+        _check(load().dcr_last_timing(self._ctx, ms))
+        return dict(prep=ms[0], single_strand=ms[1], duplex=ms[2], total=ms[3])
+
+
+def backend(ctx: Context):
+    """pipeline.Backend running on the GPU through the host-pointer entry."""
+    def run(packed, params):
+        if params != ctx.params:
+            ctx.set_params(params)
+        return ctx.run_host(packed)
+    return run

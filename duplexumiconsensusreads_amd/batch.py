@@ -28,6 +28,8 @@ _f64p = ctypes.POINTER(ctypes.c_double)
 
 class DcrBatch(ctypes.Structure):
     _fields_ = [("n_fam", ctypes.c_int32), ("n_reads", ctypes.c_int32),
+                ("n_cigar", ctypes.c_int64), ("n_bases", ctypes.c_int64),
+                ("ss_cols", ctypes.c_int64), ("ds_cols", ctypes.c_int64),
                 ("sub_off", ctypes.c_void_p), ("read_pos", ctypes.c_void_p),
                 ("read_mapq", ctypes.c_void_p), ("seq_off", ctypes.c_void_p),
                 ("seq_len", ctypes.c_void_p), ("cig_off", ctypes.c_void_p),
@@ -92,6 +94,10 @@ class PackedBatch:
         s = DcrBatch()
         s.n_fam = self.n_fam
         s.n_reads = self.n_reads
+        s.n_cigar = self.n_cigar
+        s.n_bases = self.n_bases
+        s.ss_cols = self.ss_cols
+        s.ds_cols = self.ds_cols
         for k in BATCH_FIELDS:
             setattr(s, k, ptrs[k] if ptrs is not None else getattr(self, k).ctypes.data)
         return s

@@ -1,0 +1,371 @@
+// dcr_capi.hip — C-ABI of libdcr.so (include/dcr.h): context, workspace,
+// launches and timing for the gfx950 kernels in dcr_kernels.hip.
+//
+// One context per GPU: its own HIP stream, device copy of the parameters, and
+// a grow-only workspace (reserve it once; the launch path never allocates,
+// so a caller may capture dcr_run_batch into a hipGraph).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/dcr.h"
+
+namespace dcr {
+struct Workspace {
+    dcr_read_info *info;
+    uint32_t *norm_cig;
+    int32_t *cons;
+    double *et;
+    uint8_t *insflag;
+    int4 *state;
+    int *err;
+};
+struct Args {
+    dcr_batch in;
+    const dcr_params *P;
+    Workspace ws;
+    dcr_out ss;
+    dcr_out ds;
+    int64_t n_rec;
+};
+__global__ void k_prep(dcr_batch in, const dcr_params *P, Workspace ws);
+template <bool DUPLEX> __global__ void k_consensus(Args a);
+}  // namespace dcr
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return fail(DCR_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, n ? n : 16);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+}  // namespace
+
+struct dcr_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    dcr_params *d_params = nullptr;
+    DevBuf ws;          // workspace
+    DevBuf io;          // staging for the host-pointer entry point
+    dcr::Workspace w{};
+    int64_t last_reads = 0;
+    bool timed = false;
+};
+
+extern "C" {
+
+int dcr_abi_version(void) { return DCR_ABI_VERSION; }
+
+const char *dcr_last_error(void) { return g_err.c_str(); }
+
+static int check_params(const dcr_params *p) {
+    if (!p) return fail(DCR_EARG, "params is NULL");
+    if (p->max_base_quality < 0 || p->max_base_quality > DCR_MAX_QTHRESH - 1)
+        return fail(DCR_EARG, "max_base_quality out of range [0, 256]");
+    if (p->n_qthresh != p->max_base_quality + 1)
+        return fail(DCR_EARG, "n_qthresh must equal max_base_quality + 1");
+    return DCR_OK;
+}
+
+dcr_ctx *dcr_create(int device, const dcr_params *params) {
+    if (check_params(params) != DCR_OK) return nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+        fail(DCR_ENODEV, "no HIP device " + std::to_string(device));
+        return nullptr;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess ||
+        std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        fail(DCR_ENODEV, std::string("device is not gfx950 (MI355X): ") + prop.gcnArchName);
+        return nullptr;
+    }
+    dcr_ctx *c = new dcr_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->d_params, sizeof(dcr_params)) != hipSuccess) {
+        fail(DCR_EHIP, "context allocation failed");
+        delete c;
+        return nullptr;
+    }
+    for (auto &e : c->ev) (void)hipEventCreate(&e);
+    if (hipMemcpy(c->d_params, params, sizeof(dcr_params), hipMemcpyHostToDevice) != hipSuccess) {
+        fail(DCR_EHIP, "params upload failed");
+        dcr_destroy(c);
+        return nullptr;
+    }
+    return c;
+}
+
+void dcr_destroy(dcr_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    c->ws.release();
+    c->io.release();
+    if (c->d_params) (void)hipFree(c->d_params);
+    for (auto &e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int dcr_set_params(dcr_ctx *c, const dcr_params *params) {
+    if (!c) return fail(DCR_EARG, "ctx is NULL");
+    int rc = check_params(params);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpyAsync(c->d_params, params, sizeof(dcr_params), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DCR_OK;
+}
+
+void *dcr_stream(dcr_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
+    if (!c || !s) return fail(DCR_EARG, "NULL argument");
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t cols = std::max(s->ss_cols, s->ds_cols);
+    size_t o = 0;
+    const size_t o_info = o; o = align_up(o + sizeof(dcr_read_info) * (size_t)std::max<int64_t>(s->n_reads, 1));
+    const size_t o_cig = o;  o = align_up(o + sizeof(uint32_t) * (size_t)std::max<int64_t>(s->n_cigar, 1));
+    const size_t o_cons = o; o = align_up(o + sizeof(int32_t) * (size_t)std::max<int64_t>(cols, 1));
+    const size_t o_et = o;   o = align_up(o + sizeof(double) * (size_t)std::max<int64_t>(cols, 1));
+    const size_t o_ins = o;  o = align_up(o + (size_t)std::max<int64_t>(s->ss_cols, 1));
+    const size_t o_st = o;   o = align_up(o + sizeof(int4) * (size_t)std::max<int64_t>(s->n_reads, 1));
+    const size_t o_err = o;  o = align_up(o + 16);
+    if (o > c->ws.cap) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(c->ws.ensure(o + o / 8));
+    }
+    char *b = (char *)c->ws.p;
+    c->w.info = (dcr_read_info *)(b + o_info);
+    c->w.norm_cig = (uint32_t *)(b + o_cig);
+    c->w.cons = (int32_t *)(b + o_cons);
+    c->w.et = (double *)(b + o_et);
+    c->w.insflag = (uint8_t *)(b + o_ins);
+    c->w.state = (int4 *)(b + o_st);
+    c->w.err = (int *)(b + o_err);
+    return DCR_OK;
+}
+
+int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
+    if (!c || !in || !ss || !ds) return fail(DCR_EARG, "NULL argument");
+    if (in->n_fam < 0 || in->n_reads < 0) return fail(DCR_EARG, "negative batch size");
+    int rc = dcr_reserve(c, in);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemsetAsync(c->w.err, 0, sizeof(int), c->stream));
+    c->last_reads = in->n_reads;
+    HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+    if (in->n_reads > 0) {
+        const int nb = (in->n_reads + 255) / 256;
+        dcr::Workspace w;
+        std::memcpy(&w, &c->w, sizeof(w));
+        hipLaunchKernelGGL(dcr::k_prep, dim3(nb), dim3(256), 0, c->stream, *in, c->d_params, w);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    dcr::Args a;
+    a.in = *in;
+    a.P = c->d_params;
+    std::memcpy(&a.ws, &c->w, sizeof(a.ws));
+    a.ss = *ss;
+    a.ds = *ds;
+    if (in->n_fam > 0) {
+        a.n_rec = 4LL * in->n_fam;
+        hipLaunchKernelGGL(dcr::k_consensus<false>, dim3((unsigned)((a.n_rec + 3) / 4)), dim3(256), 0,
+                           c->stream, a);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    if (in->n_fam > 0) {
+        a.n_rec = 2LL * in->n_fam;
+        hipLaunchKernelGGL(dcr::k_consensus<true>, dim3((unsigned)((a.n_rec + 3) / 4)), dim3(256), 0,
+                           c->stream, a);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+    c->timed = true;
+    return DCR_OK;
+}
+
+int dcr_sync(dcr_ctx *c) {
+    if (!c) return fail(DCR_EARG, "ctx is NULL");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->w.err) {
+        int err = 0;
+        HIP_TRY(hipMemcpy(&err, c->w.err, sizeof(int), hipMemcpyDeviceToHost));
+        if (err) return fail(DCR_ECAPACITY, "a consensus needed more columns than its output region");
+    }
+    return DCR_OK;
+}
+
+int dcr_last_timing(dcr_ctx *c, float *ms4) {
+    if (!c || !ms4) return fail(DCR_EARG, "NULL argument");
+    if (!c->timed) return fail(DCR_EARG, "no batch has run");
+    HIP_TRY(hipEventSynchronize(c->ev[3]));
+    HIP_TRY(hipEventElapsedTime(&ms4[0], c->ev[0], c->ev[1]));
+    HIP_TRY(hipEventElapsedTime(&ms4[1], c->ev[1], c->ev[2]));
+    HIP_TRY(hipEventElapsedTime(&ms4[2], c->ev[2], c->ev[3]));
+    HIP_TRY(hipEventElapsedTime(&ms4[3], c->ev[0], c->ev[3]));
+    return DCR_OK;
+}
+
+int dcr_read_info_host(dcr_ctx *c, dcr_read_info *out, int64_t n) {
+    if (!c || !out) return fail(DCR_EARG, "NULL argument");
+    if (n > c->last_reads) return fail(DCR_EARG, "more reads requested than the last batch held");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (n > 0) HIP_TRY(hipMemcpy(out, c->w.info, sizeof(dcr_read_info) * n, hipMemcpyDeviceToHost));
+    return DCR_OK;
+}
+
+// host-pointer entry point: one staging allocation, H2D, run, D2H
+int dcr_run_batch_host(dcr_ctx *c, const dcr_batch *h, dcr_out *hss, dcr_out *hds) {
+    if (!c || !h || !hss || !hds) return fail(DCR_EARG, "NULL argument");
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t F = h->n_fam, n = h->n_reads;
+    struct Piece { const void *src; void **dst_in; size_t bytes; };
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + std::max<size_t>(bytes, 1)); return o; };
+    // inputs
+    const size_t o_sub = take(sizeof(int32_t) * (4 * F + 1));
+    const size_t o_pos = take(sizeof(int32_t) * n);
+    const size_t o_mq = take(n);
+    const size_t o_so = take(sizeof(int64_t) * n);
+    const size_t o_sl = take(sizeof(int32_t) * n);
+    const size_t o_co = take(sizeof(int32_t) * n);
+    const size_t o_cn = take(sizeof(int32_t) * n);
+    const size_t o_cg = take(sizeof(uint32_t) * h->n_cigar);
+    const size_t o_b = take(h->n_bases);
+    const size_t o_q = take(h->n_bases);
+    const size_t o_sc = take(sizeof(int64_t) * (4 * F + 1));
+    const size_t o_dc = take(sizeof(int64_t) * (2 * F + 1));
+    // outputs
+    size_t oo[2][14];
+    const int64_t nrec[2] = {4 * F, 2 * F};
+    const int64_t ncol[2] = {h->ss_cols, h->ds_cols};
+    for (int k = 0; k < 2; ++k) {
+        oo[k][0] = take(nrec[k]);
+        for (int j = 1; j <= 7; ++j) oo[k][j] = take(sizeof(int32_t) * nrec[k]);
+        oo[k][8] = take(sizeof(double) * nrec[k]);
+        oo[k][9] = take(ncol[k]);
+        oo[k][10] = take(ncol[k]);
+        oo[k][11] = take(sizeof(uint32_t) * ncol[k]);
+        oo[k][12] = take(sizeof(uint16_t) * ncol[k]);
+        oo[k][13] = take(sizeof(uint16_t) * ncol[k]);
+    }
+    if (off > c->io.cap) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(c->io.ensure(off));
+    }
+    char *d = (char *)c->io.p;
+    dcr_batch db = *h;
+    auto up = [&](size_t o, const void *src, size_t bytes) -> hipError_t {
+        if (!bytes) return hipSuccess;
+        return hipMemcpyAsync(d + o, src, bytes, hipMemcpyHostToDevice, c->stream);
+    };
+    HIP_TRY(up(o_sub, h->sub_off, sizeof(int32_t) * (4 * F + 1)));
+    HIP_TRY(up(o_pos, h->read_pos, sizeof(int32_t) * n));
+    HIP_TRY(up(o_mq, h->read_mapq, n));
+    HIP_TRY(up(o_so, h->seq_off, sizeof(int64_t) * n));
+    HIP_TRY(up(o_sl, h->seq_len, sizeof(int32_t) * n));
+    HIP_TRY(up(o_co, h->cig_off, sizeof(int32_t) * n));
+    HIP_TRY(up(o_cn, h->cig_n, sizeof(int32_t) * n));
+    HIP_TRY(up(o_cg, h->cigar, sizeof(uint32_t) * h->n_cigar));
+    HIP_TRY(up(o_b, h->bases, h->n_bases));
+    HIP_TRY(up(o_q, h->quals, h->n_bases));
+    HIP_TRY(up(o_sc, h->ss_col_off, sizeof(int64_t) * (4 * F + 1)));
+    HIP_TRY(up(o_dc, h->ds_col_off, sizeof(int64_t) * (2 * F + 1)));
+    db.sub_off = (const int32_t *)(d + o_sub);
+    db.read_pos = (const int32_t *)(d + o_pos);
+    db.read_mapq = (const uint8_t *)(d + o_mq);
+    db.seq_off = (const int64_t *)(d + o_so);
+    db.seq_len = (const int32_t *)(d + o_sl);
+    db.cig_off = (const int32_t *)(d + o_co);
+    db.cig_n = (const int32_t *)(d + o_cn);
+    db.cigar = (const uint32_t *)(d + o_cg);
+    db.bases = (const uint8_t *)(d + o_b);
+    db.quals = (const uint8_t *)(d + o_q);
+    db.ss_col_off = (const int64_t *)(d + o_sc);
+    db.ds_col_off = (const int64_t *)(d + o_dc);
+    dcr_out dout[2];
+    for (int k = 0; k < 2; ++k) {
+        dout[k].status = (uint8_t *)(d + oo[k][0]);
+        dout[k].pos = (int32_t *)(d + oo[k][1]);
+        dout[k].mapq = (int32_t *)(d + oo[k][2]);
+        dout[k].len = (int32_t *)(d + oo[k][3]);
+        dout[k].n_cig = (int32_t *)(d + oo[k][4]);
+        dout[k].n_de = (int32_t *)(d + oo[k][5]);
+        dout[k].D = (int32_t *)(d + oo[k][6]);
+        dout[k].M = (int32_t *)(d + oo[k][7]);
+        dout[k].E = (double *)(d + oo[k][8]);
+        dout[k].seq = (uint8_t *)(d + oo[k][9]);
+        dout[k].qual = (uint8_t *)(d + oo[k][10]);
+        dout[k].cigar = (uint32_t *)(d + oo[k][11]);
+        dout[k].d = (uint16_t *)(d + oo[k][12]);
+        dout[k].e = (uint16_t *)(d + oo[k][13]);
+    }
+    int rc = dcr_run_batch(c, &db, &dout[0], &dout[1]);
+    if (rc) return rc;
+    dcr_out *hh[2] = {hss, hds};
+    for (int k = 0; k < 2; ++k) {
+        auto dn = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
+            if (!bytes || !dst) return hipSuccess;
+            return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream);
+        };
+        const size_t R = nrec[k], C = ncol[k];
+        HIP_TRY(dn(hh[k]->status, dout[k].status, R));
+        HIP_TRY(dn(hh[k]->pos, dout[k].pos, 4 * R));
+        HIP_TRY(dn(hh[k]->mapq, dout[k].mapq, 4 * R));
+        HIP_TRY(dn(hh[k]->len, dout[k].len, 4 * R));
+        HIP_TRY(dn(hh[k]->n_cig, dout[k].n_cig, 4 * R));
+        HIP_TRY(dn(hh[k]->n_de, dout[k].n_de, 4 * R));
+        HIP_TRY(dn(hh[k]->D, dout[k].D, 4 * R));
+        HIP_TRY(dn(hh[k]->M, dout[k].M, 4 * R));
+        HIP_TRY(dn(hh[k]->E, dout[k].E, 8 * R));
+        HIP_TRY(dn(hh[k]->seq, dout[k].seq, C));
+        HIP_TRY(dn(hh[k]->qual, dout[k].qual, C));
+        HIP_TRY(dn(hh[k]->cigar, dout[k].cigar, 4 * C));
+        HIP_TRY(dn(hh[k]->d, dout[k].d, 2 * C));
+        HIP_TRY(dn(hh[k]->e, dout[k].e, 2 * C));
+    }
+    return dcr_sync(c);
+}
+
+}  // extern "C"

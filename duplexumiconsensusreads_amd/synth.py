@@ -168,3 +168,83 @@ def write_config_bam(path, cfg: SynthConfig, n_families=None, seed=None):
             for r in family_records(rng, cfg, f, locus=locus):
                 out.write(r)
     return path
+
+
+def split_records(recs):
+    """Four subfamilies in A1, B2, B1, A2 order (split_family :132-154)."""
+    out = [[], [], [], []]
+    for r in recs:
+        if not r.is_reverse and r.is_read1:
+            out[0].append(r)
+        elif not r.is_reverse and r.is_read2:
+            out[1].append(r)
+        elif r.is_reverse and r.is_read1:
+            out[2].append(r)
+        elif r.is_reverse and r.is_read2:
+            out[3].append(r)
+    return out
+
+
+def family_splits(cfg: SynthConfig, n_families=None, seed=None):
+    rng = np.random.default_rng(cfg.seed if seed is None else seed)
+    n = cfg.n_families if n_families is None else n_families
+    fams = []
+    for f in range(n):
+        locus = 1_000_000 + 10_000 * (f % cfg.n_loci) if cfg.n_loci else None
+        fams.append(split_records(family_records(rng, cfg, f, locus=locus)))
+    return fams
+
+
+def packed_from_records(cfg: SynthConfig, n_families=None, seed=None):
+    """Packed batch through the record generator (any config, moderate sizes)."""
+    from .batch import pack_families
+    return pack_families(family_splits(cfg, n_families, seed))
+
+
+_QLUT = np.array([37] * 80 + [25] * 12 + [12] * 8, dtype=np.uint8)
+_ERR_P16 = {37: int(round(10 ** -3.7 * 65536)), 25: int(round(10 ** -2.5 * 65536)),
+            12: int(round(10 ** -1.2 * 65536))}
+
+
+def packed_fixed_size(n_families, sub_size=8, read_len=150, seed=2, chunk_reads=1 << 20):
+    """Vectorised config-2 generator: uniform subfamily size, ``150M`` reads,
+    no indels.  Same base/quality model as family_records."""
+    from .batch import finish_batch
+    rng = np.random.default_rng(seed)
+    F, L, k = n_families, read_len, sub_size
+    n = F * 4 * k
+    ins = np.clip(rng.normal(300, 30, F), 200, 500).astype(np.int64)
+    P = rng.integers(1000, 100_000_000, F).astype(np.int64)
+    fam = np.repeat(np.arange(F), 4 * k)
+    sub = np.tile(np.repeat(np.arange(4), k), F)
+    rev = sub >= 2
+    start = np.where(rev, ins[fam] - L, 0)
+    read_pos = (P[fam] + start).astype(np.int32)
+    tw = int(ins.max()) + 20
+    bases = np.empty(n * L, np.uint8)
+    quals = np.empty(n * L, np.uint8)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    fam_chunk = max(1, chunk_reads // (4 * k))
+    for f0 in range(0, F, fam_chunk):
+        f1 = min(F, f0 + fam_chunk)
+        tmpl = acgt[rng.integers(0, 4, (f1 - f0, tw), dtype=np.uint8)]
+        r0, r1 = f0 * 4 * k, f1 * 4 * k
+        idx = start[r0:r1, None] + np.arange(L)[None, :]
+        seq = tmpl[(fam[r0:r1] - f0)[:, None], idx]
+        q = _QLUT[rng.integers(0, 100, (r1 - r0, L), dtype=np.uint8)]
+        u = rng.integers(0, 65536, (r1 - r0, L), dtype=np.uint16)
+        thr = np.where(q == 37, _ERR_P16[37], np.where(q == 25, _ERR_P16[25], _ERR_P16[12]))
+        err = u < thr
+        if err.any():
+            code = np.searchsorted(acgt, seq[err])
+            seq[err] = acgt[(code + rng.integers(1, 4, err.sum())) % 4]
+        bases[r0 * L:r1 * L] = seq.reshape(-1)
+        quals[r0 * L:r1 * L] = q.reshape(-1)
+    sub_off = np.arange(0, n + 1, k, dtype=np.int32)
+    mapq = rng.integers(20, 61, n).astype(np.uint8)
+    seq_off = np.arange(n, dtype=np.int64) * L
+    seq_len = np.full(n, L, np.int32)
+    cig_off = np.arange(n, dtype=np.int32)
+    cig_n = np.ones(n, np.int32)
+    cigar = np.full(n, (L << 4) | 0, np.uint32)
+    return finish_batch(sub_off, read_pos, mapq, seq_off, seq_len, cig_off, cig_n, cigar, bases, quals)

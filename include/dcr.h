@@ -89,6 +89,10 @@ typedef struct dcr_params {
 typedef struct dcr_batch {
     int32_t n_fam;
     int32_t n_reads;
+    int64_t n_cigar;            /* entries of cigar                              */
+    int64_t n_bases;            /* entries of bases / quals                      */
+    int64_t ss_cols;            /* ss_col_off[4F]                                */
+    int64_t ds_cols;            /* ds_col_off[2F]                                */
     const int32_t *sub_off;     /* [4F+1] first read of each subfamily          */
     const int32_t *read_pos;    /* [n_reads] reference_start (0-based)          */
     const uint8_t *read_mapq;   /* [n_reads] mapping_quality                    */
@@ -143,15 +147,13 @@ dcr_ctx *dcr_create(int device, const dcr_params *params);
 void dcr_destroy(dcr_ctx *ctx);
 int dcr_set_params(dcr_ctx *ctx, const dcr_params *params);
 /* pre-size internal scratch so a timed loop never allocates */
-int dcr_reserve(dcr_ctx *ctx, int64_t n_reads, int64_t n_cigar, int64_t n_fam,
-                int64_t ss_cols, int64_t ds_cols);
+int dcr_reserve(dcr_ctx *ctx, const dcr_batch *sizes);
 void *dcr_stream(dcr_ctx *ctx);   /* the context's hipStream_t */
 
 /* device-pointer batch: asynchronous on the context stream */
-int dcr_run_batch(dcr_ctx *ctx, const dcr_batch *in, int64_t n_cigar, dcr_out *ss, dcr_out *ds);
+int dcr_run_batch(dcr_ctx *ctx, const dcr_batch *in, dcr_out *ss, dcr_out *ds);
 /* host-pointer batch: stages H2D, runs, D2H; synchronous */
-int dcr_run_batch_host(dcr_ctx *ctx, const dcr_batch *in, int64_t n_cigar, int64_t n_bases,
-                       dcr_out *ss, dcr_out *ds);
+int dcr_run_batch_host(dcr_ctx *ctx, const dcr_batch *in, dcr_out *ss, dcr_out *ds);
 int dcr_sync(dcr_ctx *ctx);
 /* copy the last batch's per-read preprocessing info (host pointer, n_reads) */
 int dcr_read_info_host(dcr_ctx *ctx, dcr_read_info *out, int64_t n_reads);
@@ -161,8 +163,8 @@ int dcr_last_timing(dcr_ctx *ctx, float *ms4);
 
 /* CPU restatement with the same contract (oracle/, test infrastructure):
    host pointers, single thread (or n_threads > 1) */
-int dcr_oracle_run(const dcr_params *params, const dcr_batch *in, int64_t n_cigar,
-                   dcr_out *ss, dcr_out *ds, dcr_read_info *info, int n_threads);
+int dcr_oracle_run(const dcr_params *params, const dcr_batch *in, dcr_out *ss, dcr_out *ds,
+                   dcr_read_info *info, int n_threads);
 
 #ifdef __cplusplus
 }

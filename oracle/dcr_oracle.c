@@ -386,9 +386,8 @@ static void *worker(void *arg) {
     return NULL;
 }
 
-int dcr_oracle_run(const dcr_params *P, const dcr_batch *in, int64_t n_cigar, dcr_out *ss,
-                   dcr_out *ds, dcr_read_info *info, int n_threads) {
-    (void)n_cigar;
+int dcr_oracle_run(const dcr_params *P, const dcr_batch *in, dcr_out *ss, dcr_out *ds,
+                   dcr_read_info *info, int n_threads) {
     if (!P || !in || !ss || !ds) return DCR_EARG;
     if (n_threads <= 1 || in->n_fam < 2 * n_threads) {
         for (int f = 0; f < in->n_fam; ++f) run_family(P, in, ss, ds, info, f);

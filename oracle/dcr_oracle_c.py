@@ -28,8 +28,8 @@ def load():
             build()
         _lib = ctypes.CDLL(LIB)
         _lib.dcr_oracle_run.restype = ctypes.c_int
-        _lib.dcr_oracle_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
-                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        _lib.dcr_oracle_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     return _lib
 
 
@@ -46,7 +46,7 @@ def run(packed, params, n_threads=1, want_info=True):
     info = (DcrReadInfo * max(packed.n_reads, 1))()
     b = packed.as_struct()
     so, do = ss.as_struct(), ds.as_struct()
-    rc = lib.dcr_oracle_run(ctypes.byref(P), ctypes.byref(b), packed.n_cigar, ctypes.byref(so),
+    rc = lib.dcr_oracle_run(ctypes.byref(P), ctypes.byref(b), ctypes.byref(so),
                             ctypes.byref(do), ctypes.cast(info, ctypes.c_void_p), n_threads)
     if rc != 0:
         raise RuntimeError(f"dcr_oracle_run failed: {rc}")

@@ -1,0 +1,66 @@
+"""CPU-side checks of the drop-in boundary: libdcr.so (built for gfx950)
+loads and exports every function include/dcr.h declares; the ctypes mirrors
+match the header's struct layouts.  No compute calls (no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dcr.h")
+LIB = os.path.join(ROOT, "duplexumiconsensusreads_amd", "libdcr.so")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = re.findall(r"^[A-Za-z_][\w\s\*]*?\b(dcr_\w+)\s*\(", txt, flags=re.M)
+    return sorted(set(names))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        import __graft_entry__
+        __graft_entry__.build()
+    return ctypes.CDLL(LIB)
+
+
+def test_library_exports_every_header_function(lib):
+    names = header_functions()
+    assert "dcr_run_batch" in names and "dcr_create" in names
+    for n in names:
+        if n == "dcr_oracle_run":
+            continue  # implemented by the oracle library (test infrastructure)
+        assert hasattr(lib, n), n
+    assert lib.dcr_abi_version() == 1
+
+
+def test_oracle_library_exports_oracle_entry():
+    from oracle import dcr_oracle_c
+    assert hasattr(dcr_oracle_c.load(), "dcr_oracle_run")
+
+
+def test_library_is_gfx950_code_object():
+    data = open(LIB, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data      # offload bundle target id
+
+
+def _c_sizeof(expr):
+    src = f'#include "{HEADER}"\n#include <stdio.h>\n#include <stddef.h>\nint main(void){{printf("%zu\\n", (size_t)({expr}));return 0;}}\n'
+    exe = "/tmp/_dcr_sizeof"
+    subprocess.run(["gcc", "-x", "c", "-", "-o", exe], input=src, text=True, check=True)
+    return int(subprocess.run([exe], capture_output=True, text=True, check=True).stdout)
+
+
+def test_ctypes_layouts_match_header():
+    from duplexumiconsensusreads_amd.batch import DcrBatch, DcrOut, DcrReadInfo
+    from duplexumiconsensusreads_amd.params import DcrParams
+    assert ctypes.sizeof(DcrParams) == _c_sizeof("sizeof(dcr_params)")
+    assert ctypes.sizeof(DcrBatch) == _c_sizeof("sizeof(dcr_batch)")
+    assert ctypes.sizeof(DcrOut) == _c_sizeof("sizeof(dcr_out)")
+    assert ctypes.sizeof(DcrReadInfo) == _c_sizeof("sizeof(dcr_read_info)")
+    assert DcrParams.qthresh.offset == _c_sizeof("offsetof(dcr_params, qthresh)")
+    assert DcrBatch.sub_off.offset == _c_sizeof("offsetof(dcr_batch, sub_off)")
