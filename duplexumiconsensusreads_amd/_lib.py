@@ -15,7 +15,7 @@ from .batch import DcrBatch, DcrOut, DcrReadInfo, OutArrays, PackedBatch
 from .params import ConsensusParams, DcrParams, build_dcr_params
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdcr.so")
+LIB_PATH = os.environ.get("DCR_LIB", os.path.join(HERE, "libdcr.so"))
 
 EXPORTS = {
     "dcr_abi_version": (ctypes.c_int, []),

@@ -22,6 +22,8 @@ struct Workspace {
     uint8_t *insflag;
     int4 *state;
     int *err;
+    int *ovf;
+    int *ovf_count;
 };
 struct Args {
     dcr_batch in;
@@ -30,9 +32,11 @@ struct Args {
     dcr_out ss;
     dcr_out ds;
     int64_t n_rec;
+    int fast_ok;
 };
 __global__ void k_prep(dcr_batch in, const dcr_params *P, Workspace ws);
-template <bool DUPLEX> __global__ void k_consensus(Args a);
+template <bool DUPLEX> __global__ void k_consensus_fast(Args a);
+template <bool DUPLEX> __global__ void k_consensus_general(Args a);
 }  // namespace dcr
 
 namespace {
@@ -82,7 +86,15 @@ struct dcr_ctx {
     dcr::Workspace w{};
     int64_t last_reads = 0;
     bool timed = false;
+    int fast_ok = 0;    // all likelihood factors in [0, 1]: the fast kernel's finalize applies
 };
+
+static int factors_unit(const dcr_params *p) {
+    for (int i = 0; i < DCR_LUT_N; ++i)
+        if (!(p->match[i] >= 0.0 && p->match[i] <= 1.0 && p->mismatch[i] >= 0.0 && p->mismatch[i] <= 1.0))
+            return 0;
+    return 1;
+}
 
 extern "C" {
 
@@ -122,6 +134,7 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
         return nullptr;
     }
     for (auto &e : c->ev) (void)hipEventCreate(&e);
+    c->fast_ok = factors_unit(params);
     if (hipMemcpy(c->d_params, params, sizeof(dcr_params), hipMemcpyHostToDevice) != hipSuccess) {
         fail(DCR_EHIP, "params upload failed");
         dcr_destroy(c);
@@ -150,6 +163,7 @@ int dcr_set_params(dcr_ctx *c, const dcr_params *params) {
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemcpyAsync(c->d_params, params, sizeof(dcr_params), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    c->fast_ok = factors_unit(params);
     return DCR_OK;
 }
 
@@ -167,6 +181,7 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     const size_t o_ins = o;  o = align_up(o + (size_t)std::max<int64_t>(s->ss_cols, 1));
     const size_t o_st = o;   o = align_up(o + sizeof(int4) * (size_t)std::max<int64_t>(s->n_reads, 1));
     const size_t o_err = o;  o = align_up(o + 16);
+    const size_t o_ovf = o;  o = align_up(o + sizeof(int) * (size_t)std::max<int64_t>(4LL * s->n_fam, 1));
     if (o > c->ws.cap) {
         HIP_TRY(hipStreamSynchronize(c->stream));
         HIP_TRY(c->ws.ensure(o + o / 8));
@@ -179,6 +194,8 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     c->w.insflag = (uint8_t *)(b + o_ins);
     c->w.state = (int4 *)(b + o_st);
     c->w.err = (int *)(b + o_err);
+    c->w.ovf_count = (int *)(b + o_err) + 1;     // err, ovf_count[2] share one 16-byte block
+    c->w.ovf = (int *)(b + o_ovf);
     return DCR_OK;
 }
 
@@ -188,7 +205,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     int rc = dcr_reserve(c, in);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMemsetAsync(c->w.err, 0, sizeof(int), c->stream));
+    HIP_TRY(hipMemsetAsync(c->w.err, 0, 16, c->stream));
     c->last_reads = in->n_reads;
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     if (in->n_reads > 0) {
@@ -205,17 +222,25 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     std::memcpy(&a.ws, &c->w, sizeof(a.ws));
     a.ss = *ss;
     a.ds = *ds;
+    a.fast_ok = c->fast_ok;
+    // fast kernel over every record, then the persistent general kernel over
+    // the records it handed over (insertions, > 64 reads, wide layouts)
+    auto general_grid = [](int64_t n_rec) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_rec + 3) / 4, 1024)); };
     if (in->n_fam > 0) {
         a.n_rec = 4LL * in->n_fam;
-        hipLaunchKernelGGL(dcr::k_consensus<false>, dim3((unsigned)((a.n_rec + 3) / 4)), dim3(256), 0,
+        hipLaunchKernelGGL(dcr::k_consensus_fast<false>, dim3((unsigned)((a.n_rec + 3) / 4)), dim3(256), 0,
                            c->stream, a);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(dcr::k_consensus_general<false>, dim3(general_grid(a.n_rec)), dim3(256), 0, c->stream, a);
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     if (in->n_fam > 0) {
         a.n_rec = 2LL * in->n_fam;
-        hipLaunchKernelGGL(dcr::k_consensus<true>, dim3((unsigned)((a.n_rec + 3) / 4)), dim3(256), 0,
+        hipLaunchKernelGGL(dcr::k_consensus_fast<true>, dim3((unsigned)((a.n_rec + 3) / 4)), dim3(256), 0,
                            c->stream, a);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(dcr::k_consensus_general<true>, dim3(general_grid(a.n_rec)), dim3(256), 0, c->stream, a);
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));

@@ -6,6 +6,8 @@
 //                (:191-325) -> kept sequence window + normalised M/I/D runs.
 //   k_consensus  one wavefront per consensus record (single-strand: one
 //                subfamily; duplex: one A1+B2 / B1+A2 pair).  Phases:
+//                  0. stage the record's bases/quals from HBM into LDS as
+//                     16-bit element codes (wide coalesced loads, one trip)
 //                  1. column layout of reconstruct_alignment (:430-547)
 //                  2. per-column likelihood products in read order + posterior,
 //                     masking and output quality (:550-712)
@@ -13,28 +15,35 @@
 //                     depth/errors and their pairwise mean (:970-1021), MAPQ
 //                     (:874-889).
 // All arithmetic is IEEE binary64 in the reference's operation order; build
-// with -ffp-contract=off (no FMA contraction).  No transcendental is
-// evaluated on device: p', thresholds and the phred rounding boundaries are
-// host tables (params.py).
+// with -ffp-contract=off (no FMA contraction).  No transcendental runs on the
+// device: p', thresholds and phred rounding boundaries are host tables.
 //
-// Data flow per wave (lane = column for phase 2/3; lane = read for setup and
-// for the insertion-aware layout of phase 1):
-//   fast layout  (no I op in the record): element (r, t) is computed directly
-//                from the read's M/D runs — no per-column simulation;
-//   ins layout   (some read has an I op): the reference's column loop is run
-//                with lane = read and a wave ballot per column deciding
-//                insertion columns (:476-478), materialising a 64x64 tile of
-//                (class, LUT row) codes in LDS that phase 2 consumes by column.
+// Likelihood "slots" (phase 2).  The reference keeps six products per column
+// (:590-600).  Every class that has not yet appeared in the column receives
+// the same factor p'/5 from every read, so all unseen classes hold the SAME
+// double — one chain U.  A class seen for the first time at read r starts
+// from U (its value so far, bit for bit) times (1 - p').  So a lane keeps U
+// plus one chain per distinct class actually observed, and the wave pays only
+// for the largest number of distinct classes among its 64 columns (usually
+// one or two) instead of six.  Results are bit-identical to the six chains.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/dcr.h"
+
+#ifndef DCR_ABL
+#define DCR_ABL 0   // diagnostic builds only (tools/ablate.py): 1 setup, 2 +accumulate, 3 +finalize
+#endif
 
 namespace dcr {
 
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
+constexpr int kStageElems = 2048;        // per-wave LDS staging (16-bit codes)
+constexpr int kTileIns = 32;             // column tile of the insertion layout
+constexpr int kFastMaxT = 240;           // pairwise_small: both halves <= 128
+constexpr int kColsLds = 256;            // per-wave LDS column scratch
 
 // element code: bits 0..8 LUT row (quality 0..255, 256 '+', 257 '-'), bits 9..11 class
 // class: 0 A, 1 T, 2 C, 3 G, 4 '+', 5 '-', 6 N/n, 7 invalid character (:580-591)
@@ -45,11 +54,13 @@ constexpr uint32_t kDel = (5u << 9) | DCR_LUT_DEL;
 struct Workspace {
     dcr_read_info *info;    // [n_reads]
     uint32_t *norm_cig;     // [n_cigar] normalised runs (M/I/D)
-    int32_t *cons;          // [cols] consensus char | quality << 8 (pre-layout)
-    double *et;             // [cols] e/d per kept column
+    int32_t *cons;          // [cols] consensus char | quality << 8 (T > kColsLds)
+    double *et;             // [cols] e/d per kept column        (T > kColsLds)
     uint8_t *insflag;       // [ss cols] insertion-column flags (R > 64 layout)
     int4 *state;            // [n_reads] layout state (R > 64)
     int *err;               // [1] capacity error flag
+    int *ovf;               // [n_rec] records the fast kernel hands to the general one
+    int *ovf_count;         // [2] single-strand / duplex overflow counts
 };
 
 struct Args {
@@ -59,33 +70,61 @@ struct Args {
     dcr_out ss;
     dcr_out ds;
     int64_t n_rec;
+    int fast_ok;            // every LUT factor in [0, 1] (host-checked): fast kernel allowed
 };
 
-__device__ __forceinline__ uint32_t base_class(uint8_t b) {
-    switch (b) {
-    case 'A': return 0;
-    case 'T': return 1;
-    case 'C': return 2;
-    case 'G': return 3;
-    case 'N': return 6;
-    default: return 7;
-    }
+struct WaveLds {
+    uint16_t pad_code[4];                  // [0] = kPad: sentinel the fast layout loads outside a read (8 B keeps stage 8-aligned)
+    union {
+        uint16_t stage[kStageElems];       // fast layout: element codes of the record's bytes
+        uint16_t tile[kWave][kTileIns];    // insertion layout: 64 reads x 32 columns
+    };
+    int32_t cons[kColsLds];
+    double et[kColsLds];
+    // uniform stack of the pairwise-sum walk (phase 3)
+    int stk_off[24], stk_n[24], stk_stage[24];
+    double stk_left[24];
+};
+
+// class of an input base (A/T/C/G/N; anything else is invalid, :580-585)
+__device__ __forceinline__ uint32_t base_class(uint32_t b) {
+    // 4-bit class per letter 'A'..'Z' packed in two 64-bit words; 7 = invalid
+    constexpr uint64_t lo = 0x7777777777777777ull & ~(0xfull << 0) & ~(0xfull << 8) & ~(0xfull << 24)
+                            & ~(0xfull << 52);
+    // letters: A=0 ('A'-'A'=0), C=2, G=6, N=13, T=19
+    const uint64_t tab_lo = (lo | (0ull << 0) | (2ull << 8) | (3ull << 24) | (6ull << 52));
+    constexpr uint64_t tab_hi = (0x7777777777777777ull & ~(0xfull << 12)) | (1ull << 12);
+    const uint32_t i = b - 'A';
+    if (i >= 32u) return 7;
+    const uint64_t t = i < 16 ? tab_lo : tab_hi;
+    return (uint32_t)(t >> ((i & 15) * 4)) & 15u;
 }
 
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
 
+// wave64 reductions on the VALU with DPP (quad_perm, half-row and row mirrors,
+// row_bcast15/31; gfx9 encodings), result read from lane 63 into an SGPR —
+// no LDS round trips (a ds_bpermute butterfly costs 6 dependent LDS latencies)
+template <class F>
+__device__ __forceinline__ int wave_reduce(int v, int ident, F op) {
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x140, 0xF, 0xF, false));  // row_mirror
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
 __device__ __forceinline__ int wave_min(int v) {
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
-    return v;
+    return wave_reduce(v, 0x7fffffff, [](int x, int y) { return min(x, y); });
 }
 __device__ __forceinline__ int wave_max(int v) {
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
-    return v;
+    return wave_reduce(v, -0x7fffffff - 1, [](int x, int y) { return max(x, y); });
 }
-__device__ __forceinline__ long long wave_sum(long long v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+__device__ __forceinline__ int wave_sum(int v) {
+    return wave_reduce(v, 0, [](int x, int y) { return x + y; });
 }
+__device__ __forceinline__ int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
 // wave-local ordering of global/LDS traffic between phases of one wavefront
 __device__ __forceinline__ void wave_fence() {
@@ -96,8 +135,8 @@ __device__ __forceinline__ void wave_fence() {
 // ------------------------------------------------------------------ k_prep
 // remove_clipping (:191-265): drop H; drop S with its bases (5'/3' ends);
 // mask_low_quality_bases (:268-289): base -> 'N' if qual < min_base_quality
-// (applied lazily by the consumer); trim_3prime_N (:292-325): drop trailing
-// 'N' and cut as many entries from the END of the expanded CIGAR.
+// (applied by the consumer); trim_3prime_N (:292-325): drop trailing 'N' and
+// cut as many entries from the END of the expanded CIGAR.
 __global__ __launch_bounds__(256) void k_prep(dcr_batch in, const dcr_params *P, Workspace ws) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= in.n_reads) return;
@@ -174,6 +213,7 @@ struct ReadRef {
     int pos, len, ncig, mapq, status;
     const uint32_t *cig;
     const uint8_t *seq, *qual;
+    int64_t seq_start;     // offset of the first kept base in its byte array
 };
 
 template <bool DUPLEX>
@@ -188,6 +228,7 @@ __device__ __forceinline__ ReadRef get_read(const Args &a, int64_t rec, int r) {
         rd.mapq = a.in.read_mapq[gr];
         rd.status = inf.status;
         rd.cig = a.ws.norm_cig + a.in.cig_off[gr];
+        rd.seq_start = inf.seq_start;
         rd.seq = a.in.bases + inf.seq_start;
         rd.qual = a.in.quals + inf.seq_start;
     } else {
@@ -200,21 +241,25 @@ __device__ __forceinline__ ReadRef get_read(const Args &a, int64_t rec, int r) {
         rd.mapq = a.ss.mapq[s];
         rd.status = a.ss.status[s];
         rd.cig = a.ss.cigar + off;
+        rd.seq_start = off;
         rd.seq = a.ss.seq + off;
         rd.qual = a.ss.qual + off;
     }
     return rd;
 }
 
-// element of read rd at seq index is (M op): class + LUT row; masking only
-// for single-strand input reads (mask_low_quality_bases :280)
+// element code of a base with its quality; masking only for single-strand
+// input reads (mask_low_quality_bases :280)
 template <bool DUPLEX>
-__device__ __forceinline__ uint32_t base_elem(const ReadRef &rd, int is, int minbq) {
-    const uint32_t b = rd.seq[is];
-    const uint32_t q = rd.qual[is];
-    uint32_t cls = base_class((uint8_t)b);
+__device__ __forceinline__ uint32_t make_code(uint32_t b, uint32_t q, int minbq) {
+    uint32_t cls = base_class(b);
     if (!DUPLEX && (int)q < minbq) cls = 6;
     return (cls << 9) | q;
+}
+
+template <bool DUPLEX>
+__device__ __forceinline__ uint32_t base_elem(const ReadRef &rd, int is, int minbq) {
+    return make_code<DUPLEX>(rd.seq[is], rd.qual[is], minbq);
 }
 
 // ------------------------------------------------ reconstruct_alignment state
@@ -272,71 +317,120 @@ __device__ __forceinline__ uint32_t sim_step(Sim &s, const ReadRef &rd, int p, b
     return e;
 }
 
-// element (r, t) of a record without insertion columns: the read's op index
-// at column t is j = t - (pos - min_pos); its seq index is the number of M
-// ops before j.  Once that reaches len the read pads (:514, :540).
-template <bool DUPLEX>
-__device__ __forceinline__ uint32_t direct_elem(const ReadRef &rd, int j, int minbq) {
-    if (j < 0) return kPad;
-    int is;
-    int op;
-    if (rd.ncig == 1) {
-        op = rd.cig[0] & 15;
-        is = j;
-        if (j >= (int)(rd.cig[0] >> 4)) return kPad;
-    } else {
-        int acc = 0, accis = 0;
-        op = -1;
-        is = 0;
-        for (int k = 0; k < rd.ncig; ++k) {
-            const uint32_t v = rd.cig[k];
-            const int ln = v >> 4, o = v & 15;
-            if (op < 0 && j < acc + ln) {
-                op = o;
-                is = accis + (o == 0 ? j - acc : 0);
-            }
-            acc += ln;
-            if (o == 0) accis += ln;
+// position of op index j of a read without I ops: (op, seq index), or pad.
+// The seq index is the number of M ops before j; once it reaches len the
+// read pads for good (:514, :540).
+__device__ __forceinline__ bool walk_runs(const uint32_t *cig, int ncig, int j, int len, int &is, bool &del) {
+    int acc = 0, accis = 0;
+    int op = -1;
+    is = 0;
+    for (int k = 0; k < ncig; ++k) {
+        const uint32_t v = cig[k];
+        const int ln = v >> 4, o = v & 15;
+        if (op < 0 && j < acc + ln) {
+            op = o;
+            is = accis + (o == 0 ? j - acc : 0);
         }
-        if (op < 0) return kPad;
-        if (op == 2 && accis == 0) { /* deletion before any base: is = 0 */ }
+        acc += ln;
+        if (o == 0) accis += ln;
     }
-    if (is >= rd.len) return kPad;
-    if (op == 2) return kDel;
-    return base_elem<DUPLEX>(rd, is, minbq);
+    if (op < 0 || is >= len) return false;
+    del = op == 2;
+    return true;
 }
 
 // --------------------------------------------------------------- phase 2
+// Likelihood slots (see header): U = the chain shared by all unseen classes,
+// s[j] = chain of the j-th distinct class seen in the column, k[j] its class,
+// n[j] its row count.
 struct Acc {
-    double L0, L1, L2, L3, L4, L5;
-    int c0, c1, c2, c3, c4, c5, c6;
-    int bad;
+    double U;
+    double s[6];
+    int k[6];
+    int n[6];
+    int ns;                    // slots used by this lane
+    int nbad;                  // rows with an invalid character
 };
 
 __device__ __forceinline__ void acc_init(Acc &A) {
-    A.L0 = A.L1 = A.L2 = A.L3 = A.L4 = A.L5 = 1.0;
-    A.c0 = A.c1 = A.c2 = A.c3 = A.c4 = A.c5 = A.c6 = 0;
-    A.bad = 0;
+    A.U = 1.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        A.s[j] = 1.0;
+        A.k[j] = -1;
+        A.n[j] = 0;
+    }
+    A.ns = 0;
+    A.nbad = 0;
 }
 
-// most_likely_nucleotide (:594-600): likelihoods multiplied in read order
-__device__ __forceinline__ void acc_add(Acc &A, uint32_t e, const double2 *lut) {
+// first sighting of class cls in this lane's column: L_cls == U until now
+__device__ __forceinline__ void acc_new_class(Acc &A, bool isnew, uint32_t cls, double Uold, double fmatch) {
+    if (!isnew) return;
+    if (cls == 7) {
+        A.nbad += 1;
+        return;
+    }
+    const double v = Uold * fmatch;
+    const int j = A.ns;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        if (i == j) {
+            A.s[i] = v;
+            A.k[i] = (int)cls;
+            A.n[i] = 1;
+        }
+    }
+    A.ns = j + 1;
+}
+
+// one read's factors for all six classes (:594-600) with NS live slots;
+// returns true when some lane now needs more than NS slots
+template <int NS>
+__device__ __forceinline__ bool acc_step(Acc &A, uint32_t e, double2 f) {
     const uint32_t cls = e >> 9;
-    const double2 f = lut[e & 511];
-    A.L0 *= (cls == 0) ? f.x : f.y;
-    A.L1 *= (cls == 1) ? f.x : f.y;
-    A.L2 *= (cls == 2) ? f.x : f.y;
-    A.L3 *= (cls == 3) ? f.x : f.y;
-    A.L4 *= (cls == 4) ? f.x : f.y;
-    A.L5 *= (cls == 5) ? f.x : f.y;
-    A.c0 += (cls == 0);
-    A.c1 += (cls == 1);
-    A.c2 += (cls == 2);
-    A.c3 += (cls == 3);
-    A.c4 += (cls == 4);
-    A.c5 += (cls == 5);
-    A.c6 += (cls == 6);
-    A.bad |= (cls == 7);
+    const double Uold = A.U;
+    A.U = Uold * f.y;
+    bool match = false;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        const bool m = cls == (uint32_t)A.k[j];
+        A.s[j] *= m ? f.x : f.y;
+        A.n[j] += m;
+        match |= m;
+    }
+    const bool isnew = cls != 6 && !match;
+    if (__ballot(isnew)) {
+        acc_new_class(A, isnew, cls, Uold, f.x);
+        return __ballot(A.ns > NS) != 0;
+    }
+    return false;
+}
+
+// most_likely_nucleotide over reads 0..R-1 in read order.  Two live slots
+// cover the usual column (one true base plus one error class); a wave that
+// meets a third distinct class switches to six slots for the rest of the tile.
+// Element codes and LUT factors are fetched four reads ahead of their use.
+template <class Src>
+__device__ __forceinline__ void accumulate(Acc &A, int R, const Src &src, const double2 *lut) {
+    bool wide = false;
+    int r = 0;
+    auto step = [&](uint32_t e, double2 f) {
+        if (!wide) wide = acc_step<2>(A, e, f);
+        else (void)acc_step<6>(A, e, f);
+    };
+    for (; r + 4 <= R; r += 4) {
+        const uint32_t e0 = src(r), e1 = src(r + 1), e2 = src(r + 2), e3 = src(r + 3);
+        const double2 f0 = lut[e0 & 511], f1 = lut[e1 & 511], f2 = lut[e2 & 511], f3 = lut[e3 & 511];
+        step(e0, f0);
+        step(e1, f1);
+        step(e2, f2);
+        step(e3, f3);
+    }
+    for (; r < R; ++r) {
+        const uint32_t e = src(r);
+        step(e, lut[e & 511]);
+    }
 }
 
 struct ColOut {
@@ -344,114 +438,206 @@ struct ColOut {
     bool overflow;
 };
 
+// consensus quality Q for error x > 0 finite: the exact table boundaries
+// (params.py) decide; a float log10 only proposes the candidate.
+// Q = lo - 1 with lo = first i with qthr[i] <= x (lo = maxQ + 1 if none).
+__device__ __forceinline__ int phred_from_table(double x, int maxq, const double *qthr) {
+    const float lf = __builtin_amdgcn_logf((float)x);          // log2
+    float qe = rintf(-3.01029995663981198f * lf);               // -10 log10 x
+    qe = fminf(fmaxf(qe, -1.0f), (float)maxq);
+    int q = (int)qe;
+    bool ok_lo = q == maxq || qthr[q + 1] <= x;
+    bool ok_hi = q < 0 || qthr[q] > x;
+    if (__builtin_expect(!(ok_lo && ok_hi), 0)) {
+        int lo = 0, hi = maxq + 1;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (qthr[mid] <= x) hi = mid; else lo = mid + 1;
+        }
+        q = lo - 1;
+    }
+    return q;
+}
+
 // posterior, mask, output quality (:603-621, :699-709), depth/errors (:1001-1012)
-__device__ __forceinline__ ColOut finalize(const Acc &A, int R, bool ins_col, const dcr_params *P,
-                                           const double *qthr) {
-    ColOut o;
-    double S = A.L0 + A.L1;                      // np.sum of 6: left to right (:608)
-    S = S + A.L2;
-    S = S + A.L3;
-    S = S + A.L4;
-    S = S + A.L5;
-    const double p[6] = {A.L0 / S, A.L1 / S, A.L2 / S, A.L3 / S, A.L4 / S, A.L5 / S};
-    int best = 0;                                // np.argmax: first NaN, else first max
-    double pm = p[0];
-    bool nan = __builtin_isnan(p[0]);
+__device__ __forceinline__ ColOut finalize(const Acc &A, int nsw, int R, bool ins_col, const dcr_params *P,
+                                           const double *qthr, bool simple_q) {
+    double L[6];
+    int c[6];
 #pragma unroll
-    for (int i = 1; i < 6; ++i) {
-        if (!nan) {
-            if (__builtin_isnan(p[i])) {
-                nan = true;
-                best = i;
-                pm = p[i];
-            } else if (p[i] > pm) {
-                best = i;
-                pm = p[i];
+    for (int i = 0; i < 6; ++i) {
+        L[i] = A.U;
+        c[i] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        if (j < nsw) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const bool m = A.k[j] == i;
+                L[i] = m ? A.s[j] : L[i];
+                c[i] = m ? A.n[j] : c[i];
             }
         }
     }
-    const bool has_plus = A.c4 > 0;              // '+' in nucleotides (:613, :618)
-    int ch = "ATCG+-"[best];
-    if (has_plus && best < 4) ch += 32;
-    if (pm < P->post_threshold) ch = has_plus ? 'n' : 'N';
+    const int cN = R - c[0] - c[1] - c[2] - c[3] - c[4] - c[5] - A.nbad;
+    ColOut o;
+    double S = L[0] + L[1];                      // np.sum of 6: left to right (:608)
+    S = S + L[2];
+    S = S + L[3];
+    S = S + L[4];
+    S = S + L[5];
+    // np.argmax of L[i]/S (first max, first NaN wins) and np.max (:613-614)
+    int best = 0;
+    double pm;
+    const double Lmin = fmin(fmin(fmin(L[0], L[1]), fmin(L[2], L[3])), fmin(L[4], L[5]));
+    if (S > 0.0 && S <= 1.79769313486231570815e308 && Lmin >= 0.0) {
+        // division by S > 0 is monotone: the first largest L gives the max
+        // posterior, unless an earlier class's quotient rounds to the same
+        // double (only possible within a few ulps: checked exactly, rarely)
+        double Lb = L[0];
+#pragma unroll
+        for (int i = 1; i < 6; ++i) {
+            const bool g = L[i] > Lb;
+            best = g ? i : best;
+            Lb = g ? L[i] : Lb;
+        }
+        pm = Lb / S;
+        const double near = Lb * 0.99999999999999;
+        bool tie = false;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) tie |= (i < best) && (L[i] >= near);
+        if (__builtin_expect(tie, 0)) {
+#pragma unroll
+            for (int i = 4; i >= 0; --i)
+                if (i < best && L[i] >= near && L[i] / S == pm) best = i;
+        }
+    } else {
+        double p[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) p[i] = L[i] / S;
+        pm = p[0];
+        bool nan = __builtin_isnan(p[0]);
+#pragma unroll
+        for (int i = 1; i < 6; ++i) {
+            if (!nan) {
+                if (__builtin_isnan(p[i])) {
+                    nan = true;
+                    best = i;
+                    pm = p[i];
+                } else if (p[i] > pm) {
+                    best = i;
+                    pm = p[i];
+                }
+            }
+        }
+    }
+    const bool has_plus = c[4] > 0;              // '+' in nucleotides (:613, :618)
+    const bool masked = pm < P->post_threshold;  // NaN is never masked (:617)
+    const int kc = masked ? 6 : best;
+    const bool lower = has_plus && (kc < 4 || kc == 6);
+    int ch;
+    if (masked) ch = has_plus ? 'n' : 'N';
+    else ch = (int)((0x2D2B47435441ull >> (8 * best)) & 0xffu) + (lower ? 32 : 0);   // "ATCG+-"
     // consensus quality (:700-709)
     const double e = 1.0 - pm;
-    const double pre = (double)P->error_rate_pre_labeling;
-    const double post = (double)P->error_rate_post_labeling;
-    const double x = pre * (1.0 - e) + (1.0 - post) * e + pre * e * 4.0 / 5.0;
+    double x;
+    if (simple_q) {
+        x = e;                                   // pre = post = 0: the formula reduces to e exactly
+    } else {
+        const double pre = (double)P->error_rate_pre_labeling;
+        const double post = (double)P->error_rate_post_labeling;
+        x = pre * (1.0 - e) + (1.0 - post) * e + pre * e * 4.0 / 5.0;
+    }
     int q = P->max_base_quality;
     o.overflow = false;
-    if (x > 0.0) {
-        if (__builtin_isinf(x)) {
-            o.overflow = true;
-        } else {
-            int lo = 0, hi = P->n_qthresh;       // qthr decreasing: first i with qthr[i] <= x
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (qthr[mid] <= x) hi = mid; else lo = mid + 1;
-            }
-            q = P->max_base_quality - (P->n_qthresh - lo);
-        }
+    if (x > 0.0) {                               // else the ValueError branch: max quality
+        if (__builtin_isinf(x)) o.overflow = true;
+        else q = phred_from_table(x, P->max_base_quality, qthr);
     }
     o.ch = ch;
     o.q = q;
     // depth: rows not in {N, n, +}; errors: rows != consensus char (case-sensitive)
-    o.d = R - A.c6 - A.c4;
-    int kc;
-    switch (ch) {
-    case 'A': case 'a': kc = 0; break;
-    case 'T': case 't': kc = 1; break;
-    case 'C': case 'c': kc = 2; break;
-    case 'G': case 'g': kc = 3; break;
-    case '+': kc = 4; break;
-    case '-': kc = 5; break;
-    default: kc = 6; break;
-    }
-    const bool lower = ch >= 'a';
-    int match = 0;
-    const int cnt[7] = {A.c0, A.c1, A.c2, A.c3, A.c4, A.c5, A.c6};
+    o.d = R - cN - c[4];
+    int cnt = cN;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) cnt = kc == i ? c[i] : cnt;
     // row characters: insertion columns hold lowercase bases / 'n' / '+',
     // normal columns uppercase bases / 'N' / '-'
-    if (kc == 4) match = cnt[4];
-    else if (kc == 5) match = ins_col ? 0 : cnt[5];
-    else match = (lower == ins_col) ? cnt[kc] : 0;
+    int match;
+    if (kc == 4) match = cnt;
+    else if (kc == 5) match = ins_col ? 0 : cnt;
+    else match = (lower == ins_col) ? cnt : 0;
     o.e = R - match;
     return o;
 }
 
+// --------------------------------------------------- per-read register view
+// lane r of these registers holds read r (R <= 64); read back with readlane
+struct LaneReads {
+    int cl;      // first column of the read (pos - min_pos) | kept length << 16
+    int sn;      // stage offset of its first kept base | runs << 16
+};
+
 // ------------------------------------------------------------ k_consensus
-template <bool DUPLEX>
-__global__ __launch_bounds__(kBlock) void k_consensus(Args a) {
-    __shared__ double2 s_lut[DCR_LUT_N];
-    __shared__ double s_qthr[DCR_MAX_QTHRESH];
-    __shared__ uint16_t s_tile[kWavesPerBlock][kWave][kWave];
-
+// One consensus record (single-strand subfamily or duplex pair) on one wave.
+// FAST: only the staged layout (no insertion column, <= 64 reads, bytes fit the
+// LDS stage, T <= kColsLds); any other record is appended to the overflow list
+// and processed by the general kernel.
+template <bool DUPLEX, bool FAST>
+__device__ __forceinline__ void process_record(const Args &a, const int64_t rec, WaveLds &W, const double2 *s_lut,
+                                               const double *s_qthr, const int lane) {
     const dcr_params *P = a.P;
-    for (int i = threadIdx.x; i < DCR_LUT_N; i += kBlock) s_lut[i] = make_double2(P->match[i], P->mismatch[i]);
-    for (int i = threadIdx.x; i < DCR_MAX_QTHRESH; i += kBlock) s_qthr[i] = P->qthresh[i];
-    __syncthreads();
 
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int64_t rec = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-    if (rec >= a.n_rec) return;
-
-    dcr_out &O = DUPLEX ? a.ds : a.ss;
-    const int64_t* col_off = DUPLEX ? a.in.ds_col_off : a.in.ss_col_off;
+    const dcr_out &O = DUPLEX ? a.ds : a.ss;
+    const int64_t *col_off = DUPLEX ? a.in.ds_col_off : a.in.ss_col_off;
     const int64_t off = col_off[rec];
     const int64_t cap = col_off[rec + 1] - off;
     const int minbq = P->min_base_quality;
-    uint16_t(*tile)[kWave] = s_tile[wave];
+    const bool simple_q = P->error_rate_pre_labeling == 0 && P->error_rate_post_labeling == 0;
 
     const int R = DUPLEX ? 2 : (a.in.sub_off[rec + 1] - a.in.sub_off[rec]);
 
+    // staging range: every read of a record lies in one contiguous byte range
+    // (single-strand: its reads are consecutive in the batch; duplex: the two
+    // single-strand regions are adjacent), known one hop before the per-read data
+    const uint8_t *gb = DUPLEX ? a.ss.seq : a.in.bases;
+    const uint8_t *gq = DUPLEX ? a.ss.qual : a.in.quals;
+    int64_t lo_byte, hi_byte;
+    if (!DUPLEX) {
+        const int g0 = a.in.sub_off[rec];
+        lo_byte = R > 0 ? a.in.seq_off[g0] : 0;
+        hi_byte = R > 0 ? a.in.seq_off[g0 + R - 1] + a.in.seq_len[g0 + R - 1] : 0;
+    } else {
+        lo_byte = a.in.ss_col_off[2 * rec];
+        hi_byte = a.in.ss_col_off[2 * rec + 1] + a.ss.len[2 * rec + 1];
+    }
+    const int64_t base_al = lo_byte & ~(int64_t)3;
+    const int64_t span = hi_byte - base_al;
+    const bool fits = R <= kWave && span <= kStageElems && ((((uintptr_t)gb) | ((uintptr_t)gq)) & 3) == 0;
+    // issue the staging loads now (consumed after the setup reductions)
+    constexpr int kStageDw = kStageElems / 4 / kWave;       // dwords per lane
+    uint32_t vb[kStageDw], vq[kStageDw];
+    const int nd = fits ? (int)((span + 3) >> 2) : 0;
+    {
+        const uint32_t *b4 = (const uint32_t *)(gb + base_al);
+        const uint32_t *q4 = (const uint32_t *)(gq + base_al);
+#pragma unroll
+        for (int u = 0; u < kStageDw; ++u) {
+            const int d = u * kWave + lane;
+            vb[u] = d < nd ? b4[d] : 0u;
+            vq[u] = d < nd ? q4[d] : 0u;
+        }
+    }
+
     // ---- setup: lane = read
-    int minpos = 0x7fffffff, maxend = -0x7fffffff, up = 0, empty = 0, ins = 0;
-    long long msum = 0;
+    int minpos = 0x7fffffff, maxend = -0x7fffffff, up = 0, empty = 0, ins = 0, msum = 0;
+    ReadRef myrd{};
     for (int c = 0; c < R; c += kWave) {
         const int r = c + lane;
         if (r < R) {
             const ReadRef rd = get_read<DUPLEX>(a, rec, r);
+            if (r < kWave) myrd = rd;
             up |= rd.status != 0;
             empty |= rd.len <= 0;
             minpos = min(minpos, rd.pos);
@@ -493,24 +679,62 @@ __global__ __launch_bounds__(kBlock) void k_consensus(Args a) {
         return;
     }
 
-    int32_t *cons = a.ws.cons + off;
-    double *et = a.ws.et + off;
+    const bool cols_lds = T <= kColsLds;
+    int32_t *cons = cols_lds ? W.cons : a.ws.cons + off;
+    double *et = cols_lds ? W.et : a.ws.et + off;
     uint16_t *od = O.d + off;
     uint16_t *oe = O.e + off;
 
     bool idx_err = false;      // IndexError inside reconstruct_alignment
-    int bad = 0;               // invalid nucleotide somewhere (:582)
-    int n_de = 0, Dmax = -1, Dmin = 0x7fffffff;
+    int nbad = 0;              // invalid nucleotide somewhere (:582)
+    int n_de = 0, dmax = -1, dmin = 0x7fffffff;
     int first = -1, last = -1;
     bool qoverflow = false;    // int(-inf) consensus quality
+
+    const bool big = R > kWave;
+    const bool staged = fits && !ins;
+    if constexpr (FAST) {
+        if (!staged || !cols_lds) {          // general kernel takes it
+            if (lane == 0) {
+                const int idx = atomicAdd(&a.ws.ovf_count[DUPLEX ? 1 : 0], 1);
+                a.ws.ovf[idx] = (int)rec;
+            }
+            return;
+        }
+    }
+
+    // ---- phase 0: element codes into LDS
+    if (staged) {
+#pragma unroll
+        for (int u = 0; u < kStageDw; ++u) {
+            const int d = u * kWave + lane;
+            if (d < nd) {
+                uint32_t cc[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    cc[k] = make_code<DUPLEX>((vb[u] >> (8 * k)) & 255u, (vq[u] >> (8 * k)) & 255u, minbq);
+                uint2 w;
+                w.x = cc[0] | (cc[1] << 16);
+                w.y = cc[2] | (cc[3] << 16);
+                *(uint2 *)&W.stage[4 * d] = w;
+            }
+        }
+        wave_fence();
+    }
+    if (DCR_ABL == 1) {
+        if (lane == 0) O.pos[rec] = minpos + nd + (int)W.stage[lane];
+        return;
+    }
+    LaneReads lr;
+    lr.cl = (myrd.pos - minpos) | (myrd.len << 16);
+    lr.sn = (int)(myrd.seq_start - base_al) | (myrd.ncig << 16);
 
     // R > 64 with insertion columns: precompute the insertion-column flags
     // (all reads must be consulted per column, :476-478) and keep per-read
     // layout state in global scratch between column tiles.
-    const bool big = R > kWave;
     uint8_t *insflag = a.ws.insflag + off;
     int4 *gstate = DUPLEX ? nullptr : a.ws.state + a.in.sub_off[rec];
-    if (ins && big && !DUPLEX) {
+    if (!FAST && ins && big && !DUPLEX) {
         for (int c = 0; c < R; c += kWave) {
             const int r = c + lane;
             if (r < R) {
@@ -561,39 +785,63 @@ __global__ __launch_bounds__(kBlock) void k_consensus(Args a) {
 
     // small-R insertion layout keeps its state in registers (lane = read)
     Sim sim{0, 0, 0, 0, 0};
-    ReadRef myrd;
-    if (ins && !big) {
-        if (lane < R) {
-            myrd = get_read<DUPLEX>(a, rec, lane);
-            sim_load_run(sim, myrd);
-        }
-    }
+    if (ins && !big && lane < R) sim_load_run(sim, myrd);
 
     // ---- phases 1+2: column tiles (lane = column)
-    for (int c0 = 0; c0 < T; c0 += kWave) {
+    const int tw = ins ? kTileIns : kWave;       // insertion layout: 32-column tiles
+    for (int c0 = 0; c0 < T; c0 += tw) {
         const int t = c0 + lane;
-        const bool live = t < T;
-        const int ncol = min(kWave, T - c0);
+        const bool live = lane < tw && t < T;
+        const int ncol = min(tw, T - c0);
         Acc A;
         acc_init(A);
         bool ins_col = false;
-        if (!ins) {
-            for (int r = 0; r < R; ++r) {
+        if (staged) {
+            // fast layout from LDS: op index j = t - col of read r (:473-545 without I)
+            auto src = [&](int r) -> uint32_t {
+                const int cl = readlane(lr.cl, r);
+                const int sn = readlane(lr.sn, r);
+                const int col = cl & 0xffff, ln = (unsigned)cl >> 16;
+                const int so = sn & 0xffff, nc = (unsigned)sn >> 16;
+                const int j = t - col;
+                uint32_t e = kPad;
+                if (nc == 1) {
+                    if (live && (unsigned)j < (unsigned)ln) e = W.stage[so + j];
+                } else if (live && j >= 0) {
+                    const ReadRef rd = get_read<DUPLEX>(a, rec, r);
+                    int is;
+                    bool del;
+                    if (walk_runs(rd.cig, rd.ncig, j, ln, is, del)) e = del ? kDel : W.stage[so + is];
+                }
+                return e;
+            };
+            accumulate(A, R, src, s_lut);
+        } else if (FAST) {
+            // unreachable: the fast kernel only keeps staged records
+        } else if (!ins) {
+            auto src = [&](int r) -> uint32_t {
                 const ReadRef rd = get_read<DUPLEX>(a, rec, r);
-                const uint32_t e = live ? direct_elem<DUPLEX>(rd, t - (rd.pos - minpos), minbq) : kPad;
-                acc_add(A, e, s_lut);
-            }
+                const int j = t - (rd.pos - minpos);
+                uint32_t e = kPad;
+                int is;
+                bool del;
+                if (live && j >= 0 && walk_runs(rd.cig, rd.ncig, j, rd.len, is, del))
+                    e = del ? kDel : base_elem<DUPLEX>(rd, is, minbq);
+                return e;
+            };
+            accumulate(A, R, src, s_lut);
         } else if (!big) {
             uint64_t insmask = 0;
             for (int tt = 0; tt < ncol; ++tt) {
                 const bool isI = lane < R && sim.curop == 1;
                 const bool any = __ballot(isI) != 0;
                 insmask |= (uint64_t)any << tt;
-                if (lane < R) tile[lane][tt] = (uint16_t)sim_step<DUPLEX>(sim, myrd, minpos + c0 + tt, any, minbq, idx_err);
+                if (lane < R) W.tile[lane][tt] = (uint16_t)sim_step<DUPLEX>(sim, myrd, minpos + c0 + tt, any, minbq, idx_err);
             }
             wave_fence();
-            ins_col = (insmask >> lane) & 1;
-            for (int r = 0; r < R; ++r) acc_add(A, live ? tile[r][lane] : kPad, s_lut);
+            ins_col = live && ((insmask >> lane) & 1);
+            auto src = [&](int r) -> uint32_t { return live ? (uint32_t)W.tile[r][lane & (kTileIns - 1)] : kPad; };
+            accumulate(A, R, src, s_lut);
             wave_fence();
         } else {
             ins_col = live && insflag[t];
@@ -606,17 +854,23 @@ __global__ __launch_bounds__(kBlock) void k_consensus(Args a) {
                     Sim s{st.x, st.y, st.z, 0, 0};
                     sim_load_run(s, rd);
                     for (int tt = 0; tt < ncol; ++tt)
-                        tile[lane][tt] = (uint16_t)sim_step<DUPLEX>(s, rd, minpos + c0 + tt, insflag[c0 + tt] != 0,
-                                                                    minbq, idx_err);
+                        W.tile[lane][tt] = (uint16_t)sim_step<DUPLEX>(s, rd, minpos + c0 + tt, insflag[c0 + tt] != 0,
+                                                                      minbq, idx_err);
                     gstate[r] = make_int4(s.k, s.o, s.is, 0);
                 }
                 wave_fence();
-                for (int rr = 0; rr < nr; ++rr) acc_add(A, live ? tile[rr][lane] : kPad, s_lut);
+                auto src = [&](int rr) -> uint32_t { return live ? (uint32_t)W.tile[rr][lane & (kTileIns - 1)] : kPad; };
+                accumulate(A, nr, src, s_lut);
                 wave_fence();
             }
         }
-        bad |= A.bad && live;
-        const ColOut co = finalize(A, R, ins_col, P, s_qthr);
+        nbad += live ? A.nbad : 0;
+        const int nsw = wave_max(A.ns);
+        if (DCR_ABL == 2) {
+            if (live) cons[t] = (int)(A.U * 1e9) + nsw + A.n[0];
+            continue;
+        }
+        const ColOut co = finalize(A, nsw, R, ins_col, P, s_qthr, simple_q);
         if (live) {
             cons[t] = co.ch | (co.q << 8);
             qoverflow |= co.overflow;
@@ -629,10 +883,10 @@ __global__ __launch_bounds__(kBlock) void k_consensus(Args a) {
             od[idx] = (uint16_t)co.d;
             oe[idx] = (uint16_t)co.e;
             et[idx] = co.d == 0 ? 1.0 : (double)co.e / (double)co.d;
+            dmax = max(dmax, co.d);
+            dmin = min(dmin, co.d);
         }
         n_de += __popcll(km);
-        Dmax = max(Dmax, wave_max(keep ? co.d : -1));
-        Dmin = min(Dmin, wave_min(keep ? co.d : 0x7fffffff));
         // 5'/3' trims count uppercase 'N' only (:770-784)
         const uint64_t nn = __ballot(live && co.ch != 'N');
         if (nn) {
@@ -640,11 +894,18 @@ __global__ __launch_bounds__(kBlock) void k_consensus(Args a) {
             last = c0 + 63 - __builtin_clzll(nn);
         }
     }
+    if (DCR_ABL == 2 || DCR_ABL == 3) {
+        if (lane == 0) O.pos[rec] = cons[0] + n_de + first + last;
+        return;
+    }
+    const int Dmax = wave_max(dmax);
+    const int Dmin = wave_min(dmin);
     idx_err = __ballot(idx_err) != 0;
-    bad = __ballot(bad) != 0;
+    const bool bad = __ballot(nbad != 0) != 0;
     qoverflow = __ballot(qoverflow) != 0;
     if (idx_err) { write_status(DCR_ST_INDEX_ERROR); return; }
     if (bad) { write_status(DCR_ST_EXIT_BADCHAR); return; }
+    if (qoverflow) { write_status(DCR_ST_OVERFLOW_ERROR); return; }
     wave_fence();
 
     // ---- phase 3: adjust_consensus_fields (:745-871) over [first, last]
@@ -653,6 +914,8 @@ __global__ __launch_bounds__(kBlock) void k_consensus(Args a) {
     uint8_t *oseq = O.seq + off;
     uint8_t *oqual = O.qual + off;
     uint32_t *ocig = O.cigar + off;
+    // run starts: LDS (the staging region is dead now) when they fit
+    uint32_t *rstart_buf = cols_lds ? (uint32_t *)W.stage : ocig;
     int nruns = 0, nops = 0, nlen = 0, last_op = -1, chain_start = lo;
     bool kept_overflow = false;
     for (int c0 = lo; c0 < hi; c0 += kWave) {
@@ -702,7 +965,7 @@ __global__ __launch_bounds__(kBlock) void k_consensus(Args a) {
         if (rstart) {
             const int ri = nruns + __popcll(rm & lanemask_lt(lane));
             const int oi = nops + __popcll(vbelow);
-            ocig[ri] = ((uint32_t)oi << 4) | (uint32_t)op;        // run start, converted below
+            rstart_buf[ri] = ((uint32_t)oi << 4) | (uint32_t)op;  // run start, converted below
         }
         if (vm) last_op = __shfl(op, 63 - __builtin_clzll(vm));
         nruns += __popcll(rm);
@@ -721,78 +984,99 @@ __global__ __launch_bounds__(kBlock) void k_consensus(Args a) {
     kept_overflow = __ballot(kept_overflow) != 0;
     if (nruns == 0) { write_status(DCR_ST_INDEX_ERROR); return; }   // compress_cigarlist([])
     if (n_de == 0) { write_status(DCR_ST_VALUE_ERROR); return; }     // max([]) at :1005
-    if (kept_overflow || qoverflow) { write_status(DCR_ST_OVERFLOW_ERROR); return; }
+    if (kept_overflow) { write_status(DCR_ST_OVERFLOW_ERROR); return; }
     wave_fence();
     for (int i0 = 0; i0 < nruns; i0 += kWave) {
         const int i = i0 + lane;
         uint32_t v = 0, nx = 0;
         if (i < nruns) {
-            v = ocig[i];
-            nx = i + 1 < nruns ? (ocig[i + 1] >> 4) : (uint32_t)nops;
+            v = rstart_buf[i];
+            nx = i + 1 < nruns ? (rstart_buf[i + 1] >> 4) : (uint32_t)nops;
         }
         wave_fence();
         if (i < nruns) ocig[i] = ((nx - (v >> 4)) << 4) | (v & 15);
     }
 
     // ---- E = round(mean(e/d), 3) with numpy's pairwise summation (:1015-1018)
+    // pairwise_sum(a, n): n < 8 sequential; n <= 128 eight accumulators; else
+    // split at n2 = n/2 rounded down to a multiple of 8 and add the halves.
     wave_fence();
+    auto leaf = [&](int fo, int fn) -> double {
+        double res;
+        if (fn < 8) {
+            res = -0.0;
+            for (int i = 0; i < fn; ++i) res += et[fo + i];
+        } else {
+            const int body = fn - (fn % 8);
+            double r = 0.0;
+            if (lane < 8) {
+                r = et[fo + lane];
+#pragma unroll 4
+                for (int i = 8; i < body; i += 8) r += et[fo + i + lane];
+            }
+            const double r0 = __shfl(r, 0), r1 = __shfl(r, 1), r2 = __shfl(r, 2), r3 = __shfl(r, 3);
+            const double r4 = __shfl(r, 4), r5 = __shfl(r, 5), r6 = __shfl(r, 6), r7 = __shfl(r, 7);
+            res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+            for (int i = body; i < fn; ++i) res += et[fo + i];
+        }
+        return res;
+    };
     double total;
-    {
-        // explicit-stack form of numpy's pairwise_sum recursion (blocks of <= 128,
-        // 8 accumulators, split at n/2 rounded down to a multiple of 8)
-        int st_off[24], st_n[24], st_stage[24];
-        double st_left[24];
+    if (n_de <= 128) {
+        total = leaf(0, n_de);
+    } else if (n_de <= 240) {           // both halves <= 128 (ceil(n/2) + 7 <= 128)
+        int n2 = n_de / 2;
+        n2 -= n2 % 8;
+        const double left = leaf(0, n2);
+        total = left + leaf(n2, n_de - n2);
+    } else if (!FAST) {
+        // general depth: explicit uniform stack in LDS
+        int *stk_off = W.stk_off, *stk_n = W.stk_n, *stk_stage = W.stk_stage;
+        double *stk_left = W.stk_left;
         int sp = 0;
-        st_off[0] = 0; st_n[0] = n_de; st_stage[0] = 0; st_left[0] = 0.0;
+        stk_off[0] = 0;
+        stk_n[0] = n_de;
+        stk_stage[0] = 0;
         double ret = 0.0;
         while (sp >= 0) {
-            const int fo = st_off[sp], fn = st_n[sp];
+            const int fo = stk_off[sp], fn = stk_n[sp];
             if (fn <= 128) {
-                double res;
-                if (fn < 8) {
-                    res = -0.0;
-                    for (int i = 0; i < fn; ++i) res += et[fo + i];
-                } else {
-                    const int body = fn - (fn % 8);
-                    double r = 0.0;
-                    if (lane < 8) {
-                        r = et[fo + lane];
-                        for (int i = 8; i < body; i += 8) r += et[fo + i + lane];
-                    }
-                    const double r0 = __shfl(r, 0), r1 = __shfl(r, 1), r2 = __shfl(r, 2), r3 = __shfl(r, 3);
-                    const double r4 = __shfl(r, 4), r5 = __shfl(r, 5), r6 = __shfl(r, 6), r7 = __shfl(r, 7);
-                    res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-                    for (int i = body; i < fn; ++i) res += et[fo + i];
-                }
-                ret = res;
+                ret = leaf(fo, fn);
                 --sp;
                 continue;
             }
             int n2 = fn / 2;
             n2 -= n2 % 8;
-            if (st_stage[sp] == 0) {
-                st_stage[sp] = 1;
+            if (stk_stage[sp] == 0) {
+                stk_stage[sp] = 1;
                 ++sp;
-                st_off[sp] = fo; st_n[sp] = n2; st_stage[sp] = 0;
-            } else if (st_stage[sp] == 1) {
-                st_left[sp] = ret;
-                st_stage[sp] = 2;
+                stk_off[sp] = fo;
+                stk_n[sp] = n2;
+                stk_stage[sp] = 0;
+            } else if (stk_stage[sp] == 1) {
+                stk_left[sp] = ret;
+                stk_stage[sp] = 2;
                 ++sp;
-                st_off[sp] = fo + n2; st_n[sp] = fn - n2; st_stage[sp] = 0;
+                stk_off[sp] = fo + n2;
+                stk_n[sp] = fn - n2;
+                stk_stage[sp] = 0;
             } else {
-                ret = st_left[sp] + ret;
+                ret = stk_left[sp] + ret;
                 --sp;
             }
         }
-        total = 0.0 + ret;
+        total = ret;
+    } else {
+        total = 0.0;   // unreachable in the fast kernel (T <= kColsLds)
     }
+    total = 0.0 + total;
     const double mean = total / (double)n_de;
     const double E = __builtin_rint(mean * 1000.0) / 1000.0;
 
     if (lane == 0) {
         O.status[rec] = DCR_ST_OK;
         O.pos[rec] = minpos + lo;                   // :790
-        O.mapq[rec] = (int)(msum / R);              // trunc(np.mean) (:887, :1377)
+        O.mapq[rec] = msum / R;                     // trunc(np.mean) (:887, :1377)
         O.len[rec] = nlen;
         O.n_cig[rec] = nruns;
         O.n_de[rec] = n_de;
@@ -802,7 +1086,430 @@ __global__ __launch_bounds__(kBlock) void k_consensus(Args a) {
     }
 }
 
-template __global__ void k_consensus<false>(Args);
-template __global__ void k_consensus<true>(Args);
+
+// ------------------------------------------------------- fast records
+// The dominant record shape: every read a single M run (no I, no D, so no
+// insertion columns and no '-' rows), <= 64 reads, bytes fit the LDS stage,
+// T <= kColsLds.  Then every aligned row is a base, a masked 'N' or a pad 'N'
+// (classes 0-3 and 6), no column holds '+', and the consensus is uppercase
+// A/C/G/T/N only, so its CIGAR is one M run over the trimmed span
+// (:797-848 yields M for every such column).
+//
+// Likelihoods: a pre-scan of the tile gives each lane (column) the set of base
+// classes present; the wave picks the loop with that many chains (U for every
+// unseen class, plus one chain per present class, fixed before the product
+// loop, so the loop is branch-free).  Products stay in read order: identical
+// doubles to the reference's six chains.
+// element code of read r at column t; outside the read's span the load is
+// redirected to the kPad sentinel (selecting the address, not the loaded
+// value, keeps the bounds mask out of VCC while the LDS read is in flight)
+__device__ __forceinline__ uint32_t fast_elem(const LaneReads &lr, int r, int t, bool live, const uint16_t *stage) {
+    const int cl = readlane(lr.cl, r);
+    const int so = readlane(lr.sn, r);
+    const int j = t - (cl & 0xffff);
+    const bool inb = live && (unsigned)j < ((unsigned)cl >> 16);
+    return stage[inb ? so + j : -4];             // stage[-4] = pad_code[0]
+}
+
+template <int NS>
+__device__ __forceinline__ void fast_mul(double &U, double (&s)[4], int (&n)[4], const int (&k)[4], uint32_t e,
+                                         double2 f) {
+    const uint32_t cls = e >> 9;
+    U *= f.y;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        const bool m = cls == (uint32_t)k[q];
+        s[q] *= m ? f.x : f.y;
+        n[q] += m;
+    }
+}
+
+// products in read order; reads fetched four at a time (codes, then LUT
+// factors) before the multiplies, so LDS latency overlaps (hand-unrolled:
+// readlane is convergent and blocks the compiler's runtime unrolling)
+template <int NS>
+__device__ __forceinline__ void fast_products(double &U, double (&s)[4], int (&n)[4], const int (&k)[4], int R,
+                                              int t, bool live, const LaneReads &lr, const uint16_t *stage,
+                                              const double2 *lut) {
+    int r = 0;
+    for (; r + 4 <= R; r += 4) {
+        const uint32_t e0 = fast_elem(lr, r, t, live, stage);
+        const uint32_t e1 = fast_elem(lr, r + 1, t, live, stage);
+        const uint32_t e2 = fast_elem(lr, r + 2, t, live, stage);
+        const uint32_t e3 = fast_elem(lr, r + 3, t, live, stage);
+        const double2 f0 = lut[e0 & 511], f1 = lut[e1 & 511], f2 = lut[e2 & 511], f3 = lut[e3 & 511];
+        fast_mul<NS>(U, s, n, k, e0, f0);
+        fast_mul<NS>(U, s, n, k, e1, f1);
+        fast_mul<NS>(U, s, n, k, e2, f2);
+        fast_mul<NS>(U, s, n, k, e3, f3);
+    }
+    for (; r < R; ++r) {
+        const uint32_t e = fast_elem(lr, r, t, live, stage);
+        fast_mul<NS>(U, s, n, k, e, lut[e & 511]);
+    }
+}
+
+// numpy pairwise_sum over a[0..n), n <= 240 (at most two blocks of <= 128, 8 accumulators):
+// accumulator j of block b lives on lane 8b + j and loads its <= 16 elements
+// up front; the fixed association order of numpy is kept exactly.
+__device__ __forceinline__ double pairwise_small(const double *a, int n, int lane) {
+    if (n < 8) {
+        double res = -0.0;
+        for (int i = 0; i < n; ++i) res += a[i];
+        return res;
+    }
+    int n2 = n, nb = 1;
+    if (n > 128) {
+        n2 = n / 2;
+        n2 -= n2 % 8;
+        nb = 2;
+    }
+    const int blk = (lane >> 3) & 1;
+    const int bo = blk ? n2 : 0;                 // block offset
+    const int bn = blk ? n - n2 : n2;            // block length (>= 8 when it is a block)
+    const int body = bn - (bn % 8);
+    const int j = lane & 7;
+    double v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int idx = j + 8 * i;
+        v[i] = (lane < 8 * nb && idx < body) ? a[bo + idx] : 0.0;
+    }
+    double r = v[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i)
+        if (8 * i < body) r += v[i];
+    // per block: ((r0+r1)+(r2+r3)) + ((r4+r5)+(r6+r7)), then the tail in order
+    const double p01 = r + __shfl_xor(r, 1);                 // lanes 8b+0/1 hold r0+r1 ...
+    const double p0123 = p01 + __shfl_xor(p01, 2);
+    // careful: the association must be ((r0+r1)+(r2+r3)) + ((r4+r5)+(r6+r7))
+    const double s8 = p0123 + __shfl_xor(p0123, 4);
+    double res[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        double x = __shfl(s8, 8 * b);
+        const int o = b ? n2 : 0, m = b ? n - n2 : n2;
+        const int bd = m - (m % 8);
+        if (b < nb)
+            for (int i = bd; i < m; ++i) x += a[o + i];
+        res[b] = x;
+    }
+    return nb == 1 ? res[0] : res[0] + res[1];
+}
+
+template <bool DUPLEX>
+__device__ __forceinline__ void process_fast(const Args &a, const int64_t rec, WaveLds &W, const double2 *s_lut,
+                                             const double *s_qthr, const int lane) {
+    const dcr_params *P = a.P;
+    const dcr_out &O = DUPLEX ? a.ds : a.ss;
+    const int64_t *col_off = DUPLEX ? a.in.ds_col_off : a.in.ss_col_off;
+    const int64_t off = col_off[rec];
+    const int64_t cap = col_off[rec + 1] - off;
+    const int minbq = P->min_base_quality;
+    const bool simple_q = P->error_rate_pre_labeling == 0 && P->error_rate_post_labeling == 0;
+    const int R = DUPLEX ? 2 : (a.in.sub_off[rec + 1] - a.in.sub_off[rec]);
+
+    const uint8_t *gb = DUPLEX ? a.ss.seq : a.in.bases;
+    const uint8_t *gq = DUPLEX ? a.ss.qual : a.in.quals;
+    int64_t lo_byte, hi_byte;
+    if (!DUPLEX) {
+        const int g0 = a.in.sub_off[rec];
+        lo_byte = R > 0 ? a.in.seq_off[g0] : 0;
+        hi_byte = R > 0 ? a.in.seq_off[g0 + R - 1] + a.in.seq_len[g0 + R - 1] : 0;
+    } else {
+        lo_byte = a.in.ss_col_off[2 * rec];
+        hi_byte = a.in.ss_col_off[2 * rec + 1] + a.ss.len[2 * rec + 1];
+    }
+    const int64_t base_al = lo_byte & ~(int64_t)3;
+    const int64_t span = hi_byte - base_al;
+    const bool fits = R <= kWave && span <= kStageElems && ((((uintptr_t)gb) | ((uintptr_t)gq)) & 3) == 0;
+    constexpr int kStageDw = kStageElems / 4 / kWave;
+    uint32_t vb[kStageDw], vq[kStageDw];
+    const int nd = fits ? (int)((span + 3) >> 2) : 0;
+    {
+        const uint32_t *b4 = (const uint32_t *)(gb + base_al);
+        const uint32_t *q4 = (const uint32_t *)(gq + base_al);
+#pragma unroll
+        for (int u = 0; u < kStageDw; ++u) {
+            const int d = u * kWave + lane;
+            vb[u] = d < nd ? b4[d] : 0u;
+            vq[u] = d < nd ? q4[d] : 0u;
+        }
+    }
+
+    // setup: lane = read (R <= 64 here, else handed over)
+    int minpos = 0x7fffffff, maxend = -0x7fffffff, up = 0, empty = 0, other = 0, msum = 0;
+    ReadRef myrd{};
+    if (lane < R) {
+        myrd = get_read<DUPLEX>(a, rec, lane);
+        up = myrd.status != 0;
+        empty = myrd.len <= 0;
+        minpos = myrd.pos;
+        maxend = myrd.pos + myrd.len;
+        msum = myrd.mapq;
+        // single M run only (no I / D anywhere in the record)
+        other = myrd.ncig != 1 || (myrd.len > 0 && (myrd.cig[0] & 15) != 0);
+    }
+    minpos = wave_min(minpos);
+    maxend = wave_max(maxend);
+    up = __ballot(up) != 0;
+    empty = __ballot(empty) != 0;
+    other = __ballot(other) != 0;
+    msum = wave_sum(msum);
+
+    auto write_status = [&](int st) {
+        if (lane == 0) {
+            O.status[rec] = (uint8_t)st;
+            O.pos[rec] = 0;
+            O.mapq[rec] = 0;
+            O.len[rec] = 0;
+            O.n_cig[rec] = 0;
+            O.n_de[rec] = 0;
+            O.D[rec] = 0;
+            O.M[rec] = 0;
+            O.E[rec] = 0.0;
+        }
+    };
+    if (R == 0 || (R <= kWave && up)) { write_status(DCR_ST_UPSTREAM); return; }
+    if (R <= kWave && empty) { write_status(DCR_ST_TYPE_ERROR); return; }
+    const int T = maxend - minpos;
+    if (R > kWave || other || !fits || T > kFastMaxT || T > cap || !a.fast_ok) {
+        if (lane == 0) {                      // general kernel takes it
+            const int idx = atomicAdd(&a.ws.ovf_count[DUPLEX ? 1 : 0], 1);
+            a.ws.ovf[idx] = (int)rec;
+        }
+        return;
+    }
+
+    // phase 0: element codes into LDS
+#pragma unroll
+    for (int u = 0; u < kStageDw; ++u) {
+        const int d = u * kWave + lane;
+        if (d < nd) {
+            uint32_t cc[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                cc[k] = make_code<DUPLEX>((vb[u] >> (8 * k)) & 255u, (vq[u] >> (8 * k)) & 255u, minbq);
+            uint2 w;
+            w.x = cc[0] | (cc[1] << 16);
+            w.y = cc[2] | (cc[3] << 16);
+            *(uint2 *)&W.stage[4 * d] = w;
+        }
+    }
+    LaneReads lr;
+    lr.cl = (myrd.pos - minpos) | (myrd.len << 16);
+    lr.sn = (int)(myrd.seq_start - base_al);
+    if (lane == 0) W.pad_code[0] = (uint16_t)kPad;
+    wave_fence();
+    if (DCR_ABL == 1) {
+        if (lane == 0) O.pos[rec] = minpos + nd + (int)W.stage[lane];
+        return;
+    }
+
+    uint16_t *od = O.d + off;
+    uint16_t *oe = O.e + off;
+    int dmax = -1, dmin = 0x7fffffff, first = -1, last = -1;
+    bool bad = false, qoverflow = false;
+    const double pre = (double)P->error_rate_pre_labeling;
+    const double post = (double)P->error_rate_post_labeling;
+
+    for (int c0 = 0; c0 < T; c0 += kWave) {
+        const int t = c0 + lane;
+        const bool live = t < T;
+        // pre-scan: classes present in this column
+        uint32_t mask = 0;
+        {
+            int r = 0;
+            for (; r + 4 <= R; r += 4) {
+                const uint32_t e0 = fast_elem(lr, r, t, live, W.stage);
+                const uint32_t e1 = fast_elem(lr, r + 1, t, live, W.stage);
+                const uint32_t e2 = fast_elem(lr, r + 2, t, live, W.stage);
+                const uint32_t e3 = fast_elem(lr, r + 3, t, live, W.stage);
+                mask |= (1u << (e0 >> 9)) | (1u << (e1 >> 9)) | (1u << (e2 >> 9)) | (1u << (e3 >> 9));
+            }
+            for (; r < R; ++r) mask |= 1u << (fast_elem(lr, r, t, live, W.stage) >> 9);
+        }
+        bad |= (mask & 0x80u) != 0;               // invalid character (:582)
+        const uint32_t cm = mask & 0x0fu;         // base classes A T C G
+        int k[4] = {-1, -1, -1, -1};
+        {
+            uint32_t m = cm;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                k[q] = m ? __builtin_ctz(m) : -1;
+                m &= m - 1;
+            }
+        }
+        const int pc = __popc(cm);                 // wave max of pc by ballots (no LDS)
+        const int nsl = __ballot(pc >= 3) ? 4 : __ballot(pc >= 2) ? 2 : __ballot(pc >= 1) ? 1 : 0;
+        double U = 1.0;
+        double sl[4] = {1.0, 1.0, 1.0, 1.0};
+        int n[4] = {0, 0, 0, 0};
+        switch (nsl) {
+        case 0: fast_products<0>(U, sl, n, k, R, t, live, lr, W.stage, s_lut); break;
+        case 1: fast_products<1>(U, sl, n, k, R, t, live, lr, W.stage, s_lut); break;
+        case 2: fast_products<2>(U, sl, n, k, R, t, live, lr, W.stage, s_lut); break;
+        default: fast_products<4>(U, sl, n, k, R, t, live, lr, W.stage, s_lut); break;
+        }
+        if (DCR_ABL == 2) {
+            if (live) W.cons[t] = (int)(U * 1e9) + n[0] + (int)sl[1];
+            continue;
+        }
+        // L_i: its chain if class i is present, else U ('+', '-' never are)
+        double L[6] = {U, U, U, U, U, U};
+        int c[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const bool m = k[q] == i;
+                L[i] = m ? sl[q] : L[i];
+                c[i] = m ? n[q] : c[i];
+            }
+        }
+        const int cN = R - c[0] - c[1] - c[2] - c[3];
+        // posterior (:603-614): S > 0 here (products of positive factors) unless
+        // everything underflowed; zero S keeps the reference's NaN semantics
+        double S = L[0] + L[1];
+        S = S + L[2];
+        S = S + L[3];
+        S = S + L[4];
+        S = S + L[5];
+        int best = 0;
+        double Lb = L[0];
+#pragma unroll
+        for (int i = 1; i < 6; ++i) {
+            const bool g = L[i] > Lb;
+            best = g ? i : best;
+            Lb = g ? L[i] : Lb;
+        }
+        double pm = Lb / S;                        // NaN when S == 0: argmax 0 ('A')
+        if (__builtin_expect(S > 0.0, 1)) {
+            const double near = Lb * 0.99999999999999;
+            bool tie = false;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) tie |= (i < best) && (L[i] >= near);
+            if (__builtin_expect(tie, 0)) {
+#pragma unroll
+                for (int i = 4; i >= 0; --i)
+                    if (i < best && L[i] >= near && L[i] / S == pm) best = i;
+            }
+        } else {
+            best = 0;
+        }
+        const bool masked = pm < P->post_threshold;
+        const int ch = masked ? 'N' : (int)((0x2D2B47435441ull >> (8 * best)) & 0xffu);
+        const double e = 1.0 - pm;
+        const double x = simple_q ? e : pre * (1.0 - e) + (1.0 - post) * e + pre * e * 4.0 / 5.0;
+        int q = P->max_base_quality;
+        if (x > 0.0) {
+            if (__builtin_isinf(x)) qoverflow = true;
+            else q = phred_from_table(x, P->max_base_quality, s_qthr);
+        }
+        // depth / errors (:1001-1012): no '+' rows and no '+' consensus here
+        const int d = R - cN;
+        int cnt = cN;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cnt = (!masked && best == i) ? c[i] : cnt;
+        if (!masked && best >= 4) cnt = 0;
+        const int er = R - cnt;
+        if (live) {
+            W.cons[t] = ch | (q << 8);
+            od[t] = (uint16_t)d;
+            oe[t] = (uint16_t)er;
+            W.et[t] = d == 0 ? 1.0 : (double)er / (double)d;
+            dmax = max(dmax, d);
+            dmin = min(dmin, d);
+        }
+        const uint64_t nn = __ballot(live && ch != 'N');
+        if (nn) {
+            if (first < 0) first = c0 + __builtin_ctzll(nn);
+            last = c0 + 63 - __builtin_clzll(nn);
+        }
+    }
+    if (DCR_ABL == 2 || DCR_ABL == 3) {
+        if (lane == 0) O.pos[rec] = W.cons[0] + first + last;
+        return;
+    }
+    const bool anybad = __ballot(bad) != 0;
+    qoverflow = __ballot(qoverflow) != 0;
+    if (anybad) { write_status(DCR_ST_EXIT_BADCHAR); return; }
+    if (qoverflow) { write_status(DCR_ST_OVERFLOW_ERROR); return; }
+    if (first < 0) { write_status(DCR_ST_INDEX_ERROR); return; }   // all 'N': compress_cigarlist([])
+    const int Dmax = wave_max(dmax);
+    const int Dmin = wave_min(dmin);
+    wave_fence();
+    // field layout: trimmed span [first, last] is all M (:770-848, :858-865)
+    const int lo = first, hi = last + 1;
+    uint8_t *oseq = O.seq + off;
+    uint8_t *oqual = O.qual + off;
+    bool kept_overflow = false;
+    for (int c0 = lo; c0 < hi; c0 += kWave) {
+        const int t = c0 + lane;
+        if (t < hi) {
+            const int v = W.cons[t];
+            const int qq = v >> 8;
+            oseq[t - lo] = (uint8_t)(v & 255);
+            oqual[t - lo] = (uint8_t)qq;
+            kept_overflow |= (qq < 0 || qq > 255);
+        }
+    }
+    if (__ballot(kept_overflow)) { write_status(DCR_ST_OVERFLOW_ERROR); return; }
+    // E = round(mean(e/d), 3) with numpy's pairwise summation over T values
+    wave_fence();
+    const double total = 0.0 + pairwise_small(W.et, T, lane);
+    const double E = __builtin_rint((total / (double)T) * 1000.0) / 1000.0;
+    if (lane == 0) {
+        O.status[rec] = DCR_ST_OK;
+        O.pos[rec] = minpos + lo;
+        O.mapq[rec] = msum / R;
+        O.len[rec] = hi - lo;
+        O.n_cig[rec] = 1;
+        O.cigar[off] = ((uint32_t)(hi - lo) << 4) | 0u;
+        O.n_de[rec] = T;
+        O.D[rec] = Dmax;
+        O.M[rec] = Dmin;
+        O.E[rec] = E;
+    }
+}
+
+template <bool DUPLEX>
+__global__ __launch_bounds__(kBlock, 4) void k_consensus_fast(Args a) {
+    __shared__ double2 s_lut[DCR_LUT_N];
+    __shared__ double s_qthr[DCR_MAX_QTHRESH];
+    __shared__ WaveLds s_wave[kWavesPerBlock];
+    const dcr_params *P = a.P;
+    for (int i = threadIdx.x; i < DCR_LUT_N; i += kBlock) s_lut[i] = make_double2(P->match[i], P->mismatch[i]);
+    for (int i = threadIdx.x; i < DCR_MAX_QTHRESH; i += kBlock) s_qthr[i] = P->qthresh[i];
+    __syncthreads();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t rec = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+    if (rec >= a.n_rec) return;
+    process_fast<DUPLEX>(a, rec, s_wave[wave], s_lut, s_qthr, threadIdx.x & 63);
+}
+
+// persistent: drains the overflow list written by k_consensus_fast
+template <bool DUPLEX>
+__global__ __launch_bounds__(kBlock, 2) void k_consensus_general(Args a) {
+    __shared__ double2 s_lut[DCR_LUT_N];
+    __shared__ double s_qthr[DCR_MAX_QTHRESH];
+    __shared__ WaveLds s_wave[kWavesPerBlock];
+    const dcr_params *P = a.P;
+    for (int i = threadIdx.x; i < DCR_LUT_N; i += kBlock) s_lut[i] = make_double2(P->match[i], P->mismatch[i]);
+    for (int i = threadIdx.x; i < DCR_MAX_QTHRESH; i += kBlock) s_qthr[i] = P->qthresh[i];
+    __syncthreads();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int n = a.ws.ovf_count[DUPLEX ? 1 : 0];
+    const int nw = gridDim.x * kWavesPerBlock;
+    for (int i = blockIdx.x * kWavesPerBlock + wave; i < n; i += nw) {
+        const int64_t rec = a.ws.ovf[i];
+        process_record<DUPLEX, false>(a, rec, s_wave[wave], s_lut, s_qthr, threadIdx.x & 63);
+    }
+}
+
+template __global__ void k_consensus_fast<false>(Args);
+template __global__ void k_consensus_fast<true>(Args);
+template __global__ void k_consensus_general<false>(Args);
+template __global__ void k_consensus_general<true>(Args);
 
 }  // namespace dcr

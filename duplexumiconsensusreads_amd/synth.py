@@ -121,7 +121,7 @@ def family_records(rng, cfg: SynthConfig, fam_id: int, tid=0, locus=None):
     """Records of one duplex family in BAM order (pairs adjacent)."""
     L = cfg.read_len
     n4 = _sub_sizes(rng, cfg, 4)
-    ins = int(np.clip(rng.normal(300, 30), 200, 500))
+    ins = max(int(np.clip(rng.normal(300, 30), 200, 500)), L + 10)
     P = int(locus if locus is not None else rng.integers(1000, 100_000_000))
     tmpl = _ACGT[rng.integers(0, 4, ins + 20)]
     u1 = "".join(chr(c) for c in _ACGT[rng.integers(0, 4, 8)])

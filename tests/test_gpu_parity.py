@@ -47,7 +47,8 @@ def test_gpu_matches_reference_goldens(ctx, pname):
     assert n_ok > 0 or pname == "pre1"
 
 
-@pytest.mark.parametrize("seed,kind", [(1, "C1"), (2, "indel"), (3, "clip"), (4, "big"), (5, "wild")])
+@pytest.mark.parametrize("seed,kind", [(1, "C1"), (2, "indel"), (3, "clip"), (4, "big"), (5, "wild"),
+                                       (6, "len250"), (7, "len600"), (8, "len90"), (9, "deep")])
 def test_gpu_matches_oracle_random(ctx, seed, kind):
     if kind == "C1":
         cfg = synth.SynthConfig("t", 300, sub_size="poisson5", seed=seed)
@@ -58,6 +59,14 @@ def test_gpu_matches_oracle_random(ctx, seed, kind):
     elif kind == "big":
         cfg = synth.SynthConfig("t", 6, sub_size="loguniform", logu_lo=60, logu_hi=300, indel_frac=0.05,
                                 n_loci=2, seed=seed)
+    elif kind == "len250":   # T around the 240/256 pairwise and LDS-scratch boundaries
+        cfg = synth.SynthConfig("t", 120, read_len=248, sub_size="poisson5", indel_frac=0.1, seed=seed)
+    elif kind == "len600":   # T > 256: global column scratch, deeper pairwise recursion
+        cfg = synth.SynthConfig("t", 30, read_len=600, sub_size="poisson5", indel_frac=0.2, seed=seed)
+    elif kind == "len90":
+        cfg = synth.SynthConfig("t", 300, read_len=90, sub_size="fixed8", seed=seed)
+    elif kind == "deep":     # > 64 reads per subfamily without insertions
+        cfg = synth.SynthConfig("t", 4, sub_size="loguniform", logu_lo=65, logu_hi=200, n_loci=1, seed=seed)
     else:
         cfg = synth.SynthConfig("t", 200, sub_size="poisson5", indel_frac=0.5, softclip_frac=0.3, seed=seed)
     packed = synth.packed_from_records(cfg)

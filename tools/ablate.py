@@ -1,0 +1,45 @@
+"""Diagnostic: time the kernels of several libdcr builds (ablation variants
+built with -DDCR_ABL=n) on one HBM-resident batch, interleaved in one process."""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402,F401
+
+from duplexumiconsensusreads_amd import synth  # noqa: E402
+from duplexumiconsensusreads_amd.device import DeviceBatch  # noqa: E402
+from duplexumiconsensusreads_amd.params import ConsensusParams, build_dcr_params  # noqa: E402
+
+libs = sys.argv[2:]
+nfam = int(sys.argv[1])
+packed = synth.packed_fixed_size(nfam, seed=3)
+db = DeviceBatch(packed)
+P = build_dcr_params(ConsensusParams())
+handles = []
+for path in libs:
+    lib = ctypes.CDLL(path)
+    lib.dcr_create.restype = ctypes.c_void_p
+    lib.dcr_create.argtypes = [ctypes.c_int, ctypes.c_void_p]
+    for n in ("dcr_run_batch", "dcr_sync", "dcr_last_timing"):
+        getattr(lib, n).restype = ctypes.c_int
+    lib.dcr_run_batch.argtypes = [ctypes.c_void_p] * 4
+    lib.dcr_sync.argtypes = [ctypes.c_void_p]
+    lib.dcr_last_timing.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    ctx = lib.dcr_create(0, ctypes.byref(P))
+    handles.append((path, lib, ctx))
+res = {p: [] for p in libs}
+for rnd in range(6):
+    for path, lib, ctx in handles:
+        assert lib.dcr_run_batch(ctx, ctypes.byref(db.batch_struct), ctypes.byref(db.ss_struct),
+                                 ctypes.byref(db.ds_struct)) == 0
+        assert lib.dcr_sync(ctx) in (0, 3)
+        ms = (ctypes.c_float * 4)()
+        lib.dcr_last_timing(ctx, ms)
+        if rnd:
+            res[path].append((ms[1], ms[2]))
+for path in libs:
+    v = res[path]
+    ss = sorted(x[0] for x in v)[len(v) // 2]
+    ds = sorted(x[1] for x in v)[len(v) // 2]
+    print(f"{os.path.basename(path):24s} single-strand {ss:8.3f} ms  duplex {ds:8.3f} ms")
