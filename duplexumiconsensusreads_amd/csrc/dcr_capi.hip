@@ -11,33 +11,7 @@
 #include <cstring>
 #include <string>
 
-#include "../../include/dcr.h"
-
-namespace dcr {
-struct Workspace {
-    dcr_read_info *info;
-    uint32_t *norm_cig;
-    int32_t *cons;
-    double *et;
-    uint8_t *insflag;
-    int4 *state;
-    int *err;
-    int *ovf;
-    int *ovf_count;
-};
-struct Args {
-    dcr_batch in;
-    const dcr_params *P;
-    Workspace ws;
-    dcr_out ss;
-    dcr_out ds;
-    int64_t n_rec;
-    int fast_ok;
-};
-__global__ void k_prep(dcr_batch in, const dcr_params *P, Workspace ws);
-template <bool DUPLEX> __global__ void k_consensus_fast(Args a);
-template <bool DUPLEX> __global__ void k_consensus_general(Args a);
-}  // namespace dcr
+#include "dcr_internal.h"
 
 namespace {
 thread_local std::string g_err;
@@ -87,6 +61,7 @@ struct dcr_ctx {
     int64_t last_reads = 0;
     bool timed = false;
     int fast_ok = 0;    // all likelihood factors in [0, 1]: the fast kernel's finalize applies
+    int n_cu = 256;     // compute units (persistent grid size)
 };
 
 static int factors_unit(const dcr_params *p) {
@@ -134,6 +109,7 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
         return nullptr;
     }
     for (auto &e : c->ev) (void)hipEventCreate(&e);
+    (void)hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device);
     c->fast_ok = factors_unit(params);
     if (hipMemcpy(c->d_params, params, sizeof(dcr_params), hipMemcpyHostToDevice) != hipSuccess) {
         fail(DCR_EHIP, "params upload failed");
@@ -180,8 +156,11 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     const size_t o_et = o;   o = align_up(o + sizeof(double) * (size_t)std::max<int64_t>(cols, 1));
     const size_t o_ins = o;  o = align_up(o + (size_t)std::max<int64_t>(s->ss_cols, 1));
     const size_t o_st = o;   o = align_up(o + sizeof(int4) * (size_t)std::max<int64_t>(s->n_reads, 1));
-    const size_t o_err = o;  o = align_up(o + 16);
-    const size_t o_ovf = o;  o = align_up(o + sizeof(int) * (size_t)std::max<int64_t>(4LL * s->n_fam, 1));
+    const size_t o_err = o;  o = align_up(o + 32);
+    const size_t n_rec = (size_t)std::max<int64_t>(4LL * s->n_fam, 1);
+    const size_t o_ovf = o;  o = align_up(o + sizeof(int) * n_rec);
+    const size_t o_meta = o; o = align_up(o + sizeof(dcr::RecMeta) * n_rec);
+    const size_t o_rm = o;   o = align_up(o + sizeof(uint2) * std::max<size_t>((size_t)s->n_reads, n_rec));
     if (o > c->ws.cap) {
         HIP_TRY(hipStreamSynchronize(c->stream));
         HIP_TRY(c->ws.ensure(o + o / 8));
@@ -194,8 +173,11 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     c->w.insflag = (uint8_t *)(b + o_ins);
     c->w.state = (int4 *)(b + o_st);
     c->w.err = (int *)(b + o_err);
-    c->w.ovf_count = (int *)(b + o_err) + 1;     // err, ovf_count[2] share one 16-byte block
+    c->w.ovf_count = (int *)(b + o_err) + 1;     // err, ovf_count[2], fast_count[2]: one 32-byte block
+    c->w.fast_count = (int *)(b + o_err) + 3;
     c->w.ovf = (int *)(b + o_ovf);
+    c->w.meta = (dcr::RecMeta *)(b + o_meta);
+    c->w.rmeta = (uint2 *)(b + o_rm);
     return DCR_OK;
 }
 
@@ -205,7 +187,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     int rc = dcr_reserve(c, in);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMemsetAsync(c->w.err, 0, 16, c->stream));
+    HIP_TRY(hipMemsetAsync(c->w.err, 0, 32, c->stream));
     c->last_reads = in->n_reads;
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     if (in->n_reads > 0) {
@@ -223,26 +205,38 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     a.ss = *ss;
     a.ds = *ds;
     a.fast_ok = c->fast_ok;
-    // fast kernel over every record, then the persistent general kernel over
-    // the records it handed over (insertions, > 64 reads, wide layouts)
-    auto general_grid = [](int64_t n_rec) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_rec + 3) / 4, 1024)); };
-    if (in->n_fam > 0) {
-        a.n_rec = 4LL * in->n_fam;
-        hipLaunchKernelGGL(dcr::k_consensus_fast<false>, dim3((unsigned)((a.n_rec + 3) / 4)), dim3(256), 0,
-                           c->stream, a);
+    // per strand: k_recmeta classifies every record (fast list / general list /
+    // status written), then the fast kernel (8 records per wave) drains the fast list and
+    // the persistent general kernel the rest (insertions, > 64 reads, wide layouts)
+    auto grid_for = [&](int64_t n_rec, unsigned cap) {
+        return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_rec + 3) / 4, cap));
+    };
+    constexpr int kFastChunk = 8;                 // records per wave (dcr_kernels.hip)
+    auto fast_grid = [&](int64_t n_rec) {
+        return (unsigned)std::max<int64_t>(1, (n_rec + 4 * kFastChunk - 1) / (4 * kFastChunk));
+    };
+    auto strand = [&](bool duplex) -> int {
+        a.n_rec = (duplex ? 2LL : 4LL) * in->n_fam;
+        const unsigned nb = (unsigned)((a.n_rec + 255) / 256);    // k_recmeta: 64 records per wave
+        if (duplex) {
+            hipLaunchKernelGGL(dcr::k_recmeta<true>, dim3(nb), dim3(256), 0, c->stream, a);
+            hipLaunchKernelGGL(dcr::k_consensus_fast<true>, dim3(fast_grid(a.n_rec)), dim3(256), 0,
+                               c->stream, a);
+            hipLaunchKernelGGL(dcr::k_consensus_general<true>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
+                               c->stream, a);
+        } else {
+            hipLaunchKernelGGL(dcr::k_recmeta<false>, dim3(nb), dim3(256), 0, c->stream, a);
+            hipLaunchKernelGGL(dcr::k_consensus_fast<false>, dim3(fast_grid(a.n_rec)), dim3(256), 0,
+                               c->stream, a);
+            hipLaunchKernelGGL(dcr::k_consensus_general<false>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
+                               c->stream, a);
+        }
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(dcr::k_consensus_general<false>, dim3(general_grid(a.n_rec)), dim3(256), 0, c->stream, a);
-        HIP_TRY(hipGetLastError());
-    }
+        return DCR_OK;
+    };
+    if (in->n_fam > 0 && (rc = strand(false))) return rc;
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-    if (in->n_fam > 0) {
-        a.n_rec = 2LL * in->n_fam;
-        hipLaunchKernelGGL(dcr::k_consensus_fast<true>, dim3((unsigned)((a.n_rec + 3) / 4)), dim3(256), 0,
-                           c->stream, a);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(dcr::k_consensus_general<true>, dim3(general_grid(a.n_rec)), dim3(256), 0, c->stream, a);
-        HIP_TRY(hipGetLastError());
-    }
+    if (in->n_fam > 0 && (rc = strand(true))) return rc;
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     c->timed = true;
     return DCR_OK;

@@ -1,0 +1,57 @@
+// dcr_internal.h — types shared by dcr_kernels.hip and dcr_capi.hip (not part
+// of the C-ABI; include/dcr.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dcr.h"
+
+namespace dcr {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = kWave * kWavesPerBlock;
+
+// Per-record launch metadata written by k_recmeta for the fast kernel, in
+// fast-list order (one scalar 32-byte load per record).
+struct RecMeta {
+    int64_t base_al;    // 4-aligned byte offset of the record's kept bases/quals
+    int64_t off;        // output column offset (ss_col_off / ds_col_off)
+    int32_t rec;        // record index
+    int32_t g0;         // index of its first read in the read-meta array
+    int32_t minpos;     // min_pos (:458)
+    uint32_t w;         // R | T << 7 | staged dwords << 15
+};
+static_assert(sizeof(RecMeta) == 32, "RecMeta is one s_load_dwordx8");
+
+struct Workspace {
+    dcr_read_info *info;    // [n_reads]
+    uint32_t *norm_cig;     // [n_cigar] normalised runs (M/I/D)
+    int32_t *cons;          // [cols] consensus char | quality << 8 (T > kColsLds)
+    double *et;             // [cols] e/d per kept column        (T > kColsLds)
+    uint8_t *insflag;       // [ss cols] insertion-column flags (R > 64 layout)
+    int4 *state;            // [n_reads] layout state (R > 64)
+    int *err;               // [1] capacity error flag
+    int *ovf;               // [n_rec] records for the general kernel
+    int *ovf_count;         // [2] single-strand / duplex general-list lengths
+    int *fast_count;        // [2] single-strand / duplex fast-list lengths
+    RecMeta *meta;          // [n_rec] fast list
+    uint2 *rmeta;           // [max(n_reads, 4F)] per read: col | len << 8 | mapq << 16, stage offset
+};
+
+struct Args {
+    dcr_batch in;
+    const dcr_params *P;
+    Workspace ws;
+    dcr_out ss;
+    dcr_out ds;
+    int64_t n_rec;
+    int fast_ok;            // every LUT factor in [0, 1] (host-checked): fast kernel allowed
+};
+
+__global__ void k_prep(dcr_batch in, const dcr_params *P, Workspace ws);
+template <bool DUPLEX> __global__ void k_recmeta(Args a);
+template <bool DUPLEX> __global__ void k_consensus_fast(Args a);
+template <bool DUPLEX> __global__ void k_consensus_general(Args a);
+
+}  // namespace dcr

@@ -26,10 +26,7 @@
 // plus one chain per distinct class actually observed, and the wave pays only
 // for the largest number of distinct classes among its 64 columns (usually
 // one or two) instead of six.  Results are bit-identical to the six chains.
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-
-#include "../../include/dcr.h"
+#include "dcr_internal.h"
 
 #ifndef DCR_ABL
 #define DCR_ABL 0   // diagnostic builds only (tools/ablate.py): 1 setup, 2 +accumulate, 3 +finalize
@@ -37,9 +34,6 @@
 
 namespace dcr {
 
-constexpr int kWave = 64;
-constexpr int kWavesPerBlock = 4;
-constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kStageElems = 2048;        // per-wave LDS staging (16-bit codes)
 constexpr int kTileIns = 32;             // column tile of the insertion layout
 constexpr int kFastMaxT = 240;           // pairwise_small: both halves <= 128
@@ -50,28 +44,6 @@ constexpr int kColsLds = 256;            // per-wave LDS column scratch
 constexpr uint32_t kPad = (6u << 9) | 2u;          // 'N' with quality 2 (:509-510, :543-544)
 constexpr uint32_t kPlus = (4u << 9) | DCR_LUT_PLUS;
 constexpr uint32_t kDel = (5u << 9) | DCR_LUT_DEL;
-
-struct Workspace {
-    dcr_read_info *info;    // [n_reads]
-    uint32_t *norm_cig;     // [n_cigar] normalised runs (M/I/D)
-    int32_t *cons;          // [cols] consensus char | quality << 8 (T > kColsLds)
-    double *et;             // [cols] e/d per kept column        (T > kColsLds)
-    uint8_t *insflag;       // [ss cols] insertion-column flags (R > 64 layout)
-    int4 *state;            // [n_reads] layout state (R > 64)
-    int *err;               // [1] capacity error flag
-    int *ovf;               // [n_rec] records the fast kernel hands to the general one
-    int *ovf_count;         // [2] single-strand / duplex overflow counts
-};
-
-struct Args {
-    dcr_batch in;
-    const dcr_params *P;
-    Workspace ws;
-    dcr_out ss;
-    dcr_out ds;
-    int64_t n_rec;
-    int fast_ok;            // every LUT factor in [0, 1] (host-checked): fast kernel allowed
-};
 
 struct WaveLds {
     uint16_t pad_code[4];                  // [0] = kPad: sentinel the fast layout loads outside a read (8 B keeps stage 8-aligned)
@@ -1102,12 +1074,18 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
 // doubles to the reference's six chains.
 // element code of read r at column t; outside the read's span the load is
 // redirected to the kPad sentinel (selecting the address, not the loaded
-// value, keeps the bounds mask out of VCC while the LDS read is in flight)
-__device__ __forceinline__ uint32_t fast_elem(const LaneReads &lr, int r, int t, bool live, const uint16_t *stage) {
-    const int cl = readlane(lr.cl, r);
-    const int so = readlane(lr.sn, r);
-    const int j = t - (cl & 0xffff);
-    const bool inb = live && (unsigned)j < ((unsigned)cl >> 16);
+// value, keeps the bounds mask out of VCC while the LDS read is in flight).
+// No column bound is needed: every read ends at or before T (T = max end).
+struct FastReads {
+    int x;      // lane r: first column | kept length << 8 | mapq << 16
+    int y;      // lane r: stage offset of its first kept base
+};
+
+__device__ __forceinline__ uint32_t fast_elem(const FastReads &fr, int r, int t, const uint16_t *stage) {
+    const int x = readlane(fr.x, r);
+    const int so = readlane(fr.y, r);
+    const int j = t - (x & 0xff);
+    const bool inb = (unsigned)j < (((unsigned)x >> 8) & 0xffu);
     return stage[inb ? so + j : -4];             // stage[-4] = pad_code[0]
 }
 
@@ -1129,14 +1107,14 @@ __device__ __forceinline__ void fast_mul(double &U, double (&s)[4], int (&n)[4],
 // readlane is convergent and blocks the compiler's runtime unrolling)
 template <int NS>
 __device__ __forceinline__ void fast_products(double &U, double (&s)[4], int (&n)[4], const int (&k)[4], int R,
-                                              int t, bool live, const LaneReads &lr, const uint16_t *stage,
+                                              int t, const FastReads &fr, const uint16_t *stage,
                                               const double2 *lut) {
     int r = 0;
     for (; r + 4 <= R; r += 4) {
-        const uint32_t e0 = fast_elem(lr, r, t, live, stage);
-        const uint32_t e1 = fast_elem(lr, r + 1, t, live, stage);
-        const uint32_t e2 = fast_elem(lr, r + 2, t, live, stage);
-        const uint32_t e3 = fast_elem(lr, r + 3, t, live, stage);
+        const uint32_t e0 = fast_elem(fr, r, t, stage);
+        const uint32_t e1 = fast_elem(fr, r + 1, t, stage);
+        const uint32_t e2 = fast_elem(fr, r + 2, t, stage);
+        const uint32_t e3 = fast_elem(fr, r + 3, t, stage);
         const double2 f0 = lut[e0 & 511], f1 = lut[e1 & 511], f2 = lut[e2 & 511], f3 = lut[e3 & 511];
         fast_mul<NS>(U, s, n, k, e0, f0);
         fast_mul<NS>(U, s, n, k, e1, f1);
@@ -1144,7 +1122,7 @@ __device__ __forceinline__ void fast_products(double &U, double (&s)[4], int (&n
         fast_mul<NS>(U, s, n, k, e3, f3);
     }
     for (; r < R; ++r) {
-        const uint32_t e = fast_elem(lr, r, t, live, stage);
+        const uint32_t e = fast_elem(fr, r, t, stage);
         fast_mul<NS>(U, s, n, k, e, lut[e & 511]);
     }
 }
@@ -1180,9 +1158,8 @@ __device__ __forceinline__ double pairwise_small(const double *a, int n, int lan
     for (int i = 1; i < 16; ++i)
         if (8 * i < body) r += v[i];
     // per block: ((r0+r1)+(r2+r3)) + ((r4+r5)+(r6+r7)), then the tail in order
-    const double p01 = r + __shfl_xor(r, 1);                 // lanes 8b+0/1 hold r0+r1 ...
+    const double p01 = r + __shfl_xor(r, 1);
     const double p0123 = p01 + __shfl_xor(p01, 2);
-    // careful: the association must be ((r0+r1)+(r2+r3)) + ((r4+r5)+(r6+r7))
     const double s8 = p0123 + __shfl_xor(p0123, 4);
     double res[2];
 #pragma unroll
@@ -1197,121 +1174,309 @@ __device__ __forceinline__ double pairwise_small(const double *a, int n, int lan
     return nb == 1 ? res[0] : res[0] + res[1];
 }
 
-template <bool DUPLEX>
-__device__ __forceinline__ void process_fast(const Args &a, const int64_t rec, WaveLds &W, const double2 *s_lut,
-                                             const double *s_qthr, const int lane) {
-    const dcr_params *P = a.P;
-    const dcr_out &O = DUPLEX ? a.ds : a.ss;
-    const int64_t *col_off = DUPLEX ? a.in.ds_col_off : a.in.ss_col_off;
-    const int64_t off = col_off[rec];
-    const int64_t cap = col_off[rec + 1] - off;
-    const int minbq = P->min_base_quality;
-    const bool simple_q = P->error_rate_pre_labeling == 0 && P->error_rate_post_labeling == 0;
-    const int R = DUPLEX ? 2 : (a.in.sub_off[rec + 1] - a.in.sub_off[rec]);
+// ------------------------------------------------------------ k_recmeta
+// Classifies every record before any consensus work: the status the reference
+// reaches first (a read that failed preprocessing, or an empty read — :1291-1300
+// via the read statuses of k_prep), a fast record, or a general one.  For fast
+// records it writes the launch metadata the fast kernel fetches with one scalar
+// load per record plus one 8-byte load per read.
+//
+// One wave per 64 records.  Reads are visited lane = read (coalesced loads) and
+// folded into their record's LDS slot with LDS atomics; the record of a read
+// comes from a marker per record start and a DPP prefix-max scan.  List appends
+// are wave-aggregated (one global atomic per wave per list).
+struct RdLite {
+    int pos, len, ncig, status, mapq;
+    int64_t seq_start;
+    uint32_t cig0;
+};
 
+template <bool DUPLEX, bool CIG>
+__device__ __forceinline__ RdLite rd_lite(const Args &a, int64_t k) {
+    RdLite r;
+    r.cig0 = 0;
+    if (!DUPLEX) {                              // k: read index
+        const dcr_read_info inf = a.ws.info[k];
+        r.pos = a.in.read_pos[k];
+        r.len = inf.len;
+        r.ncig = inf.n_cig;
+        r.status = inf.status;
+        r.mapq = a.in.read_mapq[k];
+        r.seq_start = inf.seq_start;
+        if (CIG && r.ncig == 1 && r.len > 0) r.cig0 = a.ws.norm_cig[a.in.cig_off[k]];
+    } else {                                    // k: single-strand record index
+        r.pos = a.ss.pos[k];
+        r.len = a.ss.len[k];
+        r.ncig = a.ss.n_cig[k];
+        r.status = a.ss.status[k];
+        r.mapq = a.ss.mapq[k];
+        r.seq_start = a.in.ss_col_off[k];
+        if (CIG && r.status == 0 && r.ncig == 1 && r.len > 0) r.cig0 = a.ss.cigar[r.seq_start];
+    }
+    return r;
+}
+
+__device__ __forceinline__ void write_status_at(const dcr_out &O, int64_t rec, int st) {
+    O.status[rec] = (uint8_t)st;
+    O.pos[rec] = 0;
+    O.mapq[rec] = 0;
+    O.len[rec] = 0;
+    O.n_cig[rec] = 0;
+    O.n_de[rec] = 0;
+    O.D[rec] = 0;
+    O.M[rec] = 0;
+    O.E[rec] = 0.0;
+}
+
+// wave-local LDS ordering: a wave's DS instructions execute in order, so only
+// the compiler must be kept from reordering (no vmcnt drain of prefetches)
+__device__ __forceinline__ void lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// inclusive prefix max over the wave (DPP row shifts, then row broadcasts)
+__device__ __forceinline__ int wave_scan_max(int v) {
+    constexpr int I = -0x7fffffff - 1;
+    v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x111, 0xF, 0xF, false));   // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x112, 0xF, 0xF, false));   // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x114, 0xF, 0xF, false));   // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x118, 0xF, 0xF, false));   // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x142, 0xA, 0xF, false));   // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x143, 0xC, 0xF, false));   // row_bcast:31
+    return v;
+}
+
+// record (wave lane) owning read c + lane; records are contiguous runs of reads
+__device__ __forceinline__ int read_record(int64_t c, int g0, int R, int *mark, int lane, int &carry) {
+    mark[lane] = -1;
+    lds_fence();
+    if (R > 0 && g0 >= c && g0 < c + kWave) atomicMax(&mark[g0 - c], lane);
+    lds_fence();
+    const int k = max(wave_scan_max(mark[lane]), carry);
+    carry = readlane(k, 63);
+    return k;
+}
+
+struct RecAgg {
+    int minpos, maxend, flags, kind;
+    unsigned long long lo, hi;     // kept byte window; lo becomes base_al for fast records
+};
+
+template <bool DUPLEX>
+__global__ __launch_bounds__(256) void k_recmeta(Args a) {
+    __shared__ RecAgg s_agg[kWavesPerBlock][kWave];
+    __shared__ int s_mark[kWavesPerBlock][kWave];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    RecAgg *agg = s_agg[wave];
+    int *mark = s_mark[wave];
+    const int64_t rb = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kWave;
+    if (rb >= a.n_rec) return;
+    const int64_t rk = rb + lane;
+    const bool vk = rk < a.n_rec;
+    const int64_t rend = min(rb + kWave, a.n_rec);
+    int g0 = 0, R = 0;
+    int64_t gbeg, gend;
+    if (!DUPLEX) {
+        if (vk) {
+            g0 = a.in.sub_off[rk];
+            R = a.in.sub_off[rk + 1] - g0;
+        }
+        gbeg = a.in.sub_off[rb];
+        gend = a.in.sub_off[rend];
+    } else {
+        g0 = (int)(2 * rk);                     // pair p uses single-strand records 2p, 2p+1 (:1575-1576)
+        R = vk ? 2 : 0;
+        gbeg = 2 * rb;
+        gend = 2 * rend;
+    }
+    agg[lane] = RecAgg{0x7fffffff, -0x7fffffff, 0, -1, ~0ull, 0ull};
+    lds_fence();
+    // pass 1: fold every read into its record
+    int carry = -1;
+    for (int64_t c = gbeg; c < gend; c += kWave) {
+        const int k = read_record(c, g0, R, mark, lane, carry);
+        const int64_t gr = c + lane;
+        if (gr < gend) {
+            const RdLite rd = rd_lite<DUPLEX, true>(a, gr);
+            const int fl = (rd.status != 0) | ((rd.len <= 0) << 1) |
+                           ((rd.ncig != 1 || (rd.len > 0 && (rd.cig0 & 15u) != 0)) << 2);   // single M run only
+            atomicMin(&agg[k].minpos, rd.pos);
+            atomicMax(&agg[k].maxend, rd.pos + rd.len);
+            if (fl) atomicOr(&agg[k].flags, fl);
+            atomicMin(&agg[k].lo, (unsigned long long)rd.seq_start);
+            atomicMax(&agg[k].hi, (unsigned long long)(rd.seq_start + rd.len));
+        }
+    }
+    lds_fence();
+    // per record: lane = record
+    int kind = -1;                               // 0 fast, 1 general, -1 finished here
+    RecMeta m{};
+    if (vk) {
+        const dcr_out &O = DUPLEX ? a.ds : a.ss;
+        const int64_t *col_off = DUPLEX ? a.in.ds_col_off : a.in.ss_col_off;
+        const uint8_t *gb = DUPLEX ? a.ss.seq : a.in.bases;
+        const uint8_t *gq = DUPLEX ? a.ss.qual : a.in.quals;
+        const RecAgg g = agg[lane];
+        int st = -1;
+        if (R == 0) st = DCR_ST_UPSTREAM;
+        else if (R > kWave) kind = 1;
+        else if (g.flags & 1) st = DCR_ST_UPSTREAM;
+        else if (g.flags & 2) st = DCR_ST_TYPE_ERROR;
+        else {
+            const int T = g.maxend - g.minpos;
+            const int64_t off = col_off[rk];
+            const int64_t cap = col_off[rk + 1] - off;
+            const int64_t base_al = (int64_t)g.lo & ~(int64_t)3;
+            const int64_t span = (int64_t)g.hi - base_al;
+            const bool aligned = ((((uintptr_t)gb) | ((uintptr_t)gq)) & 3) == 0;
+            if ((g.flags & 4) || !aligned || span > kStageElems || T > kFastMaxT || T > cap || !a.fast_ok) {
+                kind = 1;
+            } else {
+                kind = 0;
+                m.base_al = base_al;
+                m.off = off;
+                m.rec = (int32_t)rk;
+                m.g0 = g0;
+                m.minpos = g.minpos;
+                m.w = (uint32_t)R | ((uint32_t)T << 7) | ((uint32_t)((span + 3) >> 2) << 15);
+                agg[lane].lo = (unsigned long long)base_al;
+            }
+        }
+        agg[lane].kind = kind;
+        if (st >= 0) write_status_at(O, rk, st);
+    }
+    const uint64_t bf = __ballot(kind == 0);
+    const uint64_t bg = __ballot(kind == 1);
+    int basef = 0, baseg = 0;
+    if (lane == 0) {
+        if (bf) basef = atomicAdd(&a.ws.fast_count[DUPLEX ? 1 : 0], __popcll(bf));
+        if (bg) baseg = atomicAdd(&a.ws.ovf_count[DUPLEX ? 1 : 0], __popcll(bg));
+    }
+    basef = __shfl(basef, 0);
+    baseg = __shfl(baseg, 0);
+    const uint64_t lt = lanemask_lt(lane);
+    if (kind == 0) a.ws.meta[basef + __popcll(bf & lt)] = m;
+    if (kind == 1) a.ws.ovf[baseg + __popcll(bg & lt)] = (int)rk;
+    if (!bf) return;
+    lds_fence();
+    // pass 2: per-read metadata of fast records
+    carry = -1;
+    for (int64_t c = gbeg; c < gend; c += kWave) {
+        const int k = read_record(c, g0, R, mark, lane, carry);
+        const int64_t gr = c + lane;
+        if (gr < gend && agg[k].kind == 0) {
+            const RdLite rd = rd_lite<DUPLEX, false>(a, gr);
+            const int minpos = agg[k].minpos;
+            const int64_t base_al = (int64_t)agg[k].lo;
+            a.ws.rmeta[gr] = make_uint2((uint32_t)(rd.pos - minpos) | ((uint32_t)rd.len << 8) |
+                                            ((uint32_t)rd.mapq << 16),
+                                        (uint32_t)(rd.seq_start - base_al));
+        }
+    }
+}
+
+// ------------------------------------------------------- fast kernel body
+constexpr int kStageDw = kStageElems / 4 / kWave;   // staged dwords per lane
+
+struct FastStage {
+    uint32_t vb[kStageDw], vq[kStageDw];   // raw base / quality dwords
+    uint2 rm;                              // this lane's read meta (lane < R)
+};
+
+// issue a record's loads (consumed by the next process_fast call)
+template <bool DUPLEX>
+__device__ __forceinline__ void fast_load(const Args &a, const RecMeta &m, int lane, FastStage &st) {
     const uint8_t *gb = DUPLEX ? a.ss.seq : a.in.bases;
     const uint8_t *gq = DUPLEX ? a.ss.qual : a.in.quals;
-    int64_t lo_byte, hi_byte;
-    if (!DUPLEX) {
-        const int g0 = a.in.sub_off[rec];
-        lo_byte = R > 0 ? a.in.seq_off[g0] : 0;
-        hi_byte = R > 0 ? a.in.seq_off[g0 + R - 1] + a.in.seq_len[g0 + R - 1] : 0;
-    } else {
-        lo_byte = a.in.ss_col_off[2 * rec];
-        hi_byte = a.in.ss_col_off[2 * rec + 1] + a.ss.len[2 * rec + 1];
-    }
-    const int64_t base_al = lo_byte & ~(int64_t)3;
-    const int64_t span = hi_byte - base_al;
-    const bool fits = R <= kWave && span <= kStageElems && ((((uintptr_t)gb) | ((uintptr_t)gq)) & 3) == 0;
-    constexpr int kStageDw = kStageElems / 4 / kWave;
-    uint32_t vb[kStageDw], vq[kStageDw];
-    const int nd = fits ? (int)((span + 3) >> 2) : 0;
-    {
-        const uint32_t *b4 = (const uint32_t *)(gb + base_al);
-        const uint32_t *q4 = (const uint32_t *)(gq + base_al);
+    const int nd = (int)(m.w >> 15);
+    const uint32_t *b4 = (const uint32_t *)(gb + m.base_al);
+    const uint32_t *q4 = (const uint32_t *)(gq + m.base_al);
 #pragma unroll
-        for (int u = 0; u < kStageDw; ++u) {
-            const int d = u * kWave + lane;
-            vb[u] = d < nd ? b4[d] : 0u;
-            vq[u] = d < nd ? q4[d] : 0u;
-        }
+    for (int u = 0; u < kStageDw; ++u) {
+        const int d = u * kWave + lane;
+        st.vb[u] = d < nd ? b4[d] : 0u;
+        st.vq[u] = d < nd ? q4[d] : 0u;
     }
+    const int R = (int)(m.w & 127u);
+    st.rm = lane < R ? a.ws.rmeta[m.g0 + lane] : make_uint2(0u, 0u);
+}
 
-    // setup: lane = read (R <= 64 here, else handed over)
-    int minpos = 0x7fffffff, maxend = -0x7fffffff, up = 0, empty = 0, other = 0, msum = 0;
-    ReadRef myrd{};
-    if (lane < R) {
-        myrd = get_read<DUPLEX>(a, rec, lane);
-        up = myrd.status != 0;
-        empty = myrd.len <= 0;
-        minpos = myrd.pos;
-        maxend = myrd.pos + myrd.len;
-        msum = myrd.mapq;
-        // single M run only (no I / D anywhere in the record)
-        other = myrd.ncig != 1 || (myrd.len > 0 && (myrd.cig[0] & 15) != 0);
-    }
-    minpos = wave_min(minpos);
-    maxend = wave_max(maxend);
-    up = __ballot(up) != 0;
-    empty = __ballot(empty) != 0;
-    other = __ballot(other) != 0;
-    msum = wave_sum(msum);
+// four element codes (q | class << 9) from four bases and qualities, SWAR:
+// the class comes from a byte permute indexed by (b >> 1) & 7, which is
+// distinct for A C T G N; a second permute returns the letter each index
+// stands for, and any byte that differs from it is an invalid character
+// (class 7, :582).  Single-strand inputs then mask qual < min_base_quality to
+// class 6 ('N', keeping the quality: mask_low_quality_bases :280).
+typedef short dcr_v2i16 __attribute__((ext_vector_type(2)));
 
-    auto write_status = [&](int st) {
-        if (lane == 0) {
-            O.status[rec] = (uint8_t)st;
-            O.pos[rec] = 0;
-            O.mapq[rec] = 0;
-            O.len[rec] = 0;
-            O.n_cig[rec] = 0;
-            O.n_de[rec] = 0;
-            O.D[rec] = 0;
-            O.M[rec] = 0;
-            O.E[rec] = 0.0;
-        }
-    };
-    if (R == 0 || (R <= kWave && up)) { write_status(DCR_ST_UPSTREAM); return; }
-    if (R <= kWave && empty) { write_status(DCR_ST_TYPE_ERROR); return; }
-    const int T = maxend - minpos;
-    if (R > kWave || other || !fits || T > kFastMaxT || T > cap || !a.fast_ok) {
-        if (lane == 0) {                      // general kernel takes it
-            const int idx = atomicAdd(&a.ws.ovf_count[DUPLEX ? 1 : 0], 1);
-            a.ws.ovf[idx] = (int)rec;
-        }
-        return;
+template <bool DUPLEX>
+__device__ __forceinline__ uint2 make_codes4(uint32_t B, uint32_t Q, uint32_t m2) {
+    const uint32_t h = (B >> 1) & 0x07070707u;
+    uint32_t cls = __builtin_amdgcn_perm(0x06070707u, 0x03010200u, h);       // A0 C2 T1 G3 . . . N6
+    const uint32_t x = B ^ __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, h);
+    const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;   // 0x80 where byte != letter
+    cls |= ((nz << 1) - (nz >> 7)) & 0x07070707u;
+    if (!DUPLEX) {
+        const dcr_v2i16 qe = __builtin_bit_cast(dcr_v2i16, Q & 0x00FF00FFu);
+        const dcr_v2i16 qo = __builtin_bit_cast(dcr_v2i16, (Q >> 8) & 0x00FF00FFu);
+        const dcr_v2i16 mm = __builtin_bit_cast(dcr_v2i16, m2);
+        const uint32_t de = __builtin_bit_cast(uint32_t, (dcr_v2i16)(qe - mm));
+        const uint32_t dd = __builtin_bit_cast(uint32_t, (dcr_v2i16)(qo - mm));
+        const uint32_t lt = ((de >> 15) & 0x00010001u) | ((dd >> 7) & 0x01000100u);   // 1 where q < min_bq
+        const uint32_t ff = (lt << 8) - lt;
+        cls = (ff & 0x06060606u) | (cls & ~ff);
     }
+    const uint32_t c2 = cls << 1;
+    return make_uint2(__builtin_amdgcn_perm(c2, Q, 0x05010400u), __builtin_amdgcn_perm(c2, Q, 0x07030602u));
+}
+
+struct FastParams {
+    uint32_t m2;          // min_base_quality clamped to [0, 256], both 16-bit halves
+    int maxq;
+    bool simple_q;
+    double pre, post, thr;
+};
+
+
+template <bool DUPLEX>
+__device__ __forceinline__ void process_fast(const Args &a, const FastParams &fp, const RecMeta &m, FastStage &st,
+                                             const bool has_next, const RecMeta &mn, WaveLds &W,
+                                             const double2 *s_lut, const double *s_qthr, const int lane) {
+    const dcr_out &O = DUPLEX ? a.ds : a.ss;
+    const int64_t rec = m.rec;
+    const int64_t off = m.off;
+    const int R = (int)(m.w & 127u);
+    const int T = (int)((m.w >> 7) & 255u);
+    const int nd = (int)(m.w >> 15);
+    const int minpos = m.minpos;
 
     // phase 0: element codes into LDS
 #pragma unroll
     for (int u = 0; u < kStageDw; ++u) {
         const int d = u * kWave + lane;
-        if (d < nd) {
-            uint32_t cc[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                cc[k] = make_code<DUPLEX>((vb[u] >> (8 * k)) & 255u, (vq[u] >> (8 * k)) & 255u, minbq);
-            uint2 w;
-            w.x = cc[0] | (cc[1] << 16);
-            w.y = cc[2] | (cc[3] << 16);
-            *(uint2 *)&W.stage[4 * d] = w;
-        }
+        if (d < nd) *(uint2 *)&W.stage[4 * d] = make_codes4<DUPLEX>(st.vb[u], st.vq[u], fp.m2);
     }
-    LaneReads lr;
-    lr.cl = (myrd.pos - minpos) | (myrd.len << 16);
-    lr.sn = (int)(myrd.seq_start - base_al);
-    if (lane == 0) W.pad_code[0] = (uint16_t)kPad;
-    wave_fence();
+    FastReads fr;
+    fr.x = (int)st.rm.x;
+    fr.y = (int)st.rm.y;
+    const int msum = wave_sum(lane < R ? (fr.x >> 16) & 255 : 0);
+    // prefetch the next record; its loads complete under this record's work
+    if (has_next) fast_load<DUPLEX>(a, mn, lane, st);
+    lds_fence();
     if (DCR_ABL == 1) {
-        if (lane == 0) O.pos[rec] = minpos + nd + (int)W.stage[lane];
+        if (lane == 0) O.pos[rec] = minpos + nd + (int)W.stage[lane] + msum;
         return;
     }
 
+    auto write_status = [&](int s) {
+        if (lane == 0) write_status_at(O, rec, s);
+    };
     uint16_t *od = O.d + off;
     uint16_t *oe = O.e + off;
     int dmax = -1, dmin = 0x7fffffff, first = -1, last = -1;
     bool bad = false, qoverflow = false;
-    const double pre = (double)P->error_rate_pre_labeling;
-    const double post = (double)P->error_rate_post_labeling;
 
     for (int c0 = 0; c0 < T; c0 += kWave) {
         const int t = c0 + lane;
@@ -1321,23 +1486,23 @@ __device__ __forceinline__ void process_fast(const Args &a, const int64_t rec, W
         {
             int r = 0;
             for (; r + 4 <= R; r += 4) {
-                const uint32_t e0 = fast_elem(lr, r, t, live, W.stage);
-                const uint32_t e1 = fast_elem(lr, r + 1, t, live, W.stage);
-                const uint32_t e2 = fast_elem(lr, r + 2, t, live, W.stage);
-                const uint32_t e3 = fast_elem(lr, r + 3, t, live, W.stage);
+                const uint32_t e0 = fast_elem(fr, r, t, W.stage);
+                const uint32_t e1 = fast_elem(fr, r + 1, t, W.stage);
+                const uint32_t e2 = fast_elem(fr, r + 2, t, W.stage);
+                const uint32_t e3 = fast_elem(fr, r + 3, t, W.stage);
                 mask |= (1u << (e0 >> 9)) | (1u << (e1 >> 9)) | (1u << (e2 >> 9)) | (1u << (e3 >> 9));
             }
-            for (; r < R; ++r) mask |= 1u << (fast_elem(lr, r, t, live, W.stage) >> 9);
+            for (; r < R; ++r) mask |= 1u << (fast_elem(fr, r, t, W.stage) >> 9);
         }
         bad |= (mask & 0x80u) != 0;               // invalid character (:582)
         const uint32_t cm = mask & 0x0fu;         // base classes A T C G
         int k[4] = {-1, -1, -1, -1};
         {
-            uint32_t m = cm;
+            uint32_t mm = cm;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                k[q] = m ? __builtin_ctz(m) : -1;
-                m &= m - 1;
+                k[q] = mm ? __builtin_ctz(mm) : -1;
+                mm &= mm - 1;
             }
         }
         const int pc = __popc(cm);                 // wave max of pc by ballots (no LDS)
@@ -1346,10 +1511,10 @@ __device__ __forceinline__ void process_fast(const Args &a, const int64_t rec, W
         double sl[4] = {1.0, 1.0, 1.0, 1.0};
         int n[4] = {0, 0, 0, 0};
         switch (nsl) {
-        case 0: fast_products<0>(U, sl, n, k, R, t, live, lr, W.stage, s_lut); break;
-        case 1: fast_products<1>(U, sl, n, k, R, t, live, lr, W.stage, s_lut); break;
-        case 2: fast_products<2>(U, sl, n, k, R, t, live, lr, W.stage, s_lut); break;
-        default: fast_products<4>(U, sl, n, k, R, t, live, lr, W.stage, s_lut); break;
+        case 0: fast_products<0>(U, sl, n, k, R, t, fr, W.stage, s_lut); break;
+        case 1: fast_products<1>(U, sl, n, k, R, t, fr, W.stage, s_lut); break;
+        case 2: fast_products<2>(U, sl, n, k, R, t, fr, W.stage, s_lut); break;
+        default: fast_products<4>(U, sl, n, k, R, t, fr, W.stage, s_lut); break;
         }
         if (DCR_ABL == 2) {
             if (live) W.cons[t] = (int)(U * 1e9) + n[0] + (int)sl[1];
@@ -1362,9 +1527,9 @@ __device__ __forceinline__ void process_fast(const Args &a, const int64_t rec, W
         for (int q = 0; q < 4; ++q) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const bool m = k[q] == i;
-                L[i] = m ? sl[q] : L[i];
-                c[i] = m ? n[q] : c[i];
+                const bool mt = k[q] == i;
+                L[i] = mt ? sl[q] : L[i];
+                c[i] = mt ? n[q] : c[i];
             }
         }
         const int cN = R - c[0] - c[1] - c[2] - c[3];
@@ -1397,14 +1562,14 @@ __device__ __forceinline__ void process_fast(const Args &a, const int64_t rec, W
         } else {
             best = 0;
         }
-        const bool masked = pm < P->post_threshold;
+        const bool masked = pm < fp.thr;
         const int ch = masked ? 'N' : (int)((0x2D2B47435441ull >> (8 * best)) & 0xffu);
         const double e = 1.0 - pm;
-        const double x = simple_q ? e : pre * (1.0 - e) + (1.0 - post) * e + pre * e * 4.0 / 5.0;
-        int q = P->max_base_quality;
+        const double x = fp.simple_q ? e : fp.pre * (1.0 - e) + (1.0 - fp.post) * e + fp.pre * e * 4.0 / 5.0;
+        int q = fp.maxq;
         if (x > 0.0) {
             if (__builtin_isinf(x)) qoverflow = true;
-            else q = phred_from_table(x, P->max_base_quality, s_qthr);
+            else q = phred_from_table(x, fp.maxq, s_qthr);
         }
         // depth / errors (:1001-1012): no '+' rows and no '+' consensus here
         const int d = R - cN;
@@ -1438,7 +1603,7 @@ __device__ __forceinline__ void process_fast(const Args &a, const int64_t rec, W
     if (first < 0) { write_status(DCR_ST_INDEX_ERROR); return; }   // all 'N': compress_cigarlist([])
     const int Dmax = wave_max(dmax);
     const int Dmin = wave_min(dmin);
-    wave_fence();
+    lds_fence();
     // field layout: trimmed span [first, last] is all M (:770-848, :858-865)
     const int lo = first, hi = last + 1;
     uint8_t *oseq = O.seq + off;
@@ -1456,7 +1621,6 @@ __device__ __forceinline__ void process_fast(const Args &a, const int64_t rec, W
     }
     if (__ballot(kept_overflow)) { write_status(DCR_ST_OVERFLOW_ERROR); return; }
     // E = round(mean(e/d), 3) with numpy's pairwise summation over T values
-    wave_fence();
     const double total = 0.0 + pairwise_small(W.et, T, lane);
     const double E = __builtin_rint((total / (double)T) * 1000.0) / 1000.0;
     if (lane == 0) {
@@ -1473,6 +1637,23 @@ __device__ __forceinline__ void process_fast(const Args &a, const int64_t rec, W
     }
 }
 
+// Each wave takes kFastChunk consecutive fast-list records; record i + 1's
+// loads are issued while record i is processed, and the metadata of record
+// i + 2 is fetched by a vector load (vmcnt, not lgkmcnt, so LDS waits never
+// drain it).  Hardware block dispatch balances the chunks over the CUs.
+constexpr int kFastChunk = 8;
+
+__device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
+    RecMeta m;
+    m.base_al = (int64_t)(((uint64_t)(uint32_t)readlane((int)v, 1) << 32) | (uint32_t)readlane((int)v, 0));
+    m.off = (int64_t)(((uint64_t)(uint32_t)readlane((int)v, 3) << 32) | (uint32_t)readlane((int)v, 2));
+    m.rec = readlane((int)v, 4);
+    m.g0 = readlane((int)v, 5);
+    m.minpos = readlane((int)v, 6);
+    m.w = (uint32_t)readlane((int)v, 7);
+    return m;
+}
+
 template <bool DUPLEX>
 __global__ __launch_bounds__(kBlock, 4) void k_consensus_fast(Args a) {
     __shared__ double2 s_lut[DCR_LUT_N];
@@ -1481,14 +1662,42 @@ __global__ __launch_bounds__(kBlock, 4) void k_consensus_fast(Args a) {
     const dcr_params *P = a.P;
     for (int i = threadIdx.x; i < DCR_LUT_N; i += kBlock) s_lut[i] = make_double2(P->match[i], P->mismatch[i]);
     for (int i = threadIdx.x; i < DCR_MAX_QTHRESH; i += kBlock) s_qthr[i] = P->qthresh[i];
-    __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t rec = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-    if (rec >= a.n_rec) return;
-    process_fast<DUPLEX>(a, rec, s_wave[wave], s_lut, s_qthr, threadIdx.x & 63);
+    const int lane = threadIdx.x & 63;
+    WaveLds &W = s_wave[wave];
+    if (lane == 0) W.pad_code[0] = (uint16_t)kPad;
+    FastParams fp;
+    {
+        const int mb = min(max(P->min_base_quality, 0), 256);
+        fp.m2 = (uint32_t)mb | ((uint32_t)mb << 16);
+        fp.maxq = P->max_base_quality;
+        fp.simple_q = P->error_rate_pre_labeling == 0 && P->error_rate_post_labeling == 0;
+        fp.pre = (double)P->error_rate_pre_labeling;
+        fp.post = (double)P->error_rate_post_labeling;
+        fp.thr = P->post_threshold;
+    }
+    __syncthreads();
+    const int n = a.ws.fast_count[DUPLEX ? 1 : 0];
+    int i = (blockIdx.x * kWavesPerBlock + wave) * kFastChunk;
+    if (i >= n) return;
+    const int iend = min(i + kFastChunk, n);
+    const RecMeta *ML = a.ws.meta;
+    RecMeta m0 = ML[i];
+    RecMeta m1 = ML[min(i + 1, iend - 1)];
+    FastStage st;
+    fast_load<DUPLEX>(a, m0, lane, st);
+    for (;;) {
+        const bool has_next = i + 1 < iend;
+        const int i2 = min(i + 2, iend - 1);
+        const uint32_t mv = lane < 8 ? ((const uint32_t *)(ML + i2))[lane] : 0u;
+        process_fast<DUPLEX>(a, fp, m0, st, has_next, m1, W, s_lut, s_qthr, lane);
+        if (++i >= iend) break;
+        m0 = m1;
+        m1 = meta_from_lanes(mv);
+    }
 }
 
-// persistent: drains the overflow list written by k_consensus_fast
+// persistent: drains the general list written by k_recmeta
 template <bool DUPLEX>
 __global__ __launch_bounds__(kBlock, 2) void k_consensus_general(Args a) {
     __shared__ double2 s_lut[DCR_LUT_N];
@@ -1507,6 +1716,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_consensus_general(Args a) {
     }
 }
 
+template __global__ void k_recmeta<false>(Args);
+template __global__ void k_recmeta<true>(Args);
 template __global__ void k_consensus_fast<false>(Args);
 template __global__ void k_consensus_fast<true>(Args);
 template __global__ void k_consensus_general<false>(Args);
