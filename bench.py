@@ -49,19 +49,41 @@ def sscs_algorithmic_bytes(packed):
     return reads_b + 6 * cols + 16 * n_sub
 
 
-def cpu_baseline(args, n_sample_fam):
-    from duplexumiconsensusreads_amd import synth
+def cpu_baseline(packed, reps):
+    """The C restatement (oracle/dcr_oracle.c, test infrastructure used here
+    only as the timed CPU leg) over the bench batch itself, multi-threaded
+    over families.  The C2 batch takes ~1-2 s per pass on 16 threads, so the
+    sample is the whole batch, repeated ``reps`` times (≈10-30 thread-s)."""
     from duplexumiconsensusreads_amd.params import ConsensusParams
     from oracle import dcr_oracle_c
-    threads = min(16, os.cpu_count() or 1)
-    sample = synth.packed_fixed_size(n_sample_fam, seed=args.seed)
-    t0 = time.perf_counter()
-    ss, ds, _ = dcr_oracle_c.run(sample, ConsensusParams(), n_threads=threads, want_info=False)
-    dt = time.perf_counter() - t0
-    bases = int(ds.len.sum())
+    threads = min(16, os.cpu_count() or 1)   # the GPU box's CPU share is 16
+    dts, bases = [], 0
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        _, ds, _ = dcr_oracle_c.run(packed, ConsensusParams(), n_threads=threads, want_info=False)
+        dts.append(time.perf_counter() - t0)
+        bases = int(ds.len.sum())
+        del ds
+    dt = min(dts)
     return {"value": bases / dt, "unit": "consensus bases/s", "cores": threads, "kind": "port",
-            "sample": f"{n_sample_fam} families ({sample.n_reads} reads) of the same C2 workload, "
-                      f"C restatement oracle/dcr_oracle.c, {threads} threads, {dt:.2f} s"}
+            "sample": f"the whole bench batch ({packed.n_fam} families, {packed.n_reads} reads), "
+                      f"C restatement oracle/dcr_oracle.c on {threads} threads, best of {reps}: "
+                      f"{dt:.2f} s per pass"}
+
+
+def load_traffic(kernel, n_fam):
+    """HBM bytes per launch of ``kernel`` from the committed PMC passes
+    (tools/pmc_traffic.py -> profiles/traffic.json: FETCH_SIZE x2 + WRITE_SIZE,
+    MI355X_MICROARCH.md §HBM), scaled to this batch when the profiled batch
+    had a different family count; None when absent."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        k = t["kernels"][kernel]
+        return k["hbm_bytes_per_launch"] * n_fam / t["families"], t
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        return None, None
 
 
 def main():
@@ -71,7 +93,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--families", type=int, default=312_500, help="families per GPU (C2: 312,500)")
     ap.add_argument("--seed", type=int, default=2)
-    ap.add_argument("--cpu-sample", type=int, default=65_536, help="families in the CPU-baseline sample")
+    ap.add_argument("--cpu-reps", type=int, default=2, help="passes of the CPU baseline over the batch")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -109,14 +131,13 @@ def main():
     if dist:
         tdist.barrier()
     torch.cuda.synchronize()
-    ss_ms = prep_ms = ds_ms = 0.0
+    kms = {k: 0.0 for k in _lib.KERNELS}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.run_device(db.batch_struct, db.ss_struct, db.ds_struct)
-        tm = ctx.last_timing()          # waits on this step's events only
-        ss_ms += tm["single_strand"]
-        prep_ms += tm["prep"]
-        ds_ms += tm["duplex"]
+        tm = ctx.last_kernel_timing()   # waits on this step's events only
+        for k in kms:
+            kms[k] += tm[k]
     ctx.sync()
     torch.cuda.synchronize()
     if dist:
@@ -135,9 +156,11 @@ def main():
     if rank == 0:
         ms_step = elapsed * 1000.0 / args.steps
         value = total_bases * args.steps / elapsed
-        ss_avg_ms = ss_ms / args.steps
+        kavg = {k: v / args.steps for k, v in kms.items()}
+        dom = "k_consensus_fast<ss>"
         alg = sscs_algorithmic_bytes(packed)
-        achieved = alg / (ss_avg_ms / 1000.0) / 1e9
+        achieved = alg / (kavg[dom] / 1000.0) / 1e9
+        traffic, tsrc = load_traffic("k_consensus_fast<false>", packed.n_fam)
         res = {
             "metric": METRIC, "value": value, "unit": "consensus bases/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
@@ -147,17 +170,19 @@ def main():
                                    "312,500 MI families x 4 subfamilies x 8 reads, 2x150bp, no indels",
                        "families_per_gpu": packed.n_fam, "reads_per_gpu": packed.n_reads,
                        "input_bytes_per_gpu": packed.nbytes(),
-                       "kernel_ms": {"prep": prep_ms / args.steps, "single_strand": ss_avg_ms,
-                                     "duplex": ds_ms / args.steps},
+                       "kernel_ms": kavg,
+                       "single_strand_stage_GBps": alg / (sum(kavg[k] for k in _lib.KERNELS[1:4]) / 1e3) / 1e9,
                        "records_not_ok": n_bad,
                        "parallelism": f"family-sharded x{world}, no data-path collective"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "k_consensus<false> (single-strand)",
-                         "algorithmic_bytes_per_launch": alg},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_consensus_fast<false> (single-strand consensus)",
+                         "kernel_ms": kavg[dom], "algorithmic_bytes_per_launch": alg,
+                         "traffic_source": (f"profiles/traffic.json ({tsrc.get('source', '')})" if tsrc else None)},
         }
         if not args.no_cpu and world == 1:
-            res["cpu_baseline"] = cpu_baseline(args, args.cpu_sample)
+            del db
+            res["cpu_baseline"] = cpu_baseline(packed, args.cpu_reps)
         else:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)

@@ -31,7 +31,11 @@ EXPORTS = {
     "dcr_sync": (ctypes.c_int, [ctypes.c_void_p]),
     "dcr_read_info_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "dcr_last_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "dcr_last_kernel_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
 }
+
+KERNELS = ("k_prep", "k_recmeta<ss>", "k_consensus_fast<ss>", "k_consensus_general<ss>",
+           "k_recmeta<ds>", "k_consensus_fast<ds>", "k_consensus_general<ds>")
 
 _lib = None
 
@@ -131,6 +135,12 @@ class Context:
         ms = (ctypes.c_float * 4)()
         _check(load().dcr_last_timing(self._ctx, ms))
         return dict(prep=ms[0], single_strand=ms[1], duplex=ms[2], total=ms[3])
+
+    def last_kernel_timing(self):
+        """Per-kernel ms of the last batch (HIP events between the launches)."""
+        ms = (ctypes.c_float * len(KERNELS))()
+        _check(load().dcr_last_kernel_timing(self._ctx, ms))
+        return dict(zip(KERNELS, ms))
 
 
 def backend(ctx: Context):

@@ -53,7 +53,9 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 struct dcr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // ev[0] batch start, ev[1..7] after k_prep, k_recmeta<ss>, fast<ss>, general<ss>,
+    // k_recmeta<ds>, fast<ds>, general<ds>
+    hipEvent_t ev[DCR_N_KERNEL_TIMES + 1] = {};
     dcr_params *d_params = nullptr;
     DevBuf ws;          // workspace
     DevBuf io;          // staging for the host-pointer entry point
@@ -218,26 +220,34 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     auto strand = [&](bool duplex) -> int {
         a.n_rec = (duplex ? 2LL : 4LL) * in->n_fam;
         const unsigned nb = (unsigned)((a.n_rec + 255) / 256);    // k_recmeta: 64 records per wave
+        hipEvent_t *ev = c->ev + (duplex ? 5 : 2);
         if (duplex) {
             hipLaunchKernelGGL(dcr::k_recmeta<true>, dim3(nb), dim3(256), 0, c->stream, a);
+            HIP_TRY(hipEventRecord(ev[0], c->stream));
             hipLaunchKernelGGL(dcr::k_consensus_fast<true>, dim3(fast_grid(a.n_rec)), dim3(256), 0,
                                c->stream, a);
+            HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL(dcr::k_consensus_general<true>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
                                c->stream, a);
         } else {
             hipLaunchKernelGGL(dcr::k_recmeta<false>, dim3(nb), dim3(256), 0, c->stream, a);
+            HIP_TRY(hipEventRecord(ev[0], c->stream));
             hipLaunchKernelGGL(dcr::k_consensus_fast<false>, dim3(fast_grid(a.n_rec)), dim3(256), 0,
                                c->stream, a);
+            HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL(dcr::k_consensus_general<false>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
                                c->stream, a);
         }
         HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ev[2], c->stream));
         return DCR_OK;
     };
-    if (in->n_fam > 0 && (rc = strand(false))) return rc;
-    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-    if (in->n_fam > 0 && (rc = strand(true))) return rc;
-    HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+    if (in->n_fam > 0) {
+        if ((rc = strand(false))) return rc;
+        if ((rc = strand(true))) return rc;
+    } else {
+        for (int k = 2; k <= DCR_N_KERNEL_TIMES; ++k) HIP_TRY(hipEventRecord(c->ev[k], c->stream));
+    }
     c->timed = true;
     return DCR_OK;
 }
@@ -257,11 +267,20 @@ int dcr_sync(dcr_ctx *c) {
 int dcr_last_timing(dcr_ctx *c, float *ms4) {
     if (!c || !ms4) return fail(DCR_EARG, "NULL argument");
     if (!c->timed) return fail(DCR_EARG, "no batch has run");
-    HIP_TRY(hipEventSynchronize(c->ev[3]));
+    const int last = DCR_N_KERNEL_TIMES;
+    HIP_TRY(hipEventSynchronize(c->ev[last]));
     HIP_TRY(hipEventElapsedTime(&ms4[0], c->ev[0], c->ev[1]));
-    HIP_TRY(hipEventElapsedTime(&ms4[1], c->ev[1], c->ev[2]));
-    HIP_TRY(hipEventElapsedTime(&ms4[2], c->ev[2], c->ev[3]));
-    HIP_TRY(hipEventElapsedTime(&ms4[3], c->ev[0], c->ev[3]));
+    HIP_TRY(hipEventElapsedTime(&ms4[1], c->ev[1], c->ev[4]));
+    HIP_TRY(hipEventElapsedTime(&ms4[2], c->ev[4], c->ev[last]));
+    HIP_TRY(hipEventElapsedTime(&ms4[3], c->ev[0], c->ev[last]));
+    return DCR_OK;
+}
+
+int dcr_last_kernel_timing(dcr_ctx *c, float *ms) {
+    if (!c || !ms) return fail(DCR_EARG, "NULL argument");
+    if (!c->timed) return fail(DCR_EARG, "no batch has run");
+    HIP_TRY(hipEventSynchronize(c->ev[DCR_N_KERNEL_TIMES]));
+    for (int k = 0; k < DCR_N_KERNEL_TIMES; ++k) HIP_TRY(hipEventElapsedTime(&ms[k], c->ev[k], c->ev[k + 1]));
     return DCR_OK;
 }
 

@@ -15,6 +15,7 @@ A1/A2 and ``k/B`` on B1/B2; RX is ``U1-U2`` on A and ``U2-U1`` on B.
 from __future__ import annotations
 
 import dataclasses
+import os
 
 import numpy as np
 
@@ -206,40 +207,53 @@ _ERR_P16 = {37: int(round(10 ** -3.7 * 65536)), 25: int(round(10 ** -2.5 * 65536
             12: int(round(10 ** -1.2 * 65536))}
 
 
-def packed_fixed_size(n_families, sub_size=8, read_len=150, seed=2, chunk_reads=1 << 20):
+def packed_fixed_size(n_families, sub_size=8, read_len=150, seed=2, chunk_reads=1 << 18, threads=None):
     """Vectorised config-2 generator: uniform subfamily size, ``150M`` reads,
-    no indels.  Same base/quality model as family_records."""
+    no indels.  Same base/quality model as family_records.
+    Chunks of families are filled by a thread pool (numpy releases the GIL),
+    each from its own generator seeded by (seed, chunk): the bytes depend on
+    ``seed`` and ``chunk_reads`` only, not on the thread count."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from .batch import finish_batch
     rng = np.random.default_rng(seed)
     F, L, k = n_families, read_len, sub_size
     n = F * 4 * k
     ins = np.clip(rng.normal(300, 30, F), 200, 500).astype(np.int64)
     P = rng.integers(1000, 100_000_000, F).astype(np.int64)
-    fam = np.repeat(np.arange(F), 4 * k)
-    sub = np.tile(np.repeat(np.arange(4), k), F)
+    sub = np.repeat(np.arange(4), k)
     rev = sub >= 2
-    start = np.where(rev, ins[fam] - L, 0)
-    read_pos = (P[fam] + start).astype(np.int32)
-    tw = int(ins.max()) + 20
+    start = np.where(rev[None, :], ins[:, None] - L, 0).reshape(-1)       # [n]
+    read_pos = (np.repeat(P, 4 * k) + start).astype(np.int32)
+    tw = int(ins.max()) + 20 if F else L
     bases = np.empty(n * L, np.uint8)
     quals = np.empty(n * L, np.uint8)
     acgt = np.frombuffer(b"ACGT", np.uint8)
+    err_lut = np.zeros(256, np.uint16)
+    for q, v in _ERR_P16.items():
+        err_lut[q] = v
     fam_chunk = max(1, chunk_reads // (4 * k))
-    for f0 in range(0, F, fam_chunk):
+    ar = np.arange(L)
+
+    def fill(ci):
+        f0 = ci * fam_chunk
         f1 = min(F, f0 + fam_chunk)
-        tmpl = acgt[rng.integers(0, 4, (f1 - f0, tw), dtype=np.uint8)]
+        g = np.random.default_rng([seed, ci])
+        tmpl = acgt[g.integers(0, 4, (f1 - f0) * tw, dtype=np.uint8)]
         r0, r1 = f0 * 4 * k, f1 * 4 * k
-        idx = start[r0:r1, None] + np.arange(L)[None, :]
-        seq = tmpl[(fam[r0:r1] - f0)[:, None], idx]
-        q = _QLUT[rng.integers(0, 100, (r1 - r0, L), dtype=np.uint8)]
-        u = rng.integers(0, 65536, (r1 - r0, L), dtype=np.uint16)
-        thr = np.where(q == 37, _ERR_P16[37], np.where(q == 25, _ERR_P16[25], _ERR_P16[12]))
-        err = u < thr
+        idx = (np.repeat(np.arange(f1 - f0) * tw, 4 * k) + start[r0:r1])[:, None] + ar[None, :]
+        seq = tmpl[idx]
+        q = _QLUT[g.integers(0, 100, (r1 - r0, L), dtype=np.uint8)]
+        err = g.integers(0, 65536, (r1 - r0, L), dtype=np.uint16) < err_lut[q]
         if err.any():
             code = np.searchsorted(acgt, seq[err])
-            seq[err] = acgt[(code + rng.integers(1, 4, err.sum())) % 4]
+            seq[err] = acgt[(code + g.integers(1, 4, int(err.sum()))) % 4]
         bases[r0 * L:r1 * L] = seq.reshape(-1)
         quals[r0 * L:r1 * L] = q.reshape(-1)
+
+    n_chunks = (F + fam_chunk - 1) // fam_chunk
+    with ThreadPoolExecutor(threads or min(16, os.cpu_count() or 1)) as ex:
+        list(ex.map(fill, range(n_chunks)))
     sub_off = np.arange(0, n + 1, k, dtype=np.int32)
     mapq = rng.integers(20, 61, n).astype(np.uint8)
     seq_off = np.arange(n, dtype=np.int64) * L
