@@ -35,6 +35,16 @@ class FamilyExit(Exception):
     """The reference prints an error and calls sys.exit(1) for this family."""
 
 
+def reference_exception(name: str) -> Exception:
+    """The exception the reference raises for a record status (include/dcr.h
+    DCR_ST_*): IndexError / TypeError / ValueError / OverflowError, or the
+    sys.exit(1) of most_likely_nucleotide on an invalid nucleotide (:582-585)."""
+    if name == "exit":
+        return FamilyExit("ERROR: invalid nucleotide found in the reads")
+    return {"IndexError": IndexError, "TypeError": TypeError, "ValueError": ValueError,
+            "OverflowError": OverflowError}[name](f"reference would raise {name} here")
+
+
 @dataclasses.dataclass
 class FamilyResult:
     code: str
