@@ -6,8 +6,9 @@ order of split_family (DuplexUMIConsensusReads.py:132-154) and of the four
 single-strand calls (:1564-1569).  Duplex pairs are p = 2f + j with
 j = 0: (A1, B2) and j = 1: (B1, A2) (:1575-1576).
 
-Output regions: every consensus gets a region of ``T_ub`` columns, an upper
-bound on its alignment width T (:458-459): for a subfamily
+Output regions: every consensus gets a region of ``T_ub`` columns (rounded
+up to a multiple of 16, so regions start 16-byte aligned), an upper bound on
+its alignment width T (:458-459): for a subfamily
 ``max(pos + raw_len) - min(pos)`` (preprocessing only shortens reads and
 never moves reference_start, :242-244); for a duplex the union of its two
 subfamilies' bounds.
@@ -191,14 +192,16 @@ def finish_batch(sub_off, read_pos, read_mapq, seq_off, seq_len, cig_off, cig_n,
             if b > a:
                 mn[s] = read_pos[a:b].min()
                 mx[s] = ends[a:b].max()
-    t_ss = np.maximum(mx - mn, 1)
+    # regions are rounded up to 16 columns so every region starts 16-byte
+    # aligned (the kernels write seq/qual/d/e with 16-byte stores)
+    t_ss = (np.maximum(mx - mn, 1) + 15) & ~np.int64(15)
     ss_col_off = np.zeros(n_sub + 1, np.int64)
     ss_col_off[1:] = np.cumsum(t_ss)
     mn4, mx4 = mn.reshape(F, 4), mx.reshape(F, 4)
     t_ds = np.empty((F, 2), np.int64)
     for j, (a, b) in enumerate(((0, 1), (2, 3))):
         t_ds[:, j] = np.maximum(mx4[:, a], mx4[:, b]) - np.minimum(mn4[:, a], mn4[:, b])
-    t_ds = np.maximum(t_ds.reshape(-1), 1)
+    t_ds = (np.maximum(t_ds.reshape(-1), 1) + 15) & ~np.int64(15)
     ds_col_off = np.zeros(2 * F + 1, np.int64)
     ds_col_off[1:] = np.cumsum(t_ds)
     return PackedBatch(sub_off=sub_off, read_pos=read_pos, read_mapq=read_mapq, seq_off=seq_off,

@@ -62,15 +62,22 @@ struct dcr_ctx {
     dcr::Workspace w{};
     int64_t last_reads = 0;
     bool timed = false;
-    int fast_ok = 0;    // all likelihood factors in [0, 1]: the fast kernel's finalize applies
+    int fast_ok = 0;    // fast_allowed(): the fast kernel may take records
+    dcr_params host_params{};
     int n_cu = 256;     // compute units (persistent grid size)
+    int fast_blocks[2] = {1, 1};   // resident k_consensus_fast blocks per CU (single-strand, duplex)
 };
 
-static int factors_unit(const dcr_params *p) {
+// The fast kernel's assumptions (dcr_kernels.hip, fast kernel v2): every
+// likelihood factor in [0, 1]; the quality formula reduces to e (no pre/post
+// labelling error, :700-709); qualities fit a byte (:1383).  Otherwise every
+// record takes the general kernel.
+static int fast_allowed(const dcr_params *p) {
     for (int i = 0; i < DCR_LUT_N; ++i)
         if (!(p->match[i] >= 0.0 && p->match[i] <= 1.0 && p->mismatch[i] >= 0.0 && p->mismatch[i] <= 1.0))
             return 0;
-    return 1;
+    return p->error_rate_pre_labeling == 0 && p->error_rate_post_labeling == 0 && p->max_base_quality <= 255 &&
+           p->min_base_quality <= 255;
 }
 
 extern "C" {
@@ -112,7 +119,16 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
     }
     for (auto &e : c->ev) (void)hipEventCreate(&e);
     (void)hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device);
-    c->fast_ok = factors_unit(params);
+    // the persistent fast kernel's grid = what is resident at once (a block
+    // beyond that would start only when a resident one has finished its range)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->fast_blocks[0], dcr::k_consensus_fast<false>, dcr::kBlock, 0) !=
+            hipSuccess || c->fast_blocks[0] < 1)
+        c->fast_blocks[0] = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->fast_blocks[1], dcr::k_consensus_fast<true>, dcr::kBlock, 0) !=
+            hipSuccess || c->fast_blocks[1] < 1)
+        c->fast_blocks[1] = 1;
+    c->fast_ok = fast_allowed(params);
+    c->host_params = *params;
     if (hipMemcpy(c->d_params, params, sizeof(dcr_params), hipMemcpyHostToDevice) != hipSuccess) {
         fail(DCR_EHIP, "params upload failed");
         dcr_destroy(c);
@@ -141,7 +157,8 @@ int dcr_set_params(dcr_ctx *c, const dcr_params *params) {
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemcpyAsync(c->d_params, params, sizeof(dcr_params), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    c->fast_ok = factors_unit(params);
+    c->fast_ok = fast_allowed(params);
+    c->host_params = *params;
     return DCR_OK;
 }
 
@@ -159,6 +176,7 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     const size_t o_ins = o;  o = align_up(o + (size_t)std::max<int64_t>(s->ss_cols, 1));
     const size_t o_st = o;   o = align_up(o + sizeof(int4) * (size_t)std::max<int64_t>(s->n_reads, 1));
     const size_t o_err = o;  o = align_up(o + 32);
+    const size_t o_stamp = o; o = align_up(o + 32 * sizeof(unsigned long long));
     const size_t n_rec = (size_t)std::max<int64_t>(4LL * s->n_fam, 1);
     const size_t o_ovf = o;  o = align_up(o + sizeof(int) * n_rec);
     const size_t o_meta = o; o = align_up(o + sizeof(dcr::RecMeta) * n_rec);
@@ -177,6 +195,7 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     c->w.err = (int *)(b + o_err);
     c->w.ovf_count = (int *)(b + o_err) + 1;     // err, ovf_count[2], fast_count[2]: one 32-byte block
     c->w.fast_count = (int *)(b + o_err) + 3;
+    c->w.stamps = (unsigned long long *)(b + o_stamp);
     c->w.ovf = (int *)(b + o_ovf);
     c->w.meta = (dcr::RecMeta *)(b + o_meta);
     c->w.rmeta = (uint2 *)(b + o_rm);
@@ -207,15 +226,29 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     a.ss = *ss;
     a.ds = *ds;
     a.fast_ok = c->fast_ok;
+    {
+        // fast finalize bound (dcr_kernels.hip, fast kernel v2): a column whose
+        // largest chain b and the rest of S satisfy rest (1 + 1e-9) < b cb has
+        // quality maxQ and is not masked
+        const dcr_params &hp = c->host_params;
+        const int mb = std::min(std::max(hp.min_base_quality, 0), 255);
+        a.fast_kq = (uint32_t)(255 - mb) * 0x01010101u;
+        a.fast_maxq = hp.max_base_quality;
+        const int mq = std::min(std::max(hp.max_base_quality, 0), DCR_MAX_QTHRESH - 1);
+        const double cc = std::min(std::min(hp.qthresh[mq], 1.0 - hp.post_threshold), 0.25);
+        a.fast_ca = 1.0 + 1e-9;
+        a.fast_cb = cc * (1.0 - 1e-9) - 1e-15;
+    }
     // per strand: k_recmeta classifies every record (fast list / general list /
     // status written), then the fast kernel (8 records per wave) drains the fast list and
     // the persistent general kernel the rest (insertions, > 64 reads, wide layouts)
     auto grid_for = [&](int64_t n_rec, unsigned cap) {
         return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_rec + 3) / 4, cap));
     };
-    constexpr int kFastChunk = 8;                 // records per wave (dcr_kernels.hip)
-    auto fast_grid = [&](int64_t n_rec) {
-        return (unsigned)std::max<int64_t>(1, (n_rec + 4 * kFastChunk - 1) / (4 * kFastChunk));
+    // persistent fast kernel: the resident blocks, at least ~8 records per wave
+    auto fast_grid = [&](int64_t n_rec, bool duplex) {
+        return (unsigned)std::max<int64_t>(
+            1, std::min<int64_t>((n_rec + 31) / 32, (int64_t)c->fast_blocks[duplex ? 1 : 0] * c->n_cu));
     };
     auto strand = [&](bool duplex) -> int {
         a.n_rec = (duplex ? 2LL : 4LL) * in->n_fam;
@@ -224,7 +257,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         if (duplex) {
             hipLaunchKernelGGL(dcr::k_recmeta<true>, dim3(nb), dim3(256), 0, c->stream, a);
             HIP_TRY(hipEventRecord(ev[0], c->stream));
-            hipLaunchKernelGGL(dcr::k_consensus_fast<true>, dim3(fast_grid(a.n_rec)), dim3(256), 0,
+            hipLaunchKernelGGL(dcr::k_consensus_fast<true>, dim3(fast_grid(a.n_rec, true)), dim3(256), 0,
                                c->stream, a);
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL(dcr::k_consensus_general<true>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
@@ -232,7 +265,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         } else {
             hipLaunchKernelGGL(dcr::k_recmeta<false>, dim3(nb), dim3(256), 0, c->stream, a);
             HIP_TRY(hipEventRecord(ev[0], c->stream));
-            hipLaunchKernelGGL(dcr::k_consensus_fast<false>, dim3(fast_grid(a.n_rec)), dim3(256), 0,
+            hipLaunchKernelGGL(dcr::k_consensus_fast<false>, dim3(fast_grid(a.n_rec, false)), dim3(256), 0,
                                c->stream, a);
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL(dcr::k_consensus_general<false>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
@@ -273,6 +306,16 @@ int dcr_last_timing(dcr_ctx *c, float *ms4) {
     HIP_TRY(hipEventElapsedTime(&ms4[1], c->ev[1], c->ev[4]));
     HIP_TRY(hipEventElapsedTime(&ms4[2], c->ev[4], c->ev[last]));
     HIP_TRY(hipEventElapsedTime(&ms4[3], c->ev[0], c->ev[last]));
+    return DCR_OK;
+}
+
+// diagnostic (not in include/dcr.h): phase cycle counters of DCR_STAMP builds
+int dcr_debug_stamps(dcr_ctx *c, unsigned long long *out, int n, int reset) {
+    if (!c || !out || n > 32) return fail(DCR_EARG, "bad argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(out, c->w.stamps, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
+    if (reset) HIP_TRY(hipMemset(c->w.stamps, 0, sizeof(unsigned long long) * 32));
     return DCR_OK;
 }
 

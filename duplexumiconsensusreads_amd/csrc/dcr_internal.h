@@ -35,6 +35,7 @@ struct Workspace {
     int *ovf;               // [n_rec] records for the general kernel
     int *ovf_count;         // [2] single-strand / duplex general-list lengths
     int *fast_count;        // [2] single-strand / duplex fast-list lengths
+    unsigned long long *stamps;   // [32] diagnostic phase cycles (DCR_STAMP builds only)
     RecMeta *meta;          // [n_rec] fast list
     uint2 *rmeta;           // [max(n_reads, 4F)] per read: col | len << 8 | mapq << 16, stage offset
 };
@@ -46,7 +47,12 @@ struct Args {
     dcr_out ss;
     dcr_out ds;
     int64_t n_rec;
-    int fast_ok;            // every LUT factor in [0, 1] (host-checked): fast kernel allowed
+    int fast_ok;            // fast_allowed() (dcr_capi.hip): the fast kernel may take records
+    // fast-kernel constants (host-computed, dcr_capi.hip: fast_constants)
+    uint32_t fast_kq;       // bytes 255 - min_base_quality: v_lerp_u8 masking test
+    int fast_maxq;          // max_base_quality
+    double fast_ca;         // 1 + 1e-9
+    double fast_cb;         // min(qthresh[maxQ], 1 - threshold, 1/4) (1 - 1e-9) - 1e-15
 };
 
 __global__ void k_prep(dcr_batch in, const dcr_params *P, Workspace ws);

@@ -26,8 +26,13 @@
 // plus one chain per distinct class actually observed, and the wave pays only
 // for the largest number of distinct classes among its 64 columns (usually
 // one or two) instead of six.  Results are bit-identical to the six chains.
+#include <type_traits>
+
 #include "dcr_internal.h"
 
+#ifndef DCR_STAMP
+#define DCR_STAMP 0   // diagnostic builds only (tools/stamps.py): per-phase s_memtime cycle totals
+#endif
 #ifndef DCR_ABL
 #define DCR_ABL 0   // diagnostic builds only (tools/ablate.py): 1 setup, 2 +accumulate, 3 +finalize
 #endif
@@ -1059,74 +1064,6 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
 }
 
 
-// ------------------------------------------------------- fast records
-// The dominant record shape: every read a single M run (no I, no D, so no
-// insertion columns and no '-' rows), <= 64 reads, bytes fit the LDS stage,
-// T <= kColsLds.  Then every aligned row is a base, a masked 'N' or a pad 'N'
-// (classes 0-3 and 6), no column holds '+', and the consensus is uppercase
-// A/C/G/T/N only, so its CIGAR is one M run over the trimmed span
-// (:797-848 yields M for every such column).
-//
-// Likelihoods: a pre-scan of the tile gives each lane (column) the set of base
-// classes present; the wave picks the loop with that many chains (U for every
-// unseen class, plus one chain per present class, fixed before the product
-// loop, so the loop is branch-free).  Products stay in read order: identical
-// doubles to the reference's six chains.
-// element code of read r at column t; outside the read's span the load is
-// redirected to the kPad sentinel (selecting the address, not the loaded
-// value, keeps the bounds mask out of VCC while the LDS read is in flight).
-// No column bound is needed: every read ends at or before T (T = max end).
-struct FastReads {
-    int x;      // lane r: first column | kept length << 8 | mapq << 16
-    int y;      // lane r: stage offset of its first kept base
-};
-
-__device__ __forceinline__ uint32_t fast_elem(const FastReads &fr, int r, int t, const uint16_t *stage) {
-    const int x = readlane(fr.x, r);
-    const int so = readlane(fr.y, r);
-    const int j = t - (x & 0xff);
-    const bool inb = (unsigned)j < (((unsigned)x >> 8) & 0xffu);
-    return stage[inb ? so + j : -4];             // stage[-4] = pad_code[0]
-}
-
-template <int NS>
-__device__ __forceinline__ void fast_mul(double &U, double (&s)[4], int (&n)[4], const int (&k)[4], uint32_t e,
-                                         double2 f) {
-    const uint32_t cls = e >> 9;
-    U *= f.y;
-#pragma unroll
-    for (int q = 0; q < NS; ++q) {
-        const bool m = cls == (uint32_t)k[q];
-        s[q] *= m ? f.x : f.y;
-        n[q] += m;
-    }
-}
-
-// products in read order; reads fetched four at a time (codes, then LUT
-// factors) before the multiplies, so LDS latency overlaps (hand-unrolled:
-// readlane is convergent and blocks the compiler's runtime unrolling)
-template <int NS>
-__device__ __forceinline__ void fast_products(double &U, double (&s)[4], int (&n)[4], const int (&k)[4], int R,
-                                              int t, const FastReads &fr, const uint16_t *stage,
-                                              const double2 *lut) {
-    int r = 0;
-    for (; r + 4 <= R; r += 4) {
-        const uint32_t e0 = fast_elem(fr, r, t, stage);
-        const uint32_t e1 = fast_elem(fr, r + 1, t, stage);
-        const uint32_t e2 = fast_elem(fr, r + 2, t, stage);
-        const uint32_t e3 = fast_elem(fr, r + 3, t, stage);
-        const double2 f0 = lut[e0 & 511], f1 = lut[e1 & 511], f2 = lut[e2 & 511], f3 = lut[e3 & 511];
-        fast_mul<NS>(U, s, n, k, e0, f0);
-        fast_mul<NS>(U, s, n, k, e1, f1);
-        fast_mul<NS>(U, s, n, k, e2, f2);
-        fast_mul<NS>(U, s, n, k, e3, f3);
-    }
-    for (; r < R; ++r) {
-        const uint32_t e = fast_elem(fr, r, t, stage);
-        fast_mul<NS>(U, s, n, k, e, lut[e & 511]);
-    }
-}
-
 // numpy pairwise_sum over a[0..n), n <= 240 (at most two blocks of <= 128, 8 accumulators):
 // accumulator j of block b lives on lane 8b + j and loads its <= 16 elements
 // up front; the fixed association order of numpy is kept exactly.
@@ -1147,16 +1084,20 @@ __device__ __forceinline__ double pairwise_small(const double *a, int n, int lan
     const int bn = blk ? n - n2 : n2;            // block length (>= 8 when it is a block)
     const int body = bn - (bn % 8);
     const int j = lane & 7;
-    double v[16];
+    // accumulator j: a[j], a[j + 8], ... in order; loaded four at a time
+    double r = 0.0;
+#pragma unroll 1
+    for (int i0 = 0; i0 < 16; i0 += 4) {
+        double v[4];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int idx = j + 8 * i;
-        v[i] = (lane < 8 * nb && idx < body) ? a[bo + idx] : 0.0;
+        for (int k = 0; k < 4; ++k) {
+            const int idx = j + 8 * (i0 + k);
+            v[k] = (lane < 8 * nb && idx < body) ? a[bo + idx] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (8 * (i0 + k) < body) r = i0 + k == 0 ? v[k] : r + v[k];
     }
-    double r = v[0];
-#pragma unroll
-    for (int i = 1; i < 16; ++i)
-        if (8 * i < body) r += v[i];
     // per block: ((r0+r1)+(r2+r3)) + ((r4+r5)+(r6+r7)), then the tail in order
     const double p01 = r + __shfl_xor(r, 1);
     const double p0123 = p01 + __shfl_xor(p01, 2);
@@ -1169,6 +1110,79 @@ __device__ __forceinline__ double pairwise_small(const double *a, int n, int lan
         const int bd = m - (m % 8);
         if (b < nb)
             for (int i = bd; i < m; ++i) x += a[o + i];
+        res[b] = x;
+    }
+    return nb == 1 ? res[0] : res[0] + res[1];
+}
+
+// 64-bit DPP move (two 32-bit halves)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int2 h = __builtin_bit_cast(int2, v);
+    int2 r;
+    r.x = __builtin_amdgcn_update_dpp(0, h.x, CTRL, 0xF, 0xF, false);
+    r.y = __builtin_amdgcn_update_dpp(0, h.y, CTRL, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, r);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const int2 h = __builtin_bit_cast(int2, v);
+    return __builtin_bit_cast(double, make_int2(readlane(h.x, l), readlane(h.y, l)));
+}
+
+// numpy pairwise_sum over a[0..n) in LDS, n <= 240, for the fast kernel: as
+// pairwise_small, with every load issued up front (two batches of eight per
+// accumulator lane and the tails of both blocks) and the eight-accumulator
+// combine ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) done with DPP instead of LDS
+// permutes.  Same association order, bit for bit.
+__device__ __forceinline__ double pairwise_et(const double *a, int n, int lane) {
+    if (n < 8) {
+        double res = -0.0;
+        for (int i = 0; i < n; ++i) res += a[i];
+        return res;
+    }
+    int n2 = n, nb = 1;
+    if (n > 128) {
+        n2 = n / 2;
+        n2 -= n2 % 8;
+        nb = 2;
+    }
+    const int blk = (lane >> 3) & 1;
+    const int bo = blk ? n2 : 0;                 // block offset
+    const int bn = blk ? n - n2 : n2;            // block length (>= 8 when it is a block)
+    const int body = bn - (bn % 8);
+    const int j = lane & 7;
+    const bool acc = lane < 8 * nb;
+    // tails (< 8 elements after the body of each block), loaded by lanes 0 and 8
+    const int tail = bn % 8;
+    double tv[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) tv[i] = (acc && j == 0 && i < tail) ? a[bo + body + i] : 0.0;
+    double r = 0.0;
+#pragma unroll
+    for (int i0 = 0; i0 < 16; i0 += 8) {
+        double v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int idx = j + 8 * (i0 + k);
+            v[k] = (acc && idx < body) ? a[bo + idx] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (8 * (i0 + k) < body) r = i0 + k == 0 ? v[k] : r + v[k];
+    }
+    const double p01 = r + dpp_f64<0xB1>(r);            // quad_perm [1,0,3,2]
+    const double p0123 = p01 + dpp_f64<0x4E>(p01);      // quad_perm [2,3,0,1]
+    const double s8 = p0123 + dpp_f64<0x141>(p0123);    // row_half_mirror: quad 0 <-> quad 1
+    double res[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        double x = readlane_f64(s8, 8 * b);
+        const int m = b ? n - n2 : n2;
+        const int tc = b < nb ? m % 8 : 0;
+#pragma unroll
+        for (int i = 0; i < 7; ++i)
+            if (i < tc) x += readlane_f64(tv[i], 8 * b);
         res[b] = x;
     }
     return nb == 1 ? res[0] : res[0] + res[1];
@@ -1328,9 +1342,9 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
             const int T = g.maxend - g.minpos;
             const int64_t off = col_off[rk];
             const int64_t cap = col_off[rk + 1] - off;
-            const int64_t base_al = (int64_t)g.lo & ~(int64_t)3;
+            const int64_t base_al = (int64_t)g.lo & ~(int64_t)15;     // 16-byte staging loads
             const int64_t span = (int64_t)g.hi - base_al;
-            const bool aligned = ((((uintptr_t)gb) | ((uintptr_t)gq)) & 3) == 0;
+            const bool aligned = ((((uintptr_t)gb) | ((uintptr_t)gq)) & 15) == 0;
             if ((g.flags & 4) || !aligned || span > kStageElems || T > kFastMaxT || T > cap || !a.fast_ok) {
                 kind = 1;
             } else {
@@ -1377,11 +1391,58 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
     }
 }
 
-// ------------------------------------------------------- fast kernel body
-constexpr int kStageDw = kStageElems / 4 / kWave;   // staged dwords per lane
+// ------------------------------------------------------- fast kernel (v3)
+// Records of the dominant shape: every read a single M run (no insertion
+// column, no '-' row), <= 64 reads, bytes fit one LDS stage, T <= 240, every
+// staged quality <= 122 and every staged base a valid letter (else the record
+// is handed to the general kernel).  Then every aligned row is a base, a masked
+// 'N' or a pad 'N', and the consensus CIGAR is one M run over the trimmed span
+// (:797-848 yields M for every such column).
+//
+// Element codes ARE byte addresses of the likelihood table in LDS.  The table
+// is banked by class: bank N holds (p'/5, p'/5) and banks A/T/C/G hold
+// (1-p', p'/5) for every quality row, at LDS offsets whose bits 11-14 are the
+// class one-hot (N = 0).  For a column with one base class k the reference's
+// six products (:594-600) are then exactly two chains, in read order:
+//     s *= f.x   (the chain of class k: 1-p' on k rows, p'/5 on N rows)
+//     U *= f.y   (every other class: p'/5 on every row)
+// with no class compare or select per element; OR-ing the codes gives the
+// classes present and summing code >> 11 gives n * onehot(k).  A tile where
+// some column holds two base classes is recomputed with explicit class matches.
+//
+// Finalize: with one class present, S = s + 5U up to 5 roundings, so
+// e = 1 - s/S <= 5U/s + 6 ulp.  If 5U(1+d) < s * min(qthresh[maxQ], 1-thr, 1/4)(1-d)
+// the reference's quality is maxQ and the base is not masked (:699-709, :617),
+// with no division or phred search; other columns take finalize().
+//
+// LDS (one 40 KiB block of 4 waves, 4 blocks per CU):
+//   0x0000 bank N | 0x0800 bank A | 0x1000 bank T | 0x1800 bank X (never read:
+//   a record with an invalid byte leaves first) | 0x2000 bank C | 0x4000 bank G
+//   holes 0x1800-0x1fff and 0x2800-0x3fff: per-wave e/d columns; 0x4800+:
+//   stages (4 KiB per wave), e/d tables, pad sentinel.
+namespace fk {
+constexpr int kRowMax = 122;                               // quality rows 0..122 (+ bank index <= 127)
+constexpr uint32_t kPadCode = 16u * 2u;                    // bank N, quality 2 (:509-510, :543-544)
+constexpr int kStage = 0x4800;                             // 4 x 4 KiB
+constexpr int kEtab = kStage + kWavesPerBlock * 0x1000;    // 4 x 66 doubles
+constexpr int kEtabN = 66;
+constexpr int kSent = kEtab + kWavesPerBlock * kEtabN * 8;  // u16 pad code (out-of-read sentinel)
+constexpr int kLdsBytes = kSent + 16;
+static_assert(kStageElems * 2 == 0x1000, "one 4 KiB stage per wave");
+static_assert(kLdsBytes <= 40 * 1024, "4 blocks per CU");
+
+__device__ __forceinline__ int bank_base(int b) { return b == 5 ? 0x4000 : b << 11; }   // N A T X C G
+// per-wave e/d columns in the bank holes (1920 B each)
+__device__ __forceinline__ int et_off(int wave) {
+    return wave == 0 ? 0x1800 : 0x2800 + (wave - 1) * (kFastMaxT * 8);
+}
+static_assert(0x2800 + 3 * kFastMaxT * 8 <= 0x4000, "e/d columns fit the hole");
+}  // namespace fk
+
+constexpr int kStageQ = kStageElems / 16 / kWave;   // staged 16-byte quads per lane
 
 struct FastStage {
-    uint32_t vb[kStageDw], vq[kStageDw];   // raw base / quality dwords
+    uint4 vb[kStageQ], vq[kStageQ];        // raw base / quality bytes
     uint2 rm;                              // this lane's read meta (lane < R)
 };
 
@@ -1390,258 +1451,457 @@ template <bool DUPLEX>
 __device__ __forceinline__ void fast_load(const Args &a, const RecMeta &m, int lane, FastStage &st) {
     const uint8_t *gb = DUPLEX ? a.ss.seq : a.in.bases;
     const uint8_t *gq = DUPLEX ? a.ss.qual : a.in.quals;
-    const int nd = (int)(m.w >> 15);
-    const uint32_t *b4 = (const uint32_t *)(gb + m.base_al);
-    const uint32_t *q4 = (const uint32_t *)(gq + m.base_al);
+    const int nq = ((int)(m.w >> 15) + 3) >> 2;
+    const uint4 *b16 = (const uint4 *)(gb + m.base_al);
+    const uint4 *q16 = (const uint4 *)(gq + m.base_al);
+    // unconditional loads (indices clamped into the record): a select on the
+    // loaded value would make the compiler wait for it right here
 #pragma unroll
-    for (int u = 0; u < kStageDw; ++u) {
-        const int d = u * kWave + lane;
-        st.vb[u] = d < nd ? b4[d] : 0u;
-        st.vq[u] = d < nd ? q4[d] : 0u;
+    for (int u = 0; u < kStageQ; ++u) {
+        const int d = min(u * kWave + lane, nq - 1);
+        st.vb[u] = b16[d];
+        st.vq[u] = q16[d];
     }
     const int R = (int)(m.w & 127u);
-    st.rm = lane < R ? a.ws.rmeta[m.g0 + lane] : make_uint2(0u, 0u);
+    st.rm = a.ws.rmeta[m.g0 + min(lane, R - 1)];
 }
 
-// four element codes (q | class << 9) from four bases and qualities, SWAR:
-// the class comes from a byte permute indexed by (b >> 1) & 7, which is
-// distinct for A C T G N; a second permute returns the letter each index
-// stands for, and any byte that differs from it is an invalid character
-// (class 7, :582).  Single-strand inputs then mask qual < min_base_quality to
-// class 6 ('N', keeping the quality: mask_low_quality_bases :280).
-typedef short dcr_v2i16 __attribute__((ext_vector_type(2)));
-
+// Four element codes from four bases and qualities (SWAR).  The class comes
+// from a byte permute indexed by (b >> 1) & 7, distinct for A C T G N; a second
+// permute gives the letter of that index, and a byte that differs from it is
+// not a valid nucleotide (:580-585): flagged in `bad` (the record then goes to
+// the general kernel, which reproduces the exit), as is a quality > 122.
+// Single-strand inputs mask qual < min_base_quality to bank N keeping the
+// quality (:280): v_lerp_u8 computes (q + 256 - m) >> 1, whose bit 7 is q >= m.
+// code = bank_base + 16 * (bank index + q): bank index N0 A1 T2 X3 C4 G5.
 template <bool DUPLEX>
-__device__ __forceinline__ uint2 make_codes4(uint32_t B, uint32_t Q, uint32_t m2) {
+__device__ __forceinline__ uint2 make_codes4(uint32_t B, uint32_t Q, uint32_t kq, uint32_t &bad) {
     const uint32_t h = (B >> 1) & 0x07070707u;
-    uint32_t cls = __builtin_amdgcn_perm(0x06070707u, 0x03010200u, h);       // A0 C2 T1 G3 . . . N6
-    const uint32_t x = B ^ __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, h);
-    const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;   // 0x80 where byte != letter
-    cls |= ((nz << 1) - (nz >> 7)) & 0x07070707u;
+    uint32_t idx = __builtin_amdgcn_perm(0x00030303u, 0x05020401u, h);           // A1 C4 T2 G5 . . . N0
+    uint32_t x = B ^ __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, h);         // 0 for a valid letter
     if (!DUPLEX) {
-        const dcr_v2i16 qe = __builtin_bit_cast(dcr_v2i16, Q & 0x00FF00FFu);
-        const dcr_v2i16 qo = __builtin_bit_cast(dcr_v2i16, (Q >> 8) & 0x00FF00FFu);
-        const dcr_v2i16 mm = __builtin_bit_cast(dcr_v2i16, m2);
-        const uint32_t de = __builtin_bit_cast(uint32_t, (dcr_v2i16)(qe - mm));
-        const uint32_t dd = __builtin_bit_cast(uint32_t, (dcr_v2i16)(qo - mm));
-        const uint32_t lt = ((de >> 15) & 0x00010001u) | ((dd >> 7) & 0x01000100u);   // 1 where q < min_bq
-        const uint32_t ff = (lt << 8) - lt;
-        cls = (ff & 0x06060606u) | (cls & ~ff);
+        const uint32_t L = __builtin_amdgcn_lerp(Q, kq, 0x01010101u);
+        const uint32_t keep = __builtin_amdgcn_perm(L << 8, L, 0x090B080Au);      // 0xff per kept byte
+        idx &= keep;
+        x &= keep;                                                                // masked bytes are 'N'
     }
-    const uint32_t c2 = cls << 1;
-    return make_uint2(__builtin_amdgcn_perm(c2, Q, 0x05010400u), __builtin_amdgcn_perm(c2, Q, 0x07030602u));
+    bad |= x | (((Q + 0x05050505u) | Q) & 0x80808080u);
+    const uint32_t bank = __builtin_amdgcn_perm(0x00004020u, 0x18100800u, idx);  // one-hot << 3 per byte
+    const uint32_t w = idx + Q;                                                   // per byte, <= 127
+    const uint32_t hi = ((w >> 4) & 0x07070707u) | bank;
+    const uint32_t lo = (w << 4) & 0xF0F0F0F0u;
+    return make_uint2(__builtin_amdgcn_perm(hi, lo, 0x05010400u), __builtin_amdgcn_perm(hi, lo, 0x07030602u));
 }
 
-struct FastParams {
-    uint32_t m2;          // min_base_quality clamped to [0, 256], both 16-bit halves
-    int maxq;
-    bool simple_q;
-    double pre, post, thr;
+// general-slot form of a code (class << 9 | quality) for the exact loops
+__device__ __forceinline__ uint32_t code_to_elem(uint32_t code) {
+    const uint32_t nib = code >> 11;
+    const uint32_t bidx = (uint32_t)(0x500043210ull >> (4 * nib)) & 15u;
+    const uint32_t cls = (uint32_t)(0x300027106ull >> (4 * nib)) & 15u;
+    const uint32_t q = ((code & 0x7F0u) >> 4) - bidx;
+    return (cls << 9) | q;
+}
+
+// LDS address of read r's element code at the lane's column t, or the pad
+// sentinel outside the read
+struct ReadAddr {
+    int cr;        // byte address of the read's column 0 in the stage
+    int col, len;
+    bool full;     // the read covers every column: no bounds test
 };
 
+__device__ __forceinline__ ReadAddr read_addr(const uint2 rm, int r, int stage_addr, int T) {
+    const int x = readlane((int)rm.x, r);
+    const int y = readlane((int)rm.y, r);
+    ReadAddr ra;
+    ra.col = x & 255;
+    ra.len = (x >> 8) & 255;
+    ra.cr = stage_addr + 2 * (y - ra.col);
+    ra.full = ra.col == 0 && ra.len >= T;
+    return ra;
+}
 
-template <bool DUPLEX>
-__device__ __forceinline__ void process_fast(const Args &a, const FastParams &fp, const RecMeta &m, FastStage &st,
-                                             const bool has_next, const RecMeta &mn, WaveLds &W,
-                                             const double2 *s_lut, const double *s_qthr, const int lane) {
+__device__ __forceinline__ uint32_t code_at(const uint8_t *lds, const ReadAddr &ra, int t) {
+    uint32_t a = 2u * (uint32_t)t + (uint32_t)ra.cr;
+    if (!ra.full) a = (uint32_t)(t - ra.col) < (uint32_t)ra.len ? a : (uint32_t)fk::kSent;
+    return *(const uint16_t *)(lds + a);
+}
+
+template <int NT>
+struct Chains {
+    double U[NT], s[NT];
+    uint32_t seen[NT], cnt[NT];
+};
+
+// Products in read order, two reads per step (NT <= 3): the table rows of
+// reads r and r + 1 are in flight together while the codes of r + 2 and r + 3
+// are read.
+template <int NT>
+__device__ __forceinline__ void run_chains(Chains<NT> &c, const uint8_t *lds, int R, const uint2 rm,
+                                           int stage_addr, int T, int lane) {
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+        c.U[tt] = 1.0;
+        c.s[tt] = 1.0;
+        c.seen[tt] = 0;
+        c.cnt[tt] = 0;
+    }
+    auto codes = [&](int r, uint32_t (&cd)[NT]) {
+        const ReadAddr ra = read_addr(rm, min(r, R - 1), stage_addr, T);
+        if (ra.full) {                 // the common read: no bounds test (uniform branch)
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) cd[tt] = *(const uint16_t *)(lds + 2u * (uint32_t)(64 * tt + lane) + (uint32_t)ra.cr);
+        } else {
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) {
+                const int t = 64 * tt + lane;
+                const uint32_t a = (uint32_t)(t - ra.col) < (uint32_t)ra.len ? 2u * (uint32_t)t + (uint32_t)ra.cr
+                                                                             : (uint32_t)fk::kSent;
+                cd[tt] = *(const uint16_t *)(lds + a);
+            }
+        }
+    };
+    auto mul = [&](const uint32_t (&cd)[NT], const double2 (&f)[NT]) {
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            c.seen[tt] |= cd[tt];
+            c.cnt[tt] += cd[tt] >> 11;
+            c.s[tt] *= f[tt].x;
+            c.U[tt] *= f[tt].y;
+        }
+    };
+    uint32_t c0[NT], c1[NT];
+    codes(0, c0);
+    int r = 0;
+    if constexpr (NT <= 3) {
+        codes(1, c1);
+        for (; r + 2 <= R; r += 2) {
+            double2 f0[NT], f1[NT];
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) {
+                f0[tt] = *(const double2 *)(lds + c0[tt]);
+                f1[tt] = *(const double2 *)(lds + c1[tt]);
+            }
+            uint32_t n0[NT], n1[NT];
+            codes(r + 2, n0);
+            codes(r + 3, n1);
+            mul(c0, f0);
+            mul(c1, f1);
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) {
+                c0[tt] = n0[tt];
+                c1[tt] = n1[tt];
+            }
+        }
+    }
+    // one read per step (NT = 4 keeps its registers for the chains)
+    for (; r < R; ++r) {
+        double2 f0[NT];
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) f0[tt] = *(const double2 *)(lds + c0[tt]);
+        uint32_t n0[NT];
+        codes(r + 1, n0);
+        mul(c0, f0);
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) c0[tt] = n0[tt];
+    }
+}
+
+// the chains of the (at most two) base classes b0, b1 (bank bits) of a column,
+// explicit class matches, read order; four reads per batch so their codes and
+// table rows are each one LDS round trip
+__device__ __forceinline__ void two_chains(const uint8_t *lds, const uint2 rm, int R, int t, int stage_addr, int T,
+                                           uint32_t b0, uint32_t b1, double &U, double &s0, double &s1, int &n0,
+                                           int &n1) {
+    U = 1.0;
+    s0 = 1.0;
+    s1 = 1.0;
+    n0 = 0;
+    n1 = 0;
+    auto step = [&](uint32_t code, double2 f) {
+        const bool m0 = (code & b0) != 0, m1 = (code & b1) != 0;
+        U *= f.y;
+        s0 *= m0 ? f.x : f.y;
+        s1 *= m1 ? f.x : f.y;
+        n0 += m0;
+        n1 += m1;
+    };
+    int r = 0;
+    for (; r + 4 <= R; r += 4) {
+        uint32_t c[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c[k] = code_at(lds, read_addr(rm, r + k, stage_addr, T), t);
+        double2 f[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) f[k] = *(const double2 *)(lds + c[k]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) step(c[k], f[k]);
+    }
+    for (; r < R; ++r) {
+        const uint32_t c = code_at(lds, read_addr(rm, r, stage_addr, T), t);
+        step(c, *(const double2 *)(lds + c));
+    }
+}
+
+// per-lane destination of the record scalars (lane k: field k of dcr_out,
+// address = optr + rec * rec_mul + off * off_mul)
+struct FastPtr {
+    uint8_t *optr;
+    int64_t rec_mul, off_mul;
+};
+
+__device__ __forceinline__ FastPtr fast_ptr(const dcr_out &O, int lane) {
+    FastPtr f;
+    f.rec_mul = lane < 7 ? 4 : (lane < 9 ? 8 : 0);
+    f.off_mul = lane == 9 ? 4 : 0;
+    uint8_t *p;
+    switch (lane) {
+    case 0: p = (uint8_t *)O.pos; break;
+    case 1: p = (uint8_t *)O.mapq; break;
+    case 2: p = (uint8_t *)O.len; break;
+    case 3: p = (uint8_t *)O.n_cig; break;
+    case 4: p = (uint8_t *)O.n_de; break;
+    case 5: p = (uint8_t *)O.D; break;
+    case 6: p = (uint8_t *)O.M; break;
+    case 7: p = (uint8_t *)O.E; break;
+    case 8: p = (uint8_t *)O.E + 4; break;
+    default: p = (uint8_t *)O.cigar; break;
+    }
+    f.optr = p;
+    return f;
+}
+
+template <bool DUPLEX, int NT>
+__device__ __forceinline__ void process_fast(const Args &a, const RecMeta &m, FastStage &st, const bool has_next,
+                                             const RecMeta &mn, uint8_t *lds, const int wave, const int lane,
+                                             int &etab_r, uint64_t *stp, const FastPtr &fp) {
+    uint64_t t_prev = 0;
+    auto stamp = [&](int k) {
+        if (DCR_STAMP) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            if (k > 0) stp[k - 1] += now - t_prev;
+            t_prev = now;
+        }
+    };
+    stamp(0);
+    if (DCR_STAMP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(1);                          // [0] wait for this record's prefetched bytes
+    const dcr_params *P = a.P;
     const dcr_out &O = DUPLEX ? a.ds : a.ss;
     const int64_t rec = m.rec;
     const int64_t off = m.off;
     const int R = (int)(m.w & 127u);
     const int T = (int)((m.w >> 7) & 255u);
-    const int nd = (int)(m.w >> 15);
+    const int nq = ((int)(m.w >> 15) + 3) >> 2;
     const int minpos = m.minpos;
+    const int stage_addr = fk::kStage + (wave << 12);
+    double *et = (double *)(lds + fk::et_off(wave));
+    double *etab = (double *)(lds + fk::kEtab) + wave * fk::kEtabN;
 
-    // phase 0: element codes into LDS
+    // phase 0: element codes into the stage
+    uint32_t bad = 0;
 #pragma unroll
-    for (int u = 0; u < kStageDw; ++u) {
+    for (int u = 0; u < kStageQ; ++u) {
         const int d = u * kWave + lane;
-        if (d < nd) *(uint2 *)&W.stage[4 * d] = make_codes4<DUPLEX>(st.vb[u], st.vq[u], fp.m2);
+        if (d < nq) {
+            const uint2 c0 = make_codes4<DUPLEX>(st.vb[u].x, st.vq[u].x, a.fast_kq, bad);
+            const uint2 c1 = make_codes4<DUPLEX>(st.vb[u].y, st.vq[u].y, a.fast_kq, bad);
+            const uint2 c2 = make_codes4<DUPLEX>(st.vb[u].z, st.vq[u].z, a.fast_kq, bad);
+            const uint2 c3 = make_codes4<DUPLEX>(st.vb[u].w, st.vq[u].w, a.fast_kq, bad);
+            *(uint4 *)(lds + stage_addr + 32 * d) = make_uint4(c0.x, c0.y, c1.x, c1.y);
+            *(uint4 *)(lds + stage_addr + 32 * d + 16) = make_uint4(c2.x, c2.y, c3.x, c3.y);
+        }
     }
-    FastReads fr;
-    fr.x = (int)st.rm.x;
-    fr.y = (int)st.rm.y;
-    const int msum = wave_sum(lane < R ? (fr.x >> 16) & 255 : 0);
-    // prefetch the next record; its loads complete under this record's work
+    const uint2 rm = st.rm;            // this record's read meta; st is reused by the prefetch
+    const int msum = wave_sum(lane < R ? ((int)rm.x >> 16) & 255 : 0);
+    stamp(2);                          // [1] element codes into LDS
     if (has_next) fast_load<DUPLEX>(a, mn, lane, st);
+    stamp(3);                          // [2] prefetch issue
+    auto to_general = [&]() {
+        if (lane == 0) {
+            const int idx = atomicAdd(&a.ws.ovf_count[DUPLEX ? 1 : 0], 1);
+            a.ws.ovf[idx] = (int)rec;
+        }
+    };
+    if (__ballot(bad != 0)) { to_general(); return; }
+    if (DCR_ABL == 1) {                 // diagnostic: staging only
+        lds_fence();
+        if (lane == 0) O.pos[rec] = *(const uint16_t *)(lds + stage_addr + 2 * (int)(rm.y & 7)) + msum;
+        return;
+    }
+    // e/d of a one-class column: d = n rows of the class, e = R - n (:1001-1012)
+    if (R != etab_r) {
+        if (lane < R) etab[lane] = lane == 0 ? 1.0 : (double)(R - lane) / (double)lane;
+        if (lane == 0) etab[R] = 0.0;
+        etab_r = R;
+    }
     lds_fence();
-    if (DCR_ABL == 1) {
-        if (lane == 0) O.pos[rec] = minpos + nd + (int)W.stage[lane] + msum;
+
+    stamp(4);                          // [3] e/d table, fence
+    Chains<NT> c;
+    run_chains<NT>(c, lds, R, rm, stage_addr, T, lane);
+    stamp(5);                          // [4] products
+    if (DCR_ABL == 2) {                 // diagnostic: staging + products
+        double x = 0.0;
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) x += c.s[tt] + c.U[tt] + (double)(c.seen[tt] ^ c.cnt[tt]);
+        if (lane == 0) O.E[rec] = x;
         return;
     }
 
-    auto write_status = [&](int s) {
-        if (lane == 0) write_status_at(O, rec, s);
-    };
-    uint16_t *od = O.d + off;
-    uint16_t *oe = O.e + off;
-    int dmax = -1, dmin = 0x7fffffff, first = -1, last = -1;
-    bool bad = false, qoverflow = false;
-
-    for (int c0 = 0; c0 < T; c0 += kWave) {
-        const int t = c0 + lane;
-        const bool live = t < T;
-        // pre-scan: classes present in this column
-        uint32_t mask = 0;
-        {
-            int r = 0;
-            for (; r + 4 <= R; r += 4) {
-                const uint32_t e0 = fast_elem(fr, r, t, W.stage);
-                const uint32_t e1 = fast_elem(fr, r + 1, t, W.stage);
-                const uint32_t e2 = fast_elem(fr, r + 2, t, W.stage);
-                const uint32_t e3 = fast_elem(fr, r + 3, t, W.stage);
-                mask |= (1u << (e0 >> 9)) | (1u << (e1 >> 9)) | (1u << (e2 >> 9)) | (1u << (e3 >> 9));
-            }
-            for (; r < R; ++r) mask |= 1u << (fast_elem(fr, r, t, W.stage) >> 9);
-        }
-        bad |= (mask & 0x80u) != 0;               // invalid character (:582)
-        const uint32_t cm = mask & 0x0fu;         // base classes A T C G
-        int k[4] = {-1, -1, -1, -1};
-        {
-            uint32_t mm = cm;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                k[q] = mm ? __builtin_ctz(mm) : -1;
-                mm &= mm - 1;
-            }
-        }
-        const int pc = __popc(cm);                 // wave max of pc by ballots (no LDS)
-        const int nsl = __ballot(pc >= 3) ? 4 : __ballot(pc >= 2) ? 2 : __ballot(pc >= 1) ? 1 : 0;
-        double U = 1.0;
-        double sl[4] = {1.0, 1.0, 1.0, 1.0};
-        int n[4] = {0, 0, 0, 0};
-        switch (nsl) {
-        case 0: fast_products<0>(U, sl, n, k, R, t, fr, W.stage, s_lut); break;
-        case 1: fast_products<1>(U, sl, n, k, R, t, fr, W.stage, s_lut); break;
-        case 2: fast_products<2>(U, sl, n, k, R, t, fr, W.stage, s_lut); break;
-        default: fast_products<4>(U, sl, n, k, R, t, fr, W.stage, s_lut); break;
-        }
-        if (DCR_ABL == 2) {
-            if (live) W.cons[t] = (int)(U * 1e9) + n[0] + (int)sl[1];
-            continue;
-        }
-        // L_i: its chain if class i is present, else U ('+', '-' never are)
-        double L[6] = {U, U, U, U, U, U};
-        int c[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const bool mt = k[q] == i;
-                L[i] = mt ? sl[q] : L[i];
-                c[i] = mt ? n[q] : c[i];
-            }
-        }
-        const int cN = R - c[0] - c[1] - c[2] - c[3];
-        // posterior (:603-614): S > 0 here (products of positive factors) unless
-        // everything underflowed; zero S keeps the reference's NaN semantics
-        double S = L[0] + L[1];
-        S = S + L[2];
-        S = S + L[3];
-        S = S + L[4];
-        S = S + L[5];
-        int best = 0;
-        double Lb = L[0];
-#pragma unroll
-        for (int i = 1; i < 6; ++i) {
-            const bool g = L[i] > Lb;
-            best = g ? i : best;
-            Lb = g ? L[i] : Lb;
-        }
-        double pm = Lb / S;                        // NaN when S == 0: argmax 0 ('A')
-        if (__builtin_expect(S > 0.0, 1)) {
-            const double near = Lb * 0.99999999999999;
-            bool tie = false;
-#pragma unroll
-            for (int i = 0; i < 5; ++i) tie |= (i < best) && (L[i] >= near);
-            if (__builtin_expect(tie, 0)) {
-#pragma unroll
-                for (int i = 4; i >= 0; --i)
-                    if (i < best && L[i] >= near && L[i] / S == pm) best = i;
-            }
-        } else {
-            best = 0;
-        }
-        const bool masked = pm < fp.thr;
-        const int ch = masked ? 'N' : (int)((0x2D2B47435441ull >> (8 * best)) & 0xffu);
-        const double e = 1.0 - pm;
-        const double x = fp.simple_q ? e : fp.pre * (1.0 - e) + (1.0 - fp.post) * e + fp.pre * e * 4.0 / 5.0;
-        int q = fp.maxq;
-        if (x > 0.0) {
-            if (__builtin_isinf(x)) qoverflow = true;
-            else q = phred_from_table(x, fp.maxq, s_qthr);
-        }
-        // depth / errors (:1001-1012): no '+' rows and no '+' consensus here
-        const int d = R - cN;
-        int cnt = cN;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) cnt = (!masked && best == i) ? c[i] : cnt;
-        if (!masked && best >= 4) cnt = 0;
-        const int er = R - cnt;
+    int dmax = -1, dmin = 0x7fffffff;
+    // One column's results, kept in registers (d | e << 8 | char << 16 per tile)
+    // and written out at the end with 16-byte stores.  Every column of this
+    // kernel is called inside the fast bound (quality maxQ, a base, never
+    // masked), so there is no consensus 'N' to trim (:770-784): the kept span
+    // is [0, T), one M run.
+    uint32_t ov[NT];
+    double ex[NT];                     // e/d of the lane's column per tile (0 outside T)
+    auto put = [&](int t, bool live, int ch, int d, int e, double etv) -> uint32_t {
         if (live) {
-            W.cons[t] = ch | (q << 8);
-            od[t] = (uint16_t)d;
-            oe[t] = (uint16_t)er;
-            W.et[t] = d == 0 ? 1.0 : (double)er / (double)d;
+            et[t] = etv;
             dmax = max(dmax, d);
             dmin = min(dmin, d);
         }
-        const uint64_t nn = __ballot(live && ch != 'N');
-        if (nn) {
-            if (first < 0) first = c0 + __builtin_ctzll(nn);
-            last = c0 + 63 - __builtin_clzll(nn);
+        return (uint32_t)d | ((uint32_t)e << 8) | ((uint32_t)ch << 16);
+    };
+    // one-class columns (compile-time tile indices: chain registers are not
+    // indexed dynamically); every tile's table lookup is issued before use
+    uint32_t defer = 0;                // tiles needing the two-class path (uniform bit mask)
+    uint32_t banks = 0;                // classes present per column, 4 bits per tile
+    int kk[NT], nn_[NT];
+    bool fast[NT];
+    double ev[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+        const uint32_t bank = (c.seen[tt] >> 11) & 15u;
+        kk[tt] = bank ? __builtin_ctz(bank) : 0;
+        nn_[tt] = (int)(c.cnt[tt] >> kk[tt]);
+        fast[tt] = (bank & (bank - 1u)) == 0 && nn_[tt] > 0 && (5.0 * c.U[tt]) * a.fast_ca < c.s[tt] * a.fast_cb;
+        ev[tt] = etab[min(nn_[tt], R)];
+        banks |= bank << (4 * tt);
+    }
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+        const int t = 64 * tt + lane;
+        const bool live = t < T;
+        ov[tt] = 0;
+        ex[tt] = 0.0;
+        if (DCR_ABL != 3 && __ballot(live && !fast[tt])) {
+            defer |= 1u << tt;
+            continue;
         }
+        ov[tt] = put(t, live, (int)((0x47435441u >> (8 * kk[tt])) & 0xffu), nn_[tt], R - nn_[tt], ev[tt]);   // "ATCG"
+        ex[tt] = live ? ev[tt] : 0.0;
     }
-    if (DCR_ABL == 2 || DCR_ABL == 3) {
-        if (lane == 0) O.pos[rec] = W.cons[0] + first + last;
-        return;
+    stamp(6);                          // [5] one-class tiles
+    // other tiles: the chains of the two classes present, explicit class
+    // matches, in read order.  A column with three or more classes, or outside
+    // the bound (a low-confidence or masked call, :617), sends the record to the
+    // general kernel, which runs the reference's full finalize.
+    while (defer) {
+        const int tt = __builtin_ctz(defer);
+        defer &= defer - 1u;
+        const int t = 64 * tt + lane;
+        const bool live = t < T;
+        const uint32_t bank = (banks >> (4 * tt)) & 15u;
+        if (wave_max(live ? __popc(bank) : 0) > 2) { to_general(); return; }
+        const int k0 = bank ? __builtin_ctz(bank) : -1;
+        const uint32_t rest = bank & (bank - 1u);
+        const int k1 = rest ? __builtin_ctz(rest) : -1;
+        double U, s0, s1;
+        int n0, n1;
+        two_chains(lds, rm, R, t, stage_addr, T, k0 >= 0 ? 0x800u << k0 : 0u, k1 >= 0 ? 0x800u << k1 : 0u, U, s0, s1,
+                   n0, n1);
+        // the bound with the largest chain b against the rest: S = b + other + 4U
+        const bool two = k1 >= 0;
+        const bool hi1 = two && s1 > s0;
+        const double bb = hi1 ? s1 : s0;
+        const double other = two ? (hi1 ? s0 : s1) + 4.0 * U : 5.0 * U;
+        const bool fst = k0 >= 0 && other * a.fast_ca < bb * a.fast_cb;
+        if (__ballot(live && !fst)) { to_general(); return; }
+        const int kb = hi1 ? k1 : k0;
+        const int d = n0 + (two ? n1 : 0), e = R - (hi1 ? n1 : n0);
+        const double etv = (double)e / (double)d;
+        const uint32_t v = put(t, live, (int)((0x47435441u >> (8 * (kb & 3))) & 0xffu), d, e, etv);
+#pragma unroll
+        for (int k = 0; k < NT; ++k)   // constant register index per case
+            if (k == tt) {
+                ov[k] = v;
+                ex[k] = live ? etv : 0.0;
+            }
     }
-    const bool anybad = __ballot(bad) != 0;
-    qoverflow = __ballot(qoverflow) != 0;
-    if (anybad) { write_status(DCR_ST_EXIT_BADCHAR); return; }
-    if (qoverflow) { write_status(DCR_ST_OVERFLOW_ERROR); return; }
-    if (first < 0) { write_status(DCR_ST_INDEX_ERROR); return; }   // all 'N': compress_cigarlist([])
+    stamp(7);                          // [6] two-class tiles
     const int Dmax = wave_max(dmax);
     const int Dmin = wave_min(dmin);
-    lds_fence();
-    // field layout: trimmed span [first, last] is all M (:770-848, :858-865)
-    const int lo = first, hi = last + 1;
-    uint8_t *oseq = O.seq + off;
-    uint8_t *oqual = O.qual + off;
-    bool kept_overflow = false;
-    for (int c0 = lo; c0 < hi; c0 += kWave) {
-        const int t = c0 + lane;
-        if (t < hi) {
-            const int v = W.cons[t];
-            const int qq = v >> 8;
-            oseq[t - lo] = (uint8_t)(v & 255);
-            oqual[t - lo] = (uint8_t)qq;
-            kept_overflow |= (qq < 0 || qq > 255);
+    // d / e / seq / qual straight from registers; the region tail up to the
+    // next 16 columns gets 'N' / quality 0 so a duplex record staging this
+    // region never reads a byte that is not a valid letter
+    {
+        const int T16 = (T + 15) & ~15;
+        uint16_t *od = O.d + off;
+        uint16_t *oe = O.e + off;
+        uint8_t *oseq = O.seq + off;
+        uint8_t *oqual = O.qual + off;
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            const int t = 64 * tt + lane;
+            if (t < T) {
+                od[t] = (uint16_t)(ov[tt] & 255u);
+                oe[t] = (uint16_t)((ov[tt] >> 8) & 255u);
+                oseq[t] = (uint8_t)(ov[tt] >> 16);
+                oqual[t] = (uint8_t)a.fast_maxq;
+            } else if (t < T16) {
+                oseq[t] = (uint8_t)'N';
+                oqual[t] = (uint8_t)0;
+            }
         }
     }
-    if (__ballot(kept_overflow)) { write_status(DCR_ST_OVERFLOW_ERROR); return; }
-    // E = round(mean(e/d), 3) with numpy's pairwise summation over T values
-    const double total = 0.0 + pairwise_small(W.et, T, lane);
-    const double E = __builtin_rint((total / (double)T) * 1000.0) / 1000.0;
-    if (lane == 0) {
-        O.status[rec] = DCR_ST_OK;
-        O.pos[rec] = minpos + lo;
-        O.mapq[rec] = msum / R;
-        O.len[rec] = hi - lo;
-        O.n_cig[rec] = 1;
-        O.cigar[off] = ((uint32_t)(hi - lo) << 4) | 0u;
-        O.n_de[rec] = T;
-        O.D[rec] = Dmax;
-        O.M[rec] = Dmin;
-        O.E[rec] = E;
+    stamp(8);                          // [7] depth reductions, per-column stores
+    // E = round(mean(e/d), 3) (:1015-1018).  numpy's mean is a pairwise sum
+    // divided by T, then rounded at 3 decimals.  Any summation order lands
+    // within 1e-12 (relative) of it, so the rounding agrees unless mean x 1000
+    // sits that close to a half-integer; a DPP tree sum decides, and the exact
+    // pairwise walk over the LDS copy runs only near such a boundary.
+    double sum = 0.0;
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) sum += ex[tt];
+    sum += dpp_f64<0xB1>(sum);                   // quad_perm [1,0,3,2]
+    sum += dpp_f64<0x4E>(sum);                   // quad_perm [2,3,0,1]
+    sum += dpp_f64<0x141>(sum);                  // row_half_mirror
+    sum += dpp_f64<0x140>(sum);                  // row_mirror
+    sum = (readlane_f64(sum, 0) + readlane_f64(sum, 16)) + (readlane_f64(sum, 32) + readlane_f64(sum, 48));
+    const double y = (sum / (double)T) * 1000.0;
+    const double fr = y - __builtin_floor(y);
+    double E;
+    if (__builtin_expect(__builtin_fabs(fr - 0.5) > 1e-9 * (1.0 + y), 1) && DCR_ABL != 4) {
+        E = __builtin_rint(y) / 1000.0;
+    } else {
+        lds_fence();
+        const double total = 0.0 + pairwise_et(et, T, lane);
+        E = __builtin_rint((total / (double)T) * 1000.0) / 1000.0;
     }
+    stamp(9);                          // [8] mean
+    // the record's scalar fields in one dword store (lane k writes field k,
+    // lane 9 the single M run of the CIGAR) plus the status byte
+    {
+        const int E_lo = (int)(uint32_t)__double_as_longlong(E);
+        const int E_hi = (int)(uint32_t)((uint64_t)__double_as_longlong(E) >> 32);
+        const int v = lane == 0 ? minpos                       // pos (:790)
+                      : lane == 1 ? msum / R                   // MAPQ (:874-889, :1377)
+                      : lane == 2 ? T                          // len
+                      : lane == 3 ? 1                          // n_cig
+                      : lane == 4 ? T                          // n_de
+                      : lane == 5 ? Dmax
+                      : lane == 6 ? Dmin
+                      : lane == 7 ? E_lo
+                      : lane == 8 ? E_hi
+                                  : (int)((uint32_t)T << 4);   // one M run of T
+        if (lane < 10) *(int *)(fp.optr + rec * fp.rec_mul + off * fp.off_mul) = v;
+        if (lane == 0) O.status[rec] = DCR_ST_OK;
+    }
+    stamp(10);                         // [9] record scalars
 }
-
-// Each wave takes kFastChunk consecutive fast-list records; record i + 1's
-// loads are issued while record i is processed, and the metadata of record
-// i + 2 is fetched by a vector load (vmcnt, not lgkmcnt, so LDS waits never
-// drain it).  Hardware block dispatch balances the chunks over the CUs.
-constexpr int kFastChunk = 8;
 
 __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
     RecMeta m;
@@ -1654,48 +1914,55 @@ __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
     return m;
 }
 
+// Persistent: wave w of NW takes the contiguous fast-list range
+// [n w / NW, n (w+1) / NW); record i + 1's loads are issued while record i is
+// processed, and the descriptor of record i + 2 is fetched by a vector load
+// (vmcnt, not lgkmcnt, so LDS waits never drain it).
 template <bool DUPLEX>
-__global__ __launch_bounds__(kBlock, 4) void k_consensus_fast(Args a) {
-    __shared__ double2 s_lut[DCR_LUT_N];
-    __shared__ double s_qthr[DCR_MAX_QTHRESH];
-    __shared__ WaveLds s_wave[kWavesPerBlock];
+__global__ __launch_bounds__(kBlock, 3) void k_consensus_fast(Args a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[fk::kLdsBytes];
     const dcr_params *P = a.P;
-    for (int i = threadIdx.x; i < DCR_LUT_N; i += kBlock) s_lut[i] = make_double2(P->match[i], P->mismatch[i]);
-    for (int i = threadIdx.x; i < DCR_MAX_QTHRESH; i += kBlock) s_qthr[i] = P->qthresh[i];
+    for (int i = threadIdx.x; i < 6 * (fk::kRowMax + 1); i += kBlock) {
+        const int b = i / (fk::kRowMax + 1), q = i % (fk::kRowMax + 1);
+        if (b == 3) continue;                                 // bank X: e/d columns live there
+        const double mm = P->mismatch[q];
+        *(double2 *)(lds + fk::bank_base(b) + 16 * b + 16 * q) = make_double2(b == 0 ? mm : P->match[q], mm);
+    }
+    if (threadIdx.x == 0) *(uint16_t *)(lds + fk::kSent) = (uint16_t)fk::kPadCode;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    WaveLds &W = s_wave[wave];
-    if (lane == 0) W.pad_code[0] = (uint16_t)kPad;
-    FastParams fp;
-    {
-        const int mb = min(max(P->min_base_quality, 0), 256);
-        fp.m2 = (uint32_t)mb | ((uint32_t)mb << 16);
-        fp.maxq = P->max_base_quality;
-        fp.simple_q = P->error_rate_pre_labeling == 0 && P->error_rate_post_labeling == 0;
-        fp.pre = (double)P->error_rate_pre_labeling;
-        fp.post = (double)P->error_rate_post_labeling;
-        fp.thr = P->post_threshold;
-    }
     __syncthreads();
-    const int n = a.ws.fast_count[DUPLEX ? 1 : 0];
-    int i = (blockIdx.x * kWavesPerBlock + wave) * kFastChunk;
-    if (i >= n) return;
-    const int iend = min(i + kFastChunk, n);
+    const int64_t n = a.ws.fast_count[DUPLEX ? 1 : 0];
+    const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
+    const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+    int i = (int)(n * gw / nw);
+    const int iend = (int)(n * (gw + 1) / nw);
+    if (i >= iend) return;
     const RecMeta *ML = a.ws.meta;
     RecMeta m0 = ML[i];
     RecMeta m1 = ML[min(i + 1, iend - 1)];
     FastStage st;
     fast_load<DUPLEX>(a, m0, lane, st);
+    int etab_r = -1;
+    uint64_t stp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const FastPtr fp = fast_ptr(DUPLEX ? a.ds : a.ss, lane);
     for (;;) {
         const bool has_next = i + 1 < iend;
         const int i2 = min(i + 2, iend - 1);
         const uint32_t mv = lane < 8 ? ((const uint32_t *)(ML + i2))[lane] : 0u;
-        process_fast<DUPLEX>(a, fp, m0, st, has_next, m1, W, s_lut, s_qthr, lane);
+        const int T = (int)((m0.w >> 7) & 255u);
+        if (T <= 64) process_fast<DUPLEX, 1>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp, fp);
+        else if (T <= 128) process_fast<DUPLEX, 2>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp, fp);
+        else if (T <= 192) process_fast<DUPLEX, 3>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp, fp);
+        else process_fast<DUPLEX, 4>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp, fp);
         if (++i >= iend) break;
         m0 = m1;
         m1 = meta_from_lanes(mv);
     }
+    if (DCR_STAMP && lane == 0)
+        for (int k = 0; k < 10; ++k) atomicAdd(&a.ws.stamps[k + (DUPLEX ? 16 : 0)], (unsigned long long)stp[k]);
 }
+
 
 // persistent: drains the general list written by k_recmeta
 template <bool DUPLEX>

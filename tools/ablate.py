@@ -21,11 +21,12 @@ for path in libs:
     lib = ctypes.CDLL(path)
     lib.dcr_create.restype = ctypes.c_void_p
     lib.dcr_create.argtypes = [ctypes.c_int, ctypes.c_void_p]
-    for n in ("dcr_run_batch", "dcr_sync", "dcr_last_timing"):
+    for n in ("dcr_run_batch", "dcr_sync", "dcr_last_timing", "dcr_last_kernel_timing"):
         getattr(lib, n).restype = ctypes.c_int
     lib.dcr_run_batch.argtypes = [ctypes.c_void_p] * 4
     lib.dcr_sync.argtypes = [ctypes.c_void_p]
     lib.dcr_last_timing.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.dcr_last_kernel_timing.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     ctx = lib.dcr_create(0, ctypes.byref(P))
     handles.append((path, lib, ctx))
 res = {p: [] for p in libs}
@@ -34,12 +35,12 @@ for rnd in range(6):
         assert lib.dcr_run_batch(ctx, ctypes.byref(db.batch_struct), ctypes.byref(db.ss_struct),
                                  ctypes.byref(db.ds_struct)) == 0
         assert lib.dcr_sync(ctx) in (0, 3)
-        ms = (ctypes.c_float * 4)()
-        lib.dcr_last_timing(ctx, ms)
+        ms = (ctypes.c_float * 7)()
+        lib.dcr_last_kernel_timing(ctx, ms)
         if rnd:
-            res[path].append((ms[1], ms[2]))
+            res[path].append((ms[2], ms[5]))
 for path in libs:
     v = res[path]
     ss = sorted(x[0] for x in v)[len(v) // 2]
     ds = sorted(x[1] for x in v)[len(v) // 2]
-    print(f"{os.path.basename(path):24s} single-strand {ss:8.3f} ms  duplex {ds:8.3f} ms")
+    print(f"{os.path.basename(path):24s} fast<ss> {ss:8.3f} ms  fast<ds> {ds:8.3f} ms")
