@@ -53,7 +53,7 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 struct dcr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    // ev[0] batch start, ev[1..7] after k_prep, k_recmeta<ss>, fast<ss>, general<ss>,
+    // ev[0] batch start, ev[1..7] after (fused) prep, k_recmeta<ss>, fast<ss>, general<ss>,
     // k_recmeta<ds>, fast<ds>, general<ds>
     hipEvent_t ev[DCR_N_KERNEL_TIMES + 1] = {};
     dcr_params *d_params = nullptr;
@@ -211,13 +211,10 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     HIP_TRY(hipMemsetAsync(c->w.err, 0, 32, c->stream));
     c->last_reads = in->n_reads;
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-    if (in->n_reads > 0) {
-        const int nb = (in->n_reads + 255) / 256;
-        dcr::Workspace w;
-        std::memcpy(&w, &c->w, sizeof(w));
-        hipLaunchKernelGGL(dcr::k_prep, dim3(nb), dim3(256), 0, c->stream, *in, c->d_params, w);
-        HIP_TRY(hipGetLastError());
-    }
+    // per-read preprocessing (:191-325) is fused: k_recmeta<ss> analyses the
+    // clips and fully preprocesses the reads of records the fast kernel does
+    // not take; the fast kernel does the 3' trim of its own records.  ev[1]
+    // (the former k_prep slot) directly follows ev[0].
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     dcr::Args a;
     a.in = *in;

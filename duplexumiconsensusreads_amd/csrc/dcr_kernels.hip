@@ -114,9 +114,7 @@ __device__ __forceinline__ void wave_fence() {
 // mask_low_quality_bases (:268-289): base -> 'N' if qual < min_base_quality
 // (applied by the consumer); trim_3prime_N (:292-325): drop trailing 'N' and
 // cut as many entries from the END of the expanded CIGAR.
-__global__ __launch_bounds__(256) void k_prep(dcr_batch in, const dcr_params *P, Workspace ws) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= in.n_reads) return;
+__device__ __forceinline__ void prep_read(const dcr_batch &in, const dcr_params *P, const Workspace &ws, int64_t i) {
     const int minbq = P->min_base_quality;
     const uint32_t *cig = in.cigar + in.cig_off[i];
     const int n = in.cig_n[i];
@@ -183,6 +181,53 @@ __global__ __launch_bounds__(256) void k_prep(dcr_batch in, const dcr_params *P,
     inf.n_cig = nout;
     inf.has_ins = has_ins;
     ws.info[i] = inf;
+}
+
+__global__ __launch_bounds__(256) void k_prep(dcr_batch in, const dcr_params *P, Workspace ws) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < in.n_reads) prep_read(in, P, ws, i);
+}
+
+// Clip-only view of a read (remove_clipping :191-265 without the 3' N trim,
+// which needs the bases): kept window and whether the read is one M-like run
+// (=/X become M, :361-377) whose length matches the kept sequence.
+struct ClipView {
+    int64_t seq_start;
+    int len;          // kept length before trim_3prime_N
+    bool single_m;
+};
+
+__device__ __forceinline__ ClipView clip_view(const dcr_batch &in, int64_t i) {
+    const uint32_t *cig = in.cigar + in.cig_off[i];
+    const int n = in.cig_n[i];
+    int sc5 = 0, sc3 = 0, nm = 0, other = 0;
+    bool inseq = false, modified = false;
+    int64_t E = 0;
+    for (int j = 0; j < n; ++j) {
+        const uint32_t v = cig[j];
+        const int op = v & 15, ln = v >> 4;
+        if (op == 5) {
+            modified = true;
+        } else if (op == 4) {
+            modified = true;
+            if (!inseq) sc5 = ln; else sc3 = ln;
+        } else {
+            inseq = true;
+            E += ln;
+            if (op == 0 || op == 7 || op == 8) ++nm; else ++other;
+        }
+    }
+    ClipView cv;
+    int len = in.seq_len[i];
+    int start = 0;
+    if (modified) {
+        start = sc5;
+        len -= sc5 + sc3;
+    }
+    cv.seq_start = in.seq_off[i] + start;
+    cv.len = len;
+    cv.single_m = other == 0 && nm > 0 && E == (int64_t)len;
+    return cv;
 }
 
 // ------------------------------------------------------------ read access
@@ -1209,15 +1254,14 @@ template <bool DUPLEX, bool CIG>
 __device__ __forceinline__ RdLite rd_lite(const Args &a, int64_t k) {
     RdLite r;
     r.cig0 = 0;
-    if (!DUPLEX) {                              // k: read index
-        const dcr_read_info inf = a.ws.info[k];
+    if (!DUPLEX) {                              // k: read index; clips only (the 3' trim is the fast kernel's)
+        const ClipView cv = clip_view(a.in, k);
         r.pos = a.in.read_pos[k];
-        r.len = inf.len;
-        r.ncig = inf.n_cig;
-        r.status = inf.status;
+        r.len = cv.len;
+        r.ncig = cv.single_m ? 1 : 2;
+        r.status = cv.len <= 0 ? DCR_ST_TYPE_ERROR : 0;   // empty sequence: enumerate(None) at :279
         r.mapq = a.in.read_mapq[k];
-        r.seq_start = inf.seq_start;
-        if (CIG && r.ncig == 1 && r.len > 0) r.cig0 = a.ws.norm_cig[a.in.cig_off[k]];
+        r.seq_start = cv.seq_start;
     } else {                                    // k: single-strand record index
         r.pos = a.ss.pos[k];
         r.len = a.ss.len[k];
@@ -1315,7 +1359,7 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
         if (gr < gend) {
             const RdLite rd = rd_lite<DUPLEX, true>(a, gr);
             const int fl = (rd.status != 0) | ((rd.len <= 0) << 1) |
-                           ((rd.ncig != 1 || (rd.len > 0 && (rd.cig0 & 15u) != 0)) << 2);   // single M run only
+                           ((rd.ncig != 1 || (DUPLEX && rd.len > 0 && (rd.cig0 & 15u) != 0)) << 2);   // single M run only
             atomicMin(&agg[k].minpos, rd.pos);
             atomicMax(&agg[k].maxend, rd.pos + rd.len);
             if (fl) atomicOr(&agg[k].flags, fl);
@@ -1373,20 +1417,27 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
     const uint64_t lt = lanemask_lt(lane);
     if (kind == 0) a.ws.meta[basef + __popcll(bf & lt)] = m;
     if (kind == 1) a.ws.ovf[baseg + __popcll(bg & lt)] = (int)rk;
-    if (!bf) return;
+    // single-strand reads of records the fast kernel does not take need the full
+    // preprocessing (3' trim included) for the general kernel and the host
+    const bool prep = !DUPLEX && __ballot(vk && kind != 0) != 0;
+    if (!bf && !prep) return;
     lds_fence();
-    // pass 2: per-read metadata of fast records
+    // pass 2: per-read metadata of fast records, preprocessing of the others
     carry = -1;
     for (int64_t c = gbeg; c < gend; c += kWave) {
         const int k = read_record(c, g0, R, mark, lane, carry);
         const int64_t gr = c + lane;
-        if (gr < gend && agg[k].kind == 0) {
-            const RdLite rd = rd_lite<DUPLEX, false>(a, gr);
-            const int minpos = agg[k].minpos;
-            const int64_t base_al = (int64_t)agg[k].lo;
-            a.ws.rmeta[gr] = make_uint2((uint32_t)(rd.pos - minpos) | ((uint32_t)rd.len << 8) |
-                                            ((uint32_t)rd.mapq << 16),
-                                        (uint32_t)(rd.seq_start - base_al));
+        if (gr < gend) {
+            if (agg[k].kind == 0) {
+                const RdLite rd = rd_lite<DUPLEX, false>(a, gr);
+                const int minpos = agg[k].minpos;
+                const int64_t base_al = (int64_t)agg[k].lo;
+                a.ws.rmeta[gr] = make_uint2((uint32_t)(rd.pos - minpos) | ((uint32_t)rd.len << 8) |
+                                                ((uint32_t)rd.mapq << 16),
+                                            (uint32_t)(rd.seq_start - base_al));
+            } else if (!DUPLEX) {
+                prep_read(a.in, a.P, a.ws, gr);
+            }
         }
     }
 }
@@ -1691,7 +1742,7 @@ __device__ __forceinline__ void process_fast(const Args &a, const RecMeta &m, Fa
     const int64_t rec = m.rec;
     const int64_t off = m.off;
     const int R = (int)(m.w & 127u);
-    const int T = (int)((m.w >> 7) & 255u);
+    int T = (int)((m.w >> 7) & 255u);  // single-strand: before the 3' trim, redone below
     const int nq = ((int)(m.w >> 15) + 3) >> 2;
     const int minpos = m.minpos;
     const int stage_addr = fk::kStage + (wave << 12);
@@ -1712,17 +1763,53 @@ __device__ __forceinline__ void process_fast(const Args &a, const RecMeta &m, Fa
             *(uint4 *)(lds + stage_addr + 32 * d + 16) = make_uint4(c2.x, c2.y, c3.x, c3.y);
         }
     }
-    const uint2 rm = st.rm;            // this record's read meta; st is reused by the prefetch
+    uint2 rm = st.rm;                  // this record's read meta; st is reused by the prefetch
     const int msum = wave_sum(lane < R ? ((int)rm.x >> 16) & 255 : 0);
     stamp(2);                          // [1] element codes into LDS
     if (has_next) fast_load<DUPLEX>(a, mn, lane, st);
     stamp(3);                          // [2] prefetch issue
     auto to_general = [&]() {
+        // the general kernel reads the preprocessed reads (info, normalised runs)
+        if (!DUPLEX && lane < R) {
+            const int tl = ((int)rm.x >> 8) & 255;
+            if (tl > 0) a.ws.norm_cig[a.in.cig_off[m.g0 + lane]] = (uint32_t)tl << 4;   // one M run
+        }
         if (lane == 0) {
             const int idx = atomicAdd(&a.ws.ovf_count[DUPLEX ? 1 : 0], 1);
             a.ws.ovf[idx] = (int)rec;
         }
     };
+    if (!DUPLEX) {
+        // trim_3prime_N (:292-325): drop each read's trailing 'N' (sequenced, or
+        // masked below min_base_quality, :280): codes in bank N, read from the end
+        lds_fence();
+        const int x = (int)rm.x, y = (int)rm.y;
+        const int col = x & 255;
+        int tl = lane < R ? (x >> 8) & 255 : 0;
+        bool go = tl > 0;
+        while (__ballot(go)) {
+            if (go) {
+                const uint32_t code = *(const uint16_t *)(lds + stage_addr + 2 * (y + tl - 1));
+                if (code < 0x800u) --tl; else go = false;
+                go = go && tl > 0;
+            }
+        }
+        if (lane < R) {
+            dcr_read_info inf;
+            inf.seq_start = m.base_al + y;
+            inf.len = tl;
+            inf.n_cig = tl > 0 ? 1 : 0;
+            inf.status = tl > 0 ? DCR_ST_OK : DCR_ST_INDEX_ERROR;   // compress_cigarlist([]) :740 via :322
+            inf.has_ins = 0;
+            a.ws.info[m.g0 + lane] = inf;
+        }
+        rm.x = (rm.x & ~0xFF00u) | ((uint32_t)tl << 8);
+        T = wave_max(lane < R ? col + tl : 0);                       // :458-459 on the trimmed reads
+        if (__ballot(lane < R && tl == 0)) {
+            if (lane == 0) write_status_at(O, rec, DCR_ST_UPSTREAM);
+            return;
+        }
+    }
     if (__ballot(bad != 0)) { to_general(); return; }
     if (DCR_ABL == 1) {                 // diagnostic: staging only
         lds_fence();
