@@ -247,15 +247,37 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         return (unsigned)std::max<int64_t>(
             1, std::min<int64_t>((n_rec + 31) / 32, (int64_t)c->fast_blocks[duplex ? 1 : 0] * c->n_cu));
     };
+    auto fast_args = [&](bool duplex) {
+        dcr::FastArgs f{};
+        f.gb = duplex ? ss->seq : in->bases;
+        f.gq = duplex ? ss->qual : in->quals;
+        f.meta = c->w.meta;
+        f.rmeta = c->w.rmeta;
+        f.fast_count = c->w.fast_count + (duplex ? 1 : 0);
+        f.info = c->w.info;
+        f.norm_cig = c->w.norm_cig;
+        f.cig_off = in->cig_off;
+        f.ovf = c->w.ovf;
+        f.ovf_count = c->w.ovf_count + (duplex ? 1 : 0);
+        f.O = duplex ? *ds : *ss;
+        f.P = c->d_params;
+        f.stamps = c->w.stamps;
+        f.kq = a.fast_kq;
+        f.maxq = a.fast_maxq;
+        f.ca = a.fast_ca;
+        f.cb = a.fast_cb;
+        return f;
+    };
     auto strand = [&](bool duplex) -> int {
         a.n_rec = (duplex ? 2LL : 4LL) * in->n_fam;
+        const dcr::FastArgs fa = fast_args(duplex);
         const unsigned nb = (unsigned)((a.n_rec + 255) / 256);    // k_recmeta: 64 records per wave
         hipEvent_t *ev = c->ev + (duplex ? 5 : 2);
         if (duplex) {
             hipLaunchKernelGGL(dcr::k_recmeta<true>, dim3(nb), dim3(256), 0, c->stream, a);
             HIP_TRY(hipEventRecord(ev[0], c->stream));
             hipLaunchKernelGGL(dcr::k_consensus_fast<true>, dim3(fast_grid(a.n_rec, true)), dim3(256), 0,
-                               c->stream, a);
+                               c->stream, fa);
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL(dcr::k_consensus_general<true>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
                                c->stream, a);
@@ -263,7 +285,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
             hipLaunchKernelGGL(dcr::k_recmeta<false>, dim3(nb), dim3(256), 0, c->stream, a);
             HIP_TRY(hipEventRecord(ev[0], c->stream));
             hipLaunchKernelGGL(dcr::k_consensus_fast<false>, dim3(fast_grid(a.n_rec, false)), dim3(256), 0,
-                               c->stream, a);
+                               c->stream, fa);
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL(dcr::k_consensus_general<false>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
                                c->stream, a);

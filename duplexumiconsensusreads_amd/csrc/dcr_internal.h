@@ -55,9 +55,28 @@ struct Args {
     double fast_cb;         // min(qthresh[maxQ], 1 - threshold, 1/4) (1 - 1e-9) - 1e-15
 };
 
+// the fast kernel's compact arguments (one strand; fewer scalar registers than Args)
+struct FastArgs {
+    const uint8_t *gb, *gq;         // staged bytes: input reads (single-strand) or single-strand consensus (duplex)
+    const RecMeta *meta;            // fast list descriptors
+    const uint2 *rmeta;             // per-read words
+    const int *fast_count;          // fast-list length
+    dcr_read_info *info;            // single-strand: read info of the fast records' reads
+    uint32_t *norm_cig;             // single-strand: runs of records handed to the general kernel
+    const int32_t *cig_off;         // single-strand: batch cig_off
+    int *ovf;                       // general list of this strand
+    int *ovf_count;
+    dcr_out O;                      // this strand's outputs
+    const dcr_params *P;
+    unsigned long long *stamps;     // diagnostic builds
+    uint32_t kq;                    // bytes 255 - min_base_quality
+    int maxq;
+    double ca, cb;                  // fast finalize bound
+};
+
 __global__ void k_prep(dcr_batch in, const dcr_params *P, Workspace ws);
 template <bool DUPLEX> __global__ void k_recmeta(Args a);
-template <bool DUPLEX> __global__ void k_consensus_fast(Args a);
+template <bool DUPLEX> __global__ void k_consensus_fast(FastArgs a);
 template <bool DUPLEX> __global__ void k_consensus_general(Args a);
 
 }  // namespace dcr

@@ -1288,6 +1288,14 @@ __device__ __forceinline__ void write_status_at(const dcr_out &O, int64_t rec, i
 
 // wave-local LDS ordering: a wave's DS instructions execute in order, so only
 // the compiler must be kept from reordering (no vmcnt drain of prefetches)
+// A value the compiler cannot see through: per-lane addresses built from it
+// are formed where used instead of being hoisted out of the record loop (and
+// held in registers across it).
+__device__ __forceinline__ int opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
 __device__ __forceinline__ void lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1499,9 +1507,9 @@ struct FastStage {
 
 // issue a record's loads (consumed by the next process_fast call)
 template <bool DUPLEX>
-__device__ __forceinline__ void fast_load(const Args &a, const RecMeta &m, int lane, FastStage &st) {
-    const uint8_t *gb = DUPLEX ? a.ss.seq : a.in.bases;
-    const uint8_t *gq = DUPLEX ? a.ss.qual : a.in.quals;
+__device__ __forceinline__ void fast_load(const FastArgs &a, const RecMeta &m, int lane, FastStage &st) {
+    const uint8_t *gb = a.gb;
+    const uint8_t *gq = a.gq;
     const int nq = ((int)(m.w >> 15) + 3) >> 2;
     const uint4 *b16 = (const uint4 *)(gb + m.base_al);
     const uint4 *q16 = (const uint4 *)(gq + m.base_al);
@@ -1514,7 +1522,7 @@ __device__ __forceinline__ void fast_load(const Args &a, const RecMeta &m, int l
         st.vq[u] = q16[d];
     }
     const int R = (int)(m.w & 127u);
-    st.rm = a.ws.rmeta[m.g0 + min(lane, R - 1)];
+    st.rm = a.rmeta[m.g0 + min(lane, R - 1)];
 }
 
 // Four element codes from four bases and qualities (SWAR).  The class comes
@@ -1698,13 +1706,14 @@ __device__ __forceinline__ void two_chains(const uint8_t *lds, const uint2 rm, i
 // address = optr + rec * rec_mul + off * off_mul)
 struct FastPtr {
     uint8_t *optr;
-    int64_t rec_mul, off_mul;
+    uint32_t mul;      // rec_mul | off_mul << 8 (bytes per record / per region column)
 };
 
 __device__ __forceinline__ FastPtr fast_ptr(const dcr_out &O, int lane) {
     FastPtr f;
-    f.rec_mul = lane < 7 ? 4 : (lane < 9 ? 8 : 0);
-    f.off_mul = lane == 9 ? 4 : 0;
+    const uint32_t rec_mul = lane < 7 ? 4u : (lane < 9 ? 8u : 0u);
+    const uint32_t off_mul = lane == 9 ? 4u : 0u;
+    f.mul = rec_mul | (off_mul << 8);
     uint8_t *p;
     switch (lane) {
     case 0: p = (uint8_t *)O.pos; break;
@@ -1723,9 +1732,9 @@ __device__ __forceinline__ FastPtr fast_ptr(const dcr_out &O, int lane) {
 }
 
 template <bool DUPLEX, int NT>
-__device__ __forceinline__ void process_fast(const Args &a, const RecMeta &m, FastStage &st, const bool has_next,
+__device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m, FastStage &st, const bool has_next,
                                              const RecMeta &mn, uint8_t *lds, const int wave, const int lane,
-                                             int &etab_r, uint64_t *stp, const FastPtr &fp) {
+                                             int &etab_r, uint64_t *stp) {
     uint64_t t_prev = 0;
     auto stamp = [&](int k) {
         if (DCR_STAMP) {
@@ -1737,8 +1746,7 @@ __device__ __forceinline__ void process_fast(const Args &a, const RecMeta &m, Fa
     stamp(0);
     if (DCR_STAMP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stamp(1);                          // [0] wait for this record's prefetched bytes
-    const dcr_params *P = a.P;
-    const dcr_out &O = DUPLEX ? a.ds : a.ss;
+    const dcr_out &O = a.O;
     const int64_t rec = m.rec;
     const int64_t off = m.off;
     const int R = (int)(m.w & 127u);
@@ -1755,10 +1763,10 @@ __device__ __forceinline__ void process_fast(const Args &a, const RecMeta &m, Fa
     for (int u = 0; u < kStageQ; ++u) {
         const int d = u * kWave + lane;
         if (d < nq) {
-            const uint2 c0 = make_codes4<DUPLEX>(st.vb[u].x, st.vq[u].x, a.fast_kq, bad);
-            const uint2 c1 = make_codes4<DUPLEX>(st.vb[u].y, st.vq[u].y, a.fast_kq, bad);
-            const uint2 c2 = make_codes4<DUPLEX>(st.vb[u].z, st.vq[u].z, a.fast_kq, bad);
-            const uint2 c3 = make_codes4<DUPLEX>(st.vb[u].w, st.vq[u].w, a.fast_kq, bad);
+            const uint2 c0 = make_codes4<DUPLEX>(st.vb[u].x, st.vq[u].x, a.kq, bad);
+            const uint2 c1 = make_codes4<DUPLEX>(st.vb[u].y, st.vq[u].y, a.kq, bad);
+            const uint2 c2 = make_codes4<DUPLEX>(st.vb[u].z, st.vq[u].z, a.kq, bad);
+            const uint2 c3 = make_codes4<DUPLEX>(st.vb[u].w, st.vq[u].w, a.kq, bad);
             *(uint4 *)(lds + stage_addr + 32 * d) = make_uint4(c0.x, c0.y, c1.x, c1.y);
             *(uint4 *)(lds + stage_addr + 32 * d + 16) = make_uint4(c2.x, c2.y, c3.x, c3.y);
         }
@@ -1772,11 +1780,11 @@ __device__ __forceinline__ void process_fast(const Args &a, const RecMeta &m, Fa
         // the general kernel reads the preprocessed reads (info, normalised runs)
         if (!DUPLEX && lane < R) {
             const int tl = ((int)rm.x >> 8) & 255;
-            if (tl > 0) a.ws.norm_cig[a.in.cig_off[m.g0 + lane]] = (uint32_t)tl << 4;   // one M run
+            if (tl > 0) a.norm_cig[a.cig_off[m.g0 + lane]] = (uint32_t)tl << 4;   // one M run
         }
         if (lane == 0) {
-            const int idx = atomicAdd(&a.ws.ovf_count[DUPLEX ? 1 : 0], 1);
-            a.ws.ovf[idx] = (int)rec;
+            const int idx = atomicAdd(a.ovf_count, 1);
+            a.ovf[idx] = (int)rec;
         }
     };
     if (!DUPLEX) {
@@ -1801,7 +1809,7 @@ __device__ __forceinline__ void process_fast(const Args &a, const RecMeta &m, Fa
             inf.n_cig = tl > 0 ? 1 : 0;
             inf.status = tl > 0 ? DCR_ST_OK : DCR_ST_INDEX_ERROR;   // compress_cigarlist([]) :740 via :322
             inf.has_ins = 0;
-            a.ws.info[m.g0 + lane] = inf;
+            a.info[m.g0 + lane] = inf;
         }
         rm.x = (rm.x & ~0xFF00u) | ((uint32_t)tl << 8);
         T = wave_max(lane < R ? col + tl : 0);                       // :458-459 on the trimmed reads
@@ -1864,7 +1872,7 @@ __device__ __forceinline__ void process_fast(const Args &a, const RecMeta &m, Fa
         const uint32_t bank = (c.seen[tt] >> 11) & 15u;
         kk[tt] = bank ? __builtin_ctz(bank) : 0;
         nn_[tt] = (int)(c.cnt[tt] >> kk[tt]);
-        fast[tt] = (bank & (bank - 1u)) == 0 && nn_[tt] > 0 && (5.0 * c.U[tt]) * a.fast_ca < c.s[tt] * a.fast_cb;
+        fast[tt] = (bank & (bank - 1u)) == 0 && nn_[tt] > 0 && (5.0 * c.U[tt]) * a.ca < c.s[tt] * a.cb;
         ev[tt] = etab[min(nn_[tt], R)];
         banks |= bank << (4 * tt);
     }
@@ -1905,7 +1913,7 @@ __device__ __forceinline__ void process_fast(const Args &a, const RecMeta &m, Fa
         const bool hi1 = two && s1 > s0;
         const double bb = hi1 ? s1 : s0;
         const double other = two ? (hi1 ? s0 : s1) + 4.0 * U : 5.0 * U;
-        const bool fst = k0 >= 0 && other * a.fast_ca < bb * a.fast_cb;
+        const bool fst = k0 >= 0 && other * a.ca < bb * a.cb;
         if (__ballot(live && !fst)) { to_general(); return; }
         const int kb = hi1 ? k1 : k0;
         const int d = n0 + (two ? n1 : 0), e = R - (hi1 ? n1 : n0);
@@ -1926,18 +1934,19 @@ __device__ __forceinline__ void process_fast(const Args &a, const RecMeta &m, Fa
     // region never reads a byte that is not a valid letter
     {
         const int T16 = (T + 15) & ~15;
+        const int ln = opaque(lane);
         uint16_t *od = O.d + off;
         uint16_t *oe = O.e + off;
         uint8_t *oseq = O.seq + off;
         uint8_t *oqual = O.qual + off;
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt) {
-            const int t = 64 * tt + lane;
+            const int t = 64 * tt + ln;
             if (t < T) {
                 od[t] = (uint16_t)(ov[tt] & 255u);
                 oe[t] = (uint16_t)((ov[tt] >> 8) & 255u);
                 oseq[t] = (uint8_t)(ov[tt] >> 16);
-                oqual[t] = (uint8_t)a.fast_maxq;
+                oqual[t] = (uint8_t)a.maxq;
             } else if (t < T16) {
                 oseq[t] = (uint8_t)'N';
                 oqual[t] = (uint8_t)0;
@@ -1965,7 +1974,7 @@ __device__ __forceinline__ void process_fast(const Args &a, const RecMeta &m, Fa
         E = __builtin_rint(y) / 1000.0;
     } else {
         lds_fence();
-        const double total = 0.0 + pairwise_et(et, T, lane);
+        const double total = 0.0 + pairwise_et(et, T, opaque(lane));
         E = __builtin_rint((total / (double)T) * 1000.0) / 1000.0;
     }
     stamp(9);                          // [8] mean
@@ -1984,7 +1993,8 @@ __device__ __forceinline__ void process_fast(const Args &a, const RecMeta &m, Fa
                       : lane == 7 ? E_lo
                       : lane == 8 ? E_hi
                                   : (int)((uint32_t)T << 4);   // one M run of T
-        if (lane < 10) *(int *)(fp.optr + rec * fp.rec_mul + off * fp.off_mul) = v;
+        const FastPtr fp = fast_ptr(O, opaque(lane));
+        if (lane < 10) *(int *)(fp.optr + rec * (int64_t)(fp.mul & 255u) + off * (int64_t)(fp.mul >> 8)) = v;
         if (lane == 0) O.status[rec] = DCR_ST_OK;
     }
     stamp(10);                         // [9] record scalars
@@ -2006,7 +2016,10 @@ __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
 // processed, and the descriptor of record i + 2 is fetched by a vector load
 // (vmcnt, not lgkmcnt, so LDS waits never drain it).
 template <bool DUPLEX>
-__global__ __launch_bounds__(kBlock, 3) void k_consensus_fast(Args a) {
+#ifndef DCR_FAST_WAVES
+#define DCR_FAST_WAVES 4
+#endif
+__global__ __launch_bounds__(kBlock, DCR_FAST_WAVES) void k_consensus_fast(FastArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[fk::kLdsBytes];
     const dcr_params *P = a.P;
     for (int i = threadIdx.x; i < 6 * (fk::kRowMax + 1); i += kBlock) {
@@ -2019,35 +2032,34 @@ __global__ __launch_bounds__(kBlock, 3) void k_consensus_fast(Args a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     __syncthreads();
-    const int64_t n = a.ws.fast_count[DUPLEX ? 1 : 0];
+    const int64_t n = *a.fast_count;
     const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
     const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
     int i = (int)(n * gw / nw);
     const int iend = (int)(n * (gw + 1) / nw);
     if (i >= iend) return;
-    const RecMeta *ML = a.ws.meta;
+    const RecMeta *ML = a.meta;
     RecMeta m0 = ML[i];
     RecMeta m1 = ML[min(i + 1, iend - 1)];
     FastStage st;
     fast_load<DUPLEX>(a, m0, lane, st);
     int etab_r = -1;
     uint64_t stp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    const FastPtr fp = fast_ptr(DUPLEX ? a.ds : a.ss, lane);
     for (;;) {
         const bool has_next = i + 1 < iend;
         const int i2 = min(i + 2, iend - 1);
         const uint32_t mv = lane < 8 ? ((const uint32_t *)(ML + i2))[lane] : 0u;
         const int T = (int)((m0.w >> 7) & 255u);
-        if (T <= 64) process_fast<DUPLEX, 1>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp, fp);
-        else if (T <= 128) process_fast<DUPLEX, 2>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp, fp);
-        else if (T <= 192) process_fast<DUPLEX, 3>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp, fp);
-        else process_fast<DUPLEX, 4>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp, fp);
+        if (T <= 64) process_fast<DUPLEX, 1>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp);
+        else if (T <= 128) process_fast<DUPLEX, 2>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp);
+        else if (T <= 192) process_fast<DUPLEX, 3>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp);
+        else process_fast<DUPLEX, 4>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp);
         if (++i >= iend) break;
         m0 = m1;
         m1 = meta_from_lanes(mv);
     }
     if (DCR_STAMP && lane == 0)
-        for (int k = 0; k < 10; ++k) atomicAdd(&a.ws.stamps[k + (DUPLEX ? 16 : 0)], (unsigned long long)stp[k]);
+        for (int k = 0; k < 10; ++k) atomicAdd(&a.stamps[k + (DUPLEX ? 16 : 0)], (unsigned long long)stp[k]);
 }
 
 
@@ -2072,8 +2084,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_consensus_general(Args a) {
 
 template __global__ void k_recmeta<false>(Args);
 template __global__ void k_recmeta<true>(Args);
-template __global__ void k_consensus_fast<false>(Args);
-template __global__ void k_consensus_fast<true>(Args);
+template __global__ void k_consensus_fast<false>(FastArgs);
+template __global__ void k_consensus_fast<true>(FastArgs);
 template __global__ void k_consensus_general<false>(Args);
 template __global__ void k_consensus_general<true>(Args);
 
