@@ -121,10 +121,10 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
     (void)hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device);
     // the persistent fast kernel's grid = what is resident at once (a block
     // beyond that would start only when a resident one has finished its range)
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->fast_blocks[0], dcr::k_consensus_fast<false>, dcr::kBlock, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->fast_blocks[0], dcr::k_consensus_fast<false>, dcr::kFastBlock, 0) !=
             hipSuccess || c->fast_blocks[0] < 1)
         c->fast_blocks[0] = 1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->fast_blocks[1], dcr::k_consensus_fast<true>, dcr::kBlock, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->fast_blocks[1], dcr::k_consensus_fast<true>, dcr::kFastBlock, 0) !=
             hipSuccess || c->fast_blocks[1] < 1)
         c->fast_blocks[1] = 1;
     c->fast_ok = fast_allowed(params);
@@ -234,7 +234,12 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         const int mq = std::min(std::max(hp.max_base_quality, 0), DCR_MAX_QTHRESH - 1);
         const double cc = std::min(std::min(hp.qthresh[mq], 1.0 - hp.post_threshold), 0.25);
         a.fast_ca = 1.0 + 1e-9;
-        a.fast_cb = cc * (1.0 - 1e-9) - 1e-15;
+        a.fast_cb = cc * (1.0 - 1e-9) - 4e-15;
+        // lowest quality from which every row has 1 - p' >= p'/5 (fast kernel v4:
+        // every chain >= U); a kept base below it sends its record to the general kernel
+        int qlo = 123;
+        while (qlo > 0 && hp.match[qlo - 1] >= hp.mismatch[qlo - 1]) --qlo;
+        a.fast_kqlo = (uint32_t)(0x80 - qlo) * 0x01010101u;
     }
     // per strand: k_recmeta classifies every record (fast list / general list /
     // status written), then the fast kernel (8 records per wave) drains the fast list and
@@ -242,10 +247,11 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     auto grid_for = [&](int64_t n_rec, unsigned cap) {
         return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_rec + 3) / 4, cap));
     };
-    // persistent fast kernel: the resident blocks, at least ~8 records per wave
+    // persistent fast kernel: the resident blocks (16 waves each), at least
+    // ~8 records per wave
     auto fast_grid = [&](int64_t n_rec, bool duplex) {
         return (unsigned)std::max<int64_t>(
-            1, std::min<int64_t>((n_rec + 31) / 32, (int64_t)c->fast_blocks[duplex ? 1 : 0] * c->n_cu));
+            1, std::min<int64_t>((n_rec + 127) / 128, (int64_t)c->fast_blocks[duplex ? 1 : 0] * c->n_cu));
     };
     auto fast_args = [&](bool duplex) {
         dcr::FastArgs f{};
@@ -263,6 +269,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         f.P = c->d_params;
         f.stamps = c->w.stamps;
         f.kq = a.fast_kq;
+        f.kqlo = a.fast_kqlo;
         f.maxq = a.fast_maxq;
         f.ca = a.fast_ca;
         f.cb = a.fast_cb;
@@ -276,7 +283,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         if (duplex) {
             hipLaunchKernelGGL(dcr::k_recmeta<true>, dim3(nb), dim3(256), 0, c->stream, a);
             HIP_TRY(hipEventRecord(ev[0], c->stream));
-            hipLaunchKernelGGL(dcr::k_consensus_fast<true>, dim3(fast_grid(a.n_rec, true)), dim3(256), 0,
+            hipLaunchKernelGGL(dcr::k_consensus_fast<true>, dim3(fast_grid(a.n_rec, true)), dim3(dcr::kFastBlock), 0,
                                c->stream, fa);
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL(dcr::k_consensus_general<true>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
@@ -284,7 +291,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         } else {
             hipLaunchKernelGGL(dcr::k_recmeta<false>, dim3(nb), dim3(256), 0, c->stream, a);
             HIP_TRY(hipEventRecord(ev[0], c->stream));
-            hipLaunchKernelGGL(dcr::k_consensus_fast<false>, dim3(fast_grid(a.n_rec, false)), dim3(256), 0,
+            hipLaunchKernelGGL(dcr::k_consensus_fast<false>, dim3(fast_grid(a.n_rec, false)), dim3(dcr::kFastBlock), 0,
                                c->stream, fa);
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL(dcr::k_consensus_general<false>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,

@@ -11,6 +11,8 @@ namespace dcr {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
+constexpr int kFastWaves = 16;              // k_consensus_fast: one 16-wave block per CU
+constexpr int kFastBlock = kWave * kFastWaves;
 
 // Per-record launch metadata written by k_recmeta for the fast kernel, in
 // fast-list order (one scalar 32-byte load per record).
@@ -52,7 +54,8 @@ struct Args {
     uint32_t fast_kq;       // bytes 255 - min_base_quality: v_lerp_u8 masking test
     int fast_maxq;          // max_base_quality
     double fast_ca;         // 1 + 1e-9
-    double fast_cb;         // min(qthresh[maxQ], 1 - threshold, 1/4) (1 - 1e-9) - 1e-15
+    double fast_cb;         // min(qthresh[maxQ], 1 - threshold, 1/4) (1 - 1e-9) - 4e-15
+    uint32_t fast_kqlo;     // bytes 0x80 - fast_qlo
 };
 
 // the fast kernel's compact arguments (one strand; fewer scalar registers than Args)
@@ -70,6 +73,7 @@ struct FastArgs {
     const dcr_params *P;
     unsigned long long *stamps;     // diagnostic builds
     uint32_t kq;                    // bytes 255 - min_base_quality
+    uint32_t kqlo;                  // bytes 0x80 - fast_qlo (lowest quality with 1-p' >= p'/5 upward)
     int maxq;
     double ca, cb;                  // fast finalize bound
 };

@@ -33,8 +33,12 @@
 #ifndef DCR_STAMP
 #define DCR_STAMP 0   // diagnostic builds only (tools/stamps.py): per-phase s_memtime cycle totals
 #endif
+#ifndef DCR_PIPE2
+#define DCR_PIPE2 2   // tiles up to which the products keep two reads in flight
+#endif
 #ifndef DCR_ABL
-#define DCR_ABL 0   // diagnostic builds only (tools/ablate.py): 1 setup, 2 +accumulate, 3 +finalize
+#define DCR_ABL 0   // diagnostic builds only (tools/ablate.py); fast kernel: 1 staging only, 2 +products,
+                    // 4 always the exact pairwise mean, 5 no per-column stores
 #endif
 
 namespace dcr {
@@ -42,6 +46,7 @@ namespace dcr {
 constexpr int kStageElems = 2048;        // per-wave LDS staging (16-bit codes)
 constexpr int kTileIns = 32;             // column tile of the insertion layout
 constexpr int kFastMaxT = 240;           // pairwise_small: both halves <= 128
+constexpr int kFastMaxR = 63;            // fast kernel: 6-bit class counters
 constexpr int kColsLds = 256;            // per-wave LDS column scratch
 
 // element code: bits 0..8 LUT row (quality 0..255, 256 '+', 257 '-'), bits 9..11 class
@@ -1397,7 +1402,8 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
             const int64_t base_al = (int64_t)g.lo & ~(int64_t)15;     // 16-byte staging loads
             const int64_t span = (int64_t)g.hi - base_al;
             const bool aligned = ((((uintptr_t)gb) | ((uintptr_t)gq)) & 15) == 0;
-            if ((g.flags & 4) || !aligned || span > kStageElems || T > kFastMaxT || T > cap || !a.fast_ok) {
+            if ((g.flags & 4) || !aligned || R > kFastMaxR || span > kStageElems || T > kFastMaxT || T > cap ||
+                !a.fast_ok) {
                 kind = 1;
             } else {
                 kind = 0;
@@ -1450,52 +1456,62 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
     }
 }
 
-// ------------------------------------------------------- fast kernel (v3)
+// ------------------------------------------------------- fast kernel (v4)
 // Records of the dominant shape: every read a single M run (no insertion
-// column, no '-' row), <= 64 reads, bytes fit one LDS stage, T <= 240, every
-// staged quality <= 122 and every staged base a valid letter (else the record
-// is handed to the general kernel).  Then every aligned row is a base, a masked
-// 'N' or a pad 'N', and the consensus CIGAR is one M run over the trimmed span
-// (:797-848 yields M for every such column).
+// column, no '-' row), <= 63 reads, bytes fit one LDS stage, T <= 240, every
+// staged quality <= 122, every staged base a valid letter and every kept base's
+// quality >= fast_qlo (else the record is handed to the general kernel).  Then
+// every aligned row is a base, a masked 'N' or a pad 'N', and the consensus
+// CIGAR is one M run over the trimmed span (:797-848 yields M for every such
+// column).
 //
-// Element codes ARE byte addresses of the likelihood table in LDS.  The table
-// is banked by class: bank N holds (p'/5, p'/5) and banks A/T/C/G hold
-// (1-p', p'/5) for every quality row, at LDS offsets whose bits 11-14 are the
-// class one-hot (N = 0).  For a column with one base class k the reference's
-// six products (:594-600) are then exactly two chains, in read order:
-//     s *= f.x   (the chain of class k: 1-p' on k rows, p'/5 on N rows)
-//     U *= f.y   (every other class: p'/5 on every row)
-// with no class compare or select per element; OR-ing the codes gives the
-// classes present and summing code >> 11 gives n * onehot(k).  A tile where
-// some column holds two base classes is recomputed with explicit class matches.
+// Products.  The reference keeps six products per column (:594-600) in the
+// order A T C G + -.  Without '+'/'-' rows the last two are one chain U (p'/5
+// from every read).  A lane keeps the four class chains of its column; the
+// four factors of an element are one 32-byte row of an LDS table indexed by the
+// element's code, so the products need no class compare or select:
+//     LA *= f.a   LT *= f.t   LC *= f.c   LG *= f.g
+// (f.k = 1-p' on a class-k row, p'/5 otherwise; an 'N' row is p'/5 for all).
+// Element codes ARE LDS byte addresses: code = (6k << 11) | 16 (q + k) for class
+// k (N 0, A 1, T 2, C 3, G 4); the half-row (f.a, f.t) is at code, (f.c, f.g)
+// at code + 0x800, and the 16 k shift spreads the classes over LDS banks.
+// code >> 11 = 6k is also the shift of the class's 6-bit counter in a packed
+// count word (R <= 63): cnt += 1 << (code >> 11).
 //
-// Finalize: with one class present, S = s + 5U up to 5 roundings, so
-// e = 1 - s/S <= 5U/s + 6 ulp.  If 5U(1+d) < s * min(qthresh[maxQ], 1-thr, 1/4)(1-d)
-// the reference's quality is maxQ and the base is not masked (:699-709, :617),
-// with no division or phred search; other columns take finalize().
+// Finalize without division or phred search.  Every factor 1-p' >= p'/5 for
+// the qualities kept here (>= fast_qlo) and rounding is monotone, so each chain
+// is >= U and m = min(chains) >= U (= U when a class is absent).  With b the
+// largest chain, other = (sum of the four - b) + 2m bounds S - b from above
+// (the subtraction is exact when b dominates: Sterbenz), and the reference's
+// e = 1 - b/S <= (S - b)/b + 7 ulp.  If other (1 + 1e-9) < b cb with
+// cb = min(qthresh[maxQ], 1 - threshold, 1/4)(1 - 1e-9) - 4e-15 the reference's
+// quality is maxQ, its call is b and it is not masked (:699-709, :617).  A
+// record with any column outside the bound goes to the general kernel, which
+// runs the reference's full finalize.
 //
-// LDS (one 40 KiB block of 4 waves, 4 blocks per CU):
-//   0x0000 bank N | 0x0800 bank A | 0x1000 bank T | 0x1800 bank X (never read:
-//   a record with an invalid byte leaves first) | 0x2000 bank C | 0x4000 bank G
-//   holes 0x1800-0x1fff and 0x2800-0x3fff: per-wave e/d columns; 0x4800+:
-//   stages (4 KiB per wave), e/d tables, pad sentinel.
+// LDS of one 16-wave block (one per CU):
+//   class banks k = 0..4 at 0x3000 k (4 KiB each: two half-row tables)
+//   stages (4 KiB per wave): waves 0-7 in the holes between the banks,
+//   waves 8-15 from 0xD000; e/d table [d][e] (64 x 64 doubles) at 0x15000;
+//   pad sentinel at 0x1D000.
 namespace fk {
-constexpr int kRowMax = 122;                               // quality rows 0..122 (+ bank index <= 127)
+constexpr int kWaves = kFastWaves;                         // waves per block
+constexpr int kBlockThreads = kFastBlock;
+constexpr int kRowMax = 122;                               // quality rows 0..122
 constexpr uint32_t kPadCode = 16u * 2u;                    // bank N, quality 2 (:509-510, :543-544)
-constexpr int kStage = 0x4800;                             // 4 x 4 KiB
-constexpr int kEtab = kStage + kWavesPerBlock * 0x1000;    // 4 x 66 doubles
-constexpr int kEtabN = 66;
-constexpr int kSent = kEtab + kWavesPerBlock * kEtabN * 8;  // u16 pad code (out-of-read sentinel)
-constexpr int kLdsBytes = kSent + 16;
+constexpr int kHalf = 0x800;                               // (f.c, f.g) half-rows
+constexpr int kEtab = 0x15000;                             // e/d [d][e], d, e < 64
+constexpr int kSent = kEtab + 64 * 64 * 8;                 // u16 pad code (out-of-read sentinel)
+constexpr int kPtrs = kSent + 16;                          // u64 [10] record-scalar destinations, [4] rare-path pointers
+constexpr int kLdsBytes = kPtrs + 14 * 8;
 static_assert(kStageElems * 2 == 0x1000, "one 4 KiB stage per wave");
-static_assert(kLdsBytes <= 40 * 1024, "4 blocks per CU");
+static_assert(16 * (kRowMax + 4) + kHalf <= 0x1000, "a class bank fits 4 KiB");
+static_assert(kLdsBytes <= 160 * 1024, "one block per CU");
 
-__device__ __forceinline__ int bank_base(int b) { return b == 5 ? 0x4000 : b << 11; }   // N A T X C G
-// per-wave e/d columns in the bank holes (1920 B each)
-__device__ __forceinline__ int et_off(int wave) {
-    return wave == 0 ? 0x1800 : 0x2800 + (wave - 1) * (kFastMaxT * 8);
+__device__ __forceinline__ int bank_base(int k) { return 0x3000 * k; }
+__device__ __forceinline__ int stage_base(int wave) {
+    return wave < 8 ? 0x1000 + 0x3000 * (wave >> 1) + 0x1000 * (wave & 1) : 0xD000 + ((wave - 8) << 12);
 }
-static_assert(0x2800 + 3 * kFastMaxT * 8 <= 0x4000, "e/d columns fit the hole");
 }  // namespace fk
 
 constexpr int kStageQ = kStageElems / 16 / kWave;   // staged 16-byte quads per lane
@@ -1529,123 +1545,100 @@ __device__ __forceinline__ void fast_load(const FastArgs &a, const RecMeta &m, i
 // from a byte permute indexed by (b >> 1) & 7, distinct for A C T G N; a second
 // permute gives the letter of that index, and a byte that differs from it is
 // not a valid nucleotide (:580-585): flagged in `bad` (the record then goes to
-// the general kernel, which reproduces the exit), as is a quality > 122.
-// Single-strand inputs mask qual < min_base_quality to bank N keeping the
-// quality (:280): v_lerp_u8 computes (q + 256 - m) >> 1, whose bit 7 is q >= m.
-// code = bank_base + 16 * (bank index + q): bank index N0 A1 T2 X3 C4 G5.
+// the general kernel, which reproduces the exit), as are a quality > 122 and a
+// kept base below fast_qlo.  Single-strand inputs mask qual < min_base_quality
+// to class N keeping the quality (:280): v_lerp_u8 computes (q + 256 - m) >> 1,
+// whose bit 7 is q >= m.  code = (6k << 11) | 16 (q + k) per byte.
 template <bool DUPLEX>
-__device__ __forceinline__ uint2 make_codes4(uint32_t B, uint32_t Q, uint32_t kq, uint32_t &bad) {
+__device__ __forceinline__ uint2 make_codes4(uint32_t B, uint32_t Q, uint32_t kq, uint32_t kqlo, uint32_t &bad) {
     const uint32_t h = (B >> 1) & 0x07070707u;
-    uint32_t idx = __builtin_amdgcn_perm(0x00030303u, 0x05020401u, h);           // A1 C4 T2 G5 . . . N0
+    uint32_t k = __builtin_amdgcn_perm(0u, 0x04020301u, h);                       // A1 C3 T2 G4 . . . N0
     uint32_t x = B ^ __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, h);         // 0 for a valid letter
+    uint32_t lo = ~(Q + kqlo) & __builtin_amdgcn_perm(0u, 0xFFFFFFFFu, h);       // bit 7: a base with q < fast_qlo
     if (!DUPLEX) {
         const uint32_t L = __builtin_amdgcn_lerp(Q, kq, 0x01010101u);
         const uint32_t keep = __builtin_amdgcn_perm(L << 8, L, 0x090B080Au);      // 0xff per kept byte
-        idx &= keep;
+        k &= keep;
         x &= keep;                                                                // masked bytes are 'N'
+        lo &= keep;
     }
-    bad |= x | (((Q + 0x05050505u) | Q) & 0x80808080u);
-    const uint32_t bank = __builtin_amdgcn_perm(0x00004020u, 0x18100800u, idx);  // one-hot << 3 per byte
-    const uint32_t w = idx + Q;                                                   // per byte, <= 127
-    const uint32_t hi = ((w >> 4) & 0x07070707u) | bank;
-    const uint32_t lo = (w << 4) & 0xF0F0F0F0u;
-    return make_uint2(__builtin_amdgcn_perm(hi, lo, 0x05010400u), __builtin_amdgcn_perm(hi, lo, 0x07030602u));
-}
-
-// general-slot form of a code (class << 9 | quality) for the exact loops
-__device__ __forceinline__ uint32_t code_to_elem(uint32_t code) {
-    const uint32_t nib = code >> 11;
-    const uint32_t bidx = (uint32_t)(0x500043210ull >> (4 * nib)) & 15u;
-    const uint32_t cls = (uint32_t)(0x300027106ull >> (4 * nib)) & 15u;
-    const uint32_t q = ((code & 0x7F0u) >> 4) - bidx;
-    return (cls << 9) | q;
-}
-
-// LDS address of read r's element code at the lane's column t, or the pad
-// sentinel outside the read
-struct ReadAddr {
-    int cr;        // byte address of the read's column 0 in the stage
-    int col, len;
-    bool full;     // the read covers every column: no bounds test
-};
-
-__device__ __forceinline__ ReadAddr read_addr(const uint2 rm, int r, int stage_addr, int T) {
-    const int x = readlane((int)rm.x, r);
-    const int y = readlane((int)rm.y, r);
-    ReadAddr ra;
-    ra.col = x & 255;
-    ra.len = (x >> 8) & 255;
-    ra.cr = stage_addr + 2 * (y - ra.col);
-    ra.full = ra.col == 0 && ra.len >= T;
-    return ra;
-}
-
-__device__ __forceinline__ uint32_t code_at(const uint8_t *lds, const ReadAddr &ra, int t) {
-    uint32_t a = 2u * (uint32_t)t + (uint32_t)ra.cr;
-    if (!ra.full) a = (uint32_t)(t - ra.col) < (uint32_t)ra.len ? a : (uint32_t)fk::kSent;
-    return *(const uint16_t *)(lds + a);
+    bad |= x | ((((Q + 0x05050505u) | Q) | lo) & 0x80808080u);
+    const uint32_t w = k + Q;                                                     // per byte, <= 126
+    const uint32_t hi = ((w >> 4) & 0x07070707u) | __builtin_amdgcn_perm(0x000000C0u, 0x90603000u, k);   // 48 k
+    const uint32_t lw = (w << 4) & 0xF0F0F0F0u;
+    return make_uint2(__builtin_amdgcn_perm(hi, lw, 0x05010400u), __builtin_amdgcn_perm(hi, lw, 0x07030602u));
 }
 
 template <int NT>
-struct Chains {
-    double U[NT], s[NT];
-    uint32_t seen[NT], cnt[NT];
+struct Chains4 {
+    double L[NT][4];       // A T C G
+    uint32_t cnt[NT];      // 6-bit counters: N A T C G
 };
 
-// Products in read order, two reads per step (NT <= 3): the table rows of
-// reads r and r + 1 are in flight together while the codes of r + 2 and r + 3
-// are read.
-template <int NT>
-__device__ __forceinline__ void run_chains(Chains<NT> &c, const uint8_t *lds, int R, const uint2 rm,
-                                           int stage_addr, int T, int lane) {
+// Products in read order.  FULL: every read covers every column (the C2
+// shape), so a read's codes are one base address plus immediate offsets;
+// otherwise a column outside the read loads the pad sentinel.  Two reads per
+// step (NT <= 3): the table rows of reads r and r + 1 are in flight together
+// while the codes of r + 2 and r + 3 are read.
+template <int NT, bool FULL>
+__device__ __forceinline__ void run_chains4(Chains4<NT> &c, const uint8_t *lds, int R, uint32_t rmx, int crv,
+                                            int lane) {
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-        c.U[tt] = 1.0;
-        c.s[tt] = 1.0;
-        c.seen[tt] = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c.L[tt][k] = 1.0;
         c.cnt[tt] = 0;
     }
     auto codes = [&](int r, uint32_t (&cd)[NT]) {
-        const ReadAddr ra = read_addr(rm, min(r, R - 1), stage_addr, T);
-        if (ra.full) {                 // the common read: no bounds test (uniform branch)
+        const int rr = min(r, R - 1);
+        const int cr = readlane(crv, rr);          // stage address of the read's column 0
+        if (FULL) {
+            const uint8_t *p = lds + cr + 2 * lane;
 #pragma unroll
-            for (int tt = 0; tt < NT; ++tt) cd[tt] = *(const uint16_t *)(lds + 2u * (uint32_t)(64 * tt + lane) + (uint32_t)ra.cr);
+            for (int tt = 0; tt < NT; ++tt) cd[tt] = *(const uint16_t *)(p + 128 * tt);
         } else {
+            const int x = readlane((int)rmx, rr);
+            const int col = x & 255, len = (x >> 8) & 255;
 #pragma unroll
             for (int tt = 0; tt < NT; ++tt) {
                 const int t = 64 * tt + lane;
-                const uint32_t a = (uint32_t)(t - ra.col) < (uint32_t)ra.len ? 2u * (uint32_t)t + (uint32_t)ra.cr
-                                                                             : (uint32_t)fk::kSent;
+                const uint32_t a = (uint32_t)(t - col) < (uint32_t)len ? (uint32_t)(cr + 2 * t) : (uint32_t)fk::kSent;
                 cd[tt] = *(const uint16_t *)(lds + a);
             }
         }
     };
-    auto mul = [&](const uint32_t (&cd)[NT], const double2 (&f)[NT]) {
+    auto rows = [&](const uint32_t (&cd)[NT], double2 (&f0)[NT], double2 (&f1)[NT]) {
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt) {
-            c.seen[tt] |= cd[tt];
-            c.cnt[tt] += cd[tt] >> 11;
-            c.s[tt] *= f[tt].x;
-            c.U[tt] *= f[tt].y;
+            f0[tt] = *(const double2 *)(lds + cd[tt]);
+            f1[tt] = *(const double2 *)(lds + cd[tt] + fk::kHalf);
+        }
+    };
+    auto mul = [&](const uint32_t (&cd)[NT], const double2 (&f0)[NT], const double2 (&f1)[NT]) {
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            c.cnt[tt] += 1u << (cd[tt] >> 11);
+            c.L[tt][0] *= f0[tt].x;
+            c.L[tt][1] *= f0[tt].y;
+            c.L[tt][2] *= f1[tt].x;
+            c.L[tt][3] *= f1[tt].y;
         }
     };
     uint32_t c0[NT], c1[NT];
     codes(0, c0);
     int r = 0;
-    if constexpr (NT <= 3) {
+    if constexpr (NT <= DCR_PIPE2) {
         codes(1, c1);
+#pragma unroll 1
         for (; r + 2 <= R; r += 2) {
-            double2 f0[NT], f1[NT];
-#pragma unroll
-            for (int tt = 0; tt < NT; ++tt) {
-                f0[tt] = *(const double2 *)(lds + c0[tt]);
-                f1[tt] = *(const double2 *)(lds + c1[tt]);
-            }
+            double2 f0[NT], g0[NT], f1[NT], g1[NT];
+            rows(c0, f0, g0);
+            rows(c1, f1, g1);
             uint32_t n0[NT], n1[NT];
             codes(r + 2, n0);
             codes(r + 3, n1);
-            mul(c0, f0);
-            mul(c1, f1);
+            mul(c0, f0, g0);
+            mul(c1, f1, g1);
 #pragma unroll
             for (int tt = 0; tt < NT; ++tt) {
                 c0[tt] = n0[tt];
@@ -1654,87 +1647,57 @@ __device__ __forceinline__ void run_chains(Chains<NT> &c, const uint8_t *lds, in
         }
     }
     // one read per step (NT = 4 keeps its registers for the chains)
+#pragma unroll 1
     for (; r < R; ++r) {
-        double2 f0[NT];
-#pragma unroll
-        for (int tt = 0; tt < NT; ++tt) f0[tt] = *(const double2 *)(lds + c0[tt]);
+        double2 f0[NT], g0[NT];
+        rows(c0, f0, g0);
         uint32_t n0[NT];
         codes(r + 1, n0);
-        mul(c0, f0);
+        mul(c0, f0, g0);
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt) c0[tt] = n0[tt];
     }
 }
 
-// the chains of the (at most two) base classes b0, b1 (bank bits) of a column,
-// explicit class matches, read order; four reads per batch so their codes and
-// table rows are each one LDS round trip
-__device__ __forceinline__ void two_chains(const uint8_t *lds, const uint2 rm, int R, int t, int stage_addr, int T,
-                                           uint32_t b0, uint32_t b1, double &U, double &s0, double &s1, int &n0,
-                                           int &n1) {
-    U = 1.0;
-    s0 = 1.0;
-    s1 = 1.0;
-    n0 = 0;
-    n1 = 0;
-    auto step = [&](uint32_t code, double2 f) {
-        const bool m0 = (code & b0) != 0, m1 = (code & b1) != 0;
-        U *= f.y;
-        s0 *= m0 ? f.x : f.y;
-        s1 *= m1 ? f.x : f.y;
-        n0 += m0;
-        n1 += m1;
-    };
-    int r = 0;
-    for (; r + 4 <= R; r += 4) {
-        uint32_t c[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) c[k] = code_at(lds, read_addr(rm, r + k, stage_addr, T), t);
-        double2 f[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) f[k] = *(const double2 *)(lds + c[k]);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) step(c[k], f[k]);
+// destination of record scalar k (lane k: field k of dcr_out) as one word:
+// pointer | rec_mul << 56 | off_mul << 60, address = pointer + rec * rec_mul +
+// off * off_mul.  Kept in LDS (read once per record) rather than in scalar
+// registers for the whole kernel.
+__device__ __forceinline__ uint64_t scalar_dest(const dcr_out &O, int k) {
+    const uint64_t rec_mul = k < 7 ? 4u : (k < 9 ? 8u : 0u);
+    const uint64_t off_mul = k == 9 ? 4u : 0u;
+    const uint8_t *p;
+    switch (k) {
+    case 0: p = (const uint8_t *)O.pos; break;
+    case 1: p = (const uint8_t *)O.mapq; break;
+    case 2: p = (const uint8_t *)O.len; break;
+    case 3: p = (const uint8_t *)O.n_cig; break;
+    case 4: p = (const uint8_t *)O.n_de; break;
+    case 5: p = (const uint8_t *)O.D; break;
+    case 6: p = (const uint8_t *)O.M; break;
+    case 7: p = (const uint8_t *)O.E; break;
+    case 8: p = (const uint8_t *)O.E + 4; break;
+    default: p = (const uint8_t *)O.cigar; break;
     }
-    for (; r < R; ++r) {
-        const uint32_t c = code_at(lds, read_addr(rm, r, stage_addr, T), t);
-        step(c, *(const double2 *)(lds + c));
-    }
+    return (uint64_t)(uintptr_t)p | (rec_mul << 56) | (off_mul << 60);
 }
 
-// per-lane destination of the record scalars (lane k: field k of dcr_out,
-// address = optr + rec * rec_mul + off * off_mul)
-struct FastPtr {
-    uint8_t *optr;
-    uint32_t mul;      // rec_mul | off_mul << 8 (bytes per record / per region column)
-};
-
-__device__ __forceinline__ FastPtr fast_ptr(const dcr_out &O, int lane) {
-    FastPtr f;
-    const uint32_t rec_mul = lane < 7 ? 4u : (lane < 9 ? 8u : 0u);
-    const uint32_t off_mul = lane == 9 ? 4u : 0u;
-    f.mul = rec_mul | (off_mul << 8);
-    uint8_t *p;
-    switch (lane) {
-    case 0: p = (uint8_t *)O.pos; break;
-    case 1: p = (uint8_t *)O.mapq; break;
-    case 2: p = (uint8_t *)O.len; break;
-    case 3: p = (uint8_t *)O.n_cig; break;
-    case 4: p = (uint8_t *)O.n_de; break;
-    case 5: p = (uint8_t *)O.D; break;
-    case 6: p = (uint8_t *)O.M; break;
-    case 7: p = (uint8_t *)O.E; break;
-    case 8: p = (uint8_t *)O.E + 4; break;
-    default: p = (uint8_t *)O.cigar; break;
-    }
-    f.optr = p;
-    return f;
+// a pointer cached in LDS at kernel start (rare paths), as a scalar
+template <class Tp>
+__device__ __forceinline__ Tp *lds_ptr(const uint8_t *lds, int slot) {
+    const uint64_t v = *(const uint64_t *)(lds + fk::kPtrs + 8 * slot);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const int hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return (Tp *)(uintptr_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
 template <bool DUPLEX, int NT>
 __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m, FastStage &st, const bool has_next,
-                                             const RecMeta &mn, uint8_t *lds, const int wave, const int lane,
-                                             int &etab_r, uint64_t *stp) {
+                                             const RecMeta &mn, uint8_t *lds, const int stage_addr, const int lane_in,
+                                             uint64_t *stp) {
+    // lane-derived addresses are formed per record, not hoisted out of the
+    // record loop into registers held across it
+    const int lane = opaque(lane_in);
     uint64_t t_prev = 0;
     auto stamp = [&](int k) {
         if (DCR_STAMP) {
@@ -1753,9 +1716,6 @@ __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m
     int T = (int)((m.w >> 7) & 255u);  // single-strand: before the 3' trim, redone below
     const int nq = ((int)(m.w >> 15) + 3) >> 2;
     const int minpos = m.minpos;
-    const int stage_addr = fk::kStage + (wave << 12);
-    double *et = (double *)(lds + fk::et_off(wave));
-    double *etab = (double *)(lds + fk::kEtab) + wave * fk::kEtabN;
 
     // phase 0: element codes into the stage
     uint32_t bad = 0;
@@ -1763,10 +1723,10 @@ __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m
     for (int u = 0; u < kStageQ; ++u) {
         const int d = u * kWave + lane;
         if (d < nq) {
-            const uint2 c0 = make_codes4<DUPLEX>(st.vb[u].x, st.vq[u].x, a.kq, bad);
-            const uint2 c1 = make_codes4<DUPLEX>(st.vb[u].y, st.vq[u].y, a.kq, bad);
-            const uint2 c2 = make_codes4<DUPLEX>(st.vb[u].z, st.vq[u].z, a.kq, bad);
-            const uint2 c3 = make_codes4<DUPLEX>(st.vb[u].w, st.vq[u].w, a.kq, bad);
+            const uint2 c0 = make_codes4<DUPLEX>(st.vb[u].x, st.vq[u].x, a.kq, a.kqlo, bad);
+            const uint2 c1 = make_codes4<DUPLEX>(st.vb[u].y, st.vq[u].y, a.kq, a.kqlo, bad);
+            const uint2 c2 = make_codes4<DUPLEX>(st.vb[u].z, st.vq[u].z, a.kq, a.kqlo, bad);
+            const uint2 c3 = make_codes4<DUPLEX>(st.vb[u].w, st.vq[u].w, a.kq, a.kqlo, bad);
             *(uint4 *)(lds + stage_addr + 32 * d) = make_uint4(c0.x, c0.y, c1.x, c1.y);
             *(uint4 *)(lds + stage_addr + 32 * d + 16) = make_uint4(c2.x, c2.y, c3.x, c3.y);
         }
@@ -1780,17 +1740,21 @@ __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m
         // the general kernel reads the preprocessed reads (info, normalised runs)
         if (!DUPLEX && lane < R) {
             const int tl = ((int)rm.x >> 8) & 255;
-            if (tl > 0) a.norm_cig[a.cig_off[m.g0 + lane]] = (uint32_t)tl << 4;   // one M run
+            uint32_t *norm_cig = lds_ptr<uint32_t>(lds, 10);
+            const int32_t *cig_off = lds_ptr<const int32_t>(lds, 11);
+            if (tl > 0) norm_cig[cig_off[m.g0 + lane]] = (uint32_t)tl << 4;   // one M run
         }
+        int *ovf = lds_ptr<int>(lds, 12);
+        int *ovf_count = lds_ptr<int>(lds, 13);
         if (lane == 0) {
-            const int idx = atomicAdd(a.ovf_count, 1);
-            a.ovf[idx] = (int)rec;
+            const int idx = atomicAdd(ovf_count, 1);
+            ovf[idx] = (int)rec;
         }
     };
+    lds_fence();
     if (!DUPLEX) {
         // trim_3prime_N (:292-325): drop each read's trailing 'N' (sequenced, or
-        // masked below min_base_quality, :280): codes in bank N, read from the end
-        lds_fence();
+        // masked below min_base_quality, :280): codes of class N, from the end
         const int x = (int)rm.x, y = (int)rm.y;
         const int col = x & 255;
         int tl = lane < R ? (x >> 8) & 255 : 0;
@@ -1798,7 +1762,7 @@ __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m
         while (__ballot(go)) {
             if (go) {
                 const uint32_t code = *(const uint16_t *)(lds + stage_addr + 2 * (y + tl - 1));
-                if (code < 0x800u) --tl; else go = false;
+                if (code < (uint32_t)fk::kHalf) --tl; else go = false;
                 go = go && tl > 0;
             }
         }
@@ -1820,121 +1784,64 @@ __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m
     }
     if (__ballot(bad != 0)) { to_general(); return; }
     if (DCR_ABL == 1) {                 // diagnostic: staging only
-        lds_fence();
         if (lane == 0) O.pos[rec] = *(const uint16_t *)(lds + stage_addr + 2 * (int)(rm.y & 7)) + msum;
         return;
     }
-    // e/d of a one-class column: d = n rows of the class, e = R - n (:1001-1012)
-    if (R != etab_r) {
-        if (lane < R) etab[lane] = lane == 0 ? 1.0 : (double)(R - lane) / (double)lane;
-        if (lane == 0) etab[R] = 0.0;
-        etab_r = R;
-    }
-    lds_fence();
-
-    stamp(4);                          // [3] e/d table, fence
-    Chains<NT> c;
-    run_chains<NT>(c, lds, R, rm, stage_addr, T, lane);
+    stamp(4);                          // [3] trim, fence
+    const int colr = (int)(rm.x & 255u), lenr = (int)((rm.x >> 8) & 255u);
+    const int crv = stage_addr + 2 * ((int)rm.y - colr);
+    Chains4<NT> c;
+    if (__ballot(lane < R && (colr != 0 || lenr < T)) == 0) run_chains4<NT, true>(c, lds, R, rm.x, crv, lane);
+    else run_chains4<NT, false>(c, lds, R, rm.x, crv, lane);
     stamp(5);                          // [4] products
     if (DCR_ABL == 2) {                 // diagnostic: staging + products
         double x = 0.0;
 #pragma unroll
-        for (int tt = 0; tt < NT; ++tt) x += c.s[tt] + c.U[tt] + (double)(c.seen[tt] ^ c.cnt[tt]);
+        for (int tt = 0; tt < NT; ++tt)
+            x += (c.L[tt][0] + c.L[tt][1]) + (c.L[tt][2] + c.L[tt][3]) + (double)c.cnt[tt];
         if (lane == 0) O.E[rec] = x;
         return;
     }
 
+    // finalize every tile in registers: call, depth d and errors e (:970-1021)
+    const double *etab = (const double *)(lds + fk::kEtab);
+    bool outside = false;              // a live column outside the fast bound
     int dmax = -1, dmin = 0x7fffffff;
-    // One column's results, kept in registers (d | e << 8 | char << 16 per tile)
-    // and written out at the end with 16-byte stores.  Every column of this
-    // kernel is called inside the fast bound (quality maxQ, a base, never
-    // masked), so there is no consensus 'N' to trim (:770-784): the kept span
-    // is [0, T), one M run.
-    uint32_t ov[NT];
-    double ex[NT];                     // e/d of the lane's column per tile (0 outside T)
-    auto put = [&](int t, bool live, int ch, int d, int e, double etv) -> uint32_t {
+    uint32_t ov[NT];                   // d | e << 8 | char << 16
+    double ex[NT];                     // e/d of the lane's column (0 outside T)
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+        const int t = 64 * tt + lane;
+        const bool live = t < T;
+        const double LA = c.L[tt][0], LT = c.L[tt][1], LC = c.L[tt][2], LG = c.L[tt][3];
+        const double mx = __builtin_fmax(__builtin_fmax(LA, LT), __builtin_fmax(LC, LG));
+        const double mn = __builtin_fmin(__builtin_fmin(LA, LT), __builtin_fmin(LC, LG));
+        const double other = (((LA + LT) + (LC + LG)) - mx) + (mn + mn);
+        outside |= live && !(other * a.ca < mx * a.cb);
+        // the call: the first chain equal to the largest ("ATCG"), its counter shift
+        const uint32_t kb = LA == mx ? 0u : LT == mx ? 1u : LC == mx ? 2u : 3u;
+        const uint32_t cnt = c.cnt[tt];
+        const int d = R - (int)(cnt & 63u);                          // rows that are not 'N'
+        const int e = R - (int)((cnt >> (6 * kb + 6)) & 63u);        // rows that differ from the call
+        const double etv = etab[64 * d + e];
+        ov[tt] = (uint32_t)d | ((uint32_t)e << 8) | (kb << 16);
+        ex[tt] = live ? etv : 0.0;
         if (live) {
-            et[t] = etv;
             dmax = max(dmax, d);
             dmin = min(dmin, d);
         }
-        return (uint32_t)d | ((uint32_t)e << 8) | ((uint32_t)ch << 16);
-    };
-    // one-class columns (compile-time tile indices: chain registers are not
-    // indexed dynamically); every tile's table lookup is issued before use
-    uint32_t defer = 0;                // tiles needing the two-class path (uniform bit mask)
-    uint32_t banks = 0;                // classes present per column, 4 bits per tile
-    int kk[NT], nn_[NT];
-    bool fast[NT];
-    double ev[NT];
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt) {
-        const uint32_t bank = (c.seen[tt] >> 11) & 15u;
-        kk[tt] = bank ? __builtin_ctz(bank) : 0;
-        nn_[tt] = (int)(c.cnt[tt] >> kk[tt]);
-        fast[tt] = (bank & (bank - 1u)) == 0 && nn_[tt] > 0 && (5.0 * c.U[tt]) * a.ca < c.s[tt] * a.cb;
-        ev[tt] = etab[min(nn_[tt], R)];
-        banks |= bank << (4 * tt);
     }
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt) {
-        const int t = 64 * tt + lane;
-        const bool live = t < T;
-        ov[tt] = 0;
-        ex[tt] = 0.0;
-        if (DCR_ABL != 3 && __ballot(live && !fast[tt])) {
-            defer |= 1u << tt;
-            continue;
-        }
-        ov[tt] = put(t, live, (int)((0x47435441u >> (8 * kk[tt])) & 0xffu), nn_[tt], R - nn_[tt], ev[tt]);   // "ATCG"
-        ex[tt] = live ? ev[tt] : 0.0;
-    }
-    stamp(6);                          // [5] one-class tiles
-    // other tiles: the chains of the two classes present, explicit class
-    // matches, in read order.  A column with three or more classes, or outside
-    // the bound (a low-confidence or masked call, :617), sends the record to the
-    // general kernel, which runs the reference's full finalize.
-    while (defer) {
-        const int tt = __builtin_ctz(defer);
-        defer &= defer - 1u;
-        const int t = 64 * tt + lane;
-        const bool live = t < T;
-        const uint32_t bank = (banks >> (4 * tt)) & 15u;
-        if (wave_max(live ? __popc(bank) : 0) > 2) { to_general(); return; }
-        const int k0 = bank ? __builtin_ctz(bank) : -1;
-        const uint32_t rest = bank & (bank - 1u);
-        const int k1 = rest ? __builtin_ctz(rest) : -1;
-        double U, s0, s1;
-        int n0, n1;
-        two_chains(lds, rm, R, t, stage_addr, T, k0 >= 0 ? 0x800u << k0 : 0u, k1 >= 0 ? 0x800u << k1 : 0u, U, s0, s1,
-                   n0, n1);
-        // the bound with the largest chain b against the rest: S = b + other + 4U
-        const bool two = k1 >= 0;
-        const bool hi1 = two && s1 > s0;
-        const double bb = hi1 ? s1 : s0;
-        const double other = two ? (hi1 ? s0 : s1) + 4.0 * U : 5.0 * U;
-        const bool fst = k0 >= 0 && other * a.ca < bb * a.cb;
-        if (__ballot(live && !fst)) { to_general(); return; }
-        const int kb = hi1 ? k1 : k0;
-        const int d = n0 + (two ? n1 : 0), e = R - (hi1 ? n1 : n0);
-        const double etv = (double)e / (double)d;
-        const uint32_t v = put(t, live, (int)((0x47435441u >> (8 * (kb & 3))) & 0xffu), d, e, etv);
-#pragma unroll
-        for (int k = 0; k < NT; ++k)   // constant register index per case
-            if (k == tt) {
-                ov[k] = v;
-                ex[k] = live ? etv : 0.0;
-            }
-    }
-    stamp(7);                          // [6] two-class tiles
+    if (__ballot(outside)) { to_general(); return; }
+    stamp(6);                          // [5] finalize
     const int Dmax = wave_max(dmax);
     const int Dmin = wave_min(dmin);
+    stamp(7);                          // [6] depth reductions
     // d / e / seq / qual straight from registers; the region tail up to the
     // next 16 columns gets 'N' / quality 0 so a duplex record staging this
     // region never reads a byte that is not a valid letter
-    {
+    if (DCR_ABL != 5) {                 // diagnostic 5: no per-column stores
         const int T16 = (T + 15) & ~15;
-        const int ln = opaque(lane);
+        const int ln = lane;
         uint16_t *od = O.d + off;
         uint16_t *oe = O.e + off;
         uint8_t *oseq = O.seq + off;
@@ -1945,7 +1852,7 @@ __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m
             if (t < T) {
                 od[t] = (uint16_t)(ov[tt] & 255u);
                 oe[t] = (uint16_t)((ov[tt] >> 8) & 255u);
-                oseq[t] = (uint8_t)(ov[tt] >> 16);
+                oseq[t] = (uint8_t)__builtin_amdgcn_perm(0u, 0x47435441u, ov[tt] >> 16);   // "ATCG"[kb]
                 oqual[t] = (uint8_t)a.maxq;
             } else if (t < T16) {
                 oseq[t] = (uint8_t)'N';
@@ -1953,12 +1860,13 @@ __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m
             }
         }
     }
-    stamp(8);                          // [7] depth reductions, per-column stores
+    stamp(8);                          // [7] per-column stores
     // E = round(mean(e/d), 3) (:1015-1018).  numpy's mean is a pairwise sum
     // divided by T, then rounded at 3 decimals.  Any summation order lands
     // within 1e-12 (relative) of it, so the rounding agrees unless mean x 1000
     // sits that close to a half-integer; a DPP tree sum decides, and the exact
-    // pairwise walk over the LDS copy runs only near such a boundary.
+    // pairwise walk (over the e/d columns written into the now free stage) runs
+    // only near such a boundary.
     double sum = 0.0;
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) sum += ex[tt];
@@ -1973,8 +1881,13 @@ __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m
     if (__builtin_expect(__builtin_fabs(fr - 0.5) > 1e-9 * (1.0 + y), 1) && DCR_ABL != 4) {
         E = __builtin_rint(y) / 1000.0;
     } else {
+        double *et = (double *)(lds + stage_addr);
+        const int ln = lane;
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt)
+            if (64 * tt + ln < T) et[64 * tt + ln] = ex[tt];
         lds_fence();
-        const double total = 0.0 + pairwise_et(et, T, opaque(lane));
+        const double total = 0.0 + pairwise_et(et, T, ln);
         E = __builtin_rint((total / (double)T) * 1000.0) / 1000.0;
     }
     stamp(9);                          // [8] mean
@@ -1993,8 +1906,9 @@ __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m
                       : lane == 7 ? E_lo
                       : lane == 8 ? E_hi
                                   : (int)((uint32_t)T << 4);   // one M run of T
-        const FastPtr fp = fast_ptr(O, opaque(lane));
-        if (lane < 10) *(int *)(fp.optr + rec * (int64_t)(fp.mul & 255u) + off * (int64_t)(fp.mul >> 8)) = v;
+        const uint64_t dst = *(const uint64_t *)(lds + fk::kPtrs + 8 * min(lane, 9));
+        uint8_t *p = (uint8_t *)(uintptr_t)(dst & 0x00FFFFFFFFFFFFFFull);
+        if (lane < 10) *(int *)(p + rec * (int64_t)((dst >> 56) & 15u) + off * (int64_t)(dst >> 60)) = v;
         if (lane == 0) O.status[rec] = DCR_ST_OK;
     }
     stamp(10);                         // [9] record scalars
@@ -2011,30 +1925,46 @@ __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
     return m;
 }
 
-// Persistent: wave w of NW takes the contiguous fast-list range
-// [n w / NW, n (w+1) / NW); record i + 1's loads are issued while record i is
-// processed, and the descriptor of record i + 2 is fetched by a vector load
-// (vmcnt, not lgkmcnt, so LDS waits never drain it).
+// Persistent, one 16-wave block per CU sharing the likelihood and e/d tables:
+// wave w of NW takes the contiguous fast-list range [n w / NW, n (w+1) / NW);
+// record i + 1's loads are issued while record i is processed, and the
+// descriptor of record i + 2 is fetched by a vector load (vmcnt, not lgkmcnt,
+// so LDS waits never drain it).
 template <bool DUPLEX>
-#ifndef DCR_FAST_WAVES
-#define DCR_FAST_WAVES 4
-#endif
-__global__ __launch_bounds__(kBlock, DCR_FAST_WAVES) void k_consensus_fast(FastArgs a) {
+__global__ __launch_bounds__(fk::kBlockThreads) void k_consensus_fast(FastArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[fk::kLdsBytes];
     const dcr_params *P = a.P;
-    for (int i = threadIdx.x; i < 6 * (fk::kRowMax + 1); i += kBlock) {
-        const int b = i / (fk::kRowMax + 1), q = i % (fk::kRowMax + 1);
-        if (b == 3) continue;                                 // bank X: e/d columns live there
-        const double mm = P->mismatch[q];
-        *(double2 *)(lds + fk::bank_base(b) + 16 * b + 16 * q) = make_double2(b == 0 ? mm : P->match[q], mm);
+    for (int i = threadIdx.x; i < 5 * (fk::kRowMax + 1); i += fk::kBlockThreads) {
+        const int k = i / (fk::kRowMax + 1), q = i % (fk::kRowMax + 1);
+        const double mm = P->mismatch[q], mt = P->match[q];
+        uint8_t *row = lds + fk::bank_base(k) + 16 * (q + k);
+        *(double2 *)row = make_double2(k == 1 ? mt : mm, k == 2 ? mt : mm);
+        *(double2 *)(row + fk::kHalf) = make_double2(k == 3 ? mt : mm, k == 4 ? mt : mm);
+    }
+    for (int i = threadIdx.x; i < 64 * 64; i += fk::kBlockThreads) {
+        const int d = i >> 6, e = i & 63;
+        ((double *)(lds + fk::kEtab))[i] = d == 0 ? 1.0 : (double)e / (double)d;   // :1010-1012
     }
     if (threadIdx.x == 0) *(uint16_t *)(lds + fk::kSent) = (uint16_t)fk::kPadCode;
+    if (threadIdx.x < 14) {
+        const int k = threadIdx.x;
+        uint64_t v;
+        switch (k) {
+        case 10: v = (uint64_t)(uintptr_t)a.norm_cig; break;
+        case 11: v = (uint64_t)(uintptr_t)a.cig_off; break;
+        case 12: v = (uint64_t)(uintptr_t)a.ovf; break;
+        case 13: v = (uint64_t)(uintptr_t)a.ovf_count; break;
+        default: v = scalar_dest(a.O, k); break;
+        }
+        *(uint64_t *)(lds + fk::kPtrs + 8 * k) = v;
+    }
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
+    const int stage_addr = fk::stage_base(wave);
     __syncthreads();
     const int64_t n = *a.fast_count;
-    const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
-    const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+    const int64_t nw = (int64_t)gridDim.x * fk::kWaves;
+    const int64_t gw = (int64_t)blockIdx.x * fk::kWaves + wave;
     int i = (int)(n * gw / nw);
     const int iend = (int)(n * (gw + 1) / nw);
     if (i >= iend) return;
@@ -2043,17 +1973,16 @@ __global__ __launch_bounds__(kBlock, DCR_FAST_WAVES) void k_consensus_fast(FastA
     RecMeta m1 = ML[min(i + 1, iend - 1)];
     FastStage st;
     fast_load<DUPLEX>(a, m0, lane, st);
-    int etab_r = -1;
     uint64_t stp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (;;) {
         const bool has_next = i + 1 < iend;
         const int i2 = min(i + 2, iend - 1);
         const uint32_t mv = lane < 8 ? ((const uint32_t *)(ML + i2))[lane] : 0u;
         const int T = (int)((m0.w >> 7) & 255u);
-        if (T <= 64) process_fast<DUPLEX, 1>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp);
-        else if (T <= 128) process_fast<DUPLEX, 2>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp);
-        else if (T <= 192) process_fast<DUPLEX, 3>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp);
-        else process_fast<DUPLEX, 4>(a, m0, st, has_next, m1, lds, wave, lane, etab_r, stp);
+        if (T <= 64) process_fast<DUPLEX, 1>(a, m0, st, has_next, m1, lds, stage_addr, lane, stp);
+        else if (T <= 128) process_fast<DUPLEX, 2>(a, m0, st, has_next, m1, lds, stage_addr, lane, stp);
+        else if (T <= 192) process_fast<DUPLEX, 3>(a, m0, st, has_next, m1, lds, stage_addr, lane, stp);
+        else process_fast<DUPLEX, 4>(a, m0, st, has_next, m1, lds, stage_addr, lane, stp);
         if (++i >= iend) break;
         m0 = m1;
         m1 = meta_from_lanes(mv);
@@ -2061,7 +1990,6 @@ __global__ __launch_bounds__(kBlock, DCR_FAST_WAVES) void k_consensus_fast(FastA
     if (DCR_STAMP && lane == 0)
         for (int k = 0; k < 10; ++k) atomicAdd(&a.stamps[k + (DUPLEX ? 16 : 0)], (unsigned long long)stp[k]);
 }
-
 
 // persistent: drains the general list written by k_recmeta
 template <bool DUPLEX>

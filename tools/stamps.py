@@ -38,8 +38,8 @@ for _ in range(K):
     lib.dcr_last_kernel_timing(ctx, ms)
     kt = [a + b for a, b in zip(kt, ms)]
 lib.dcr_debug_stamps(ctx, st, 32, 0)
-names = ["prefetch wait", "codes into LDS", "prefetch issue", "e/d table, fence", "products",
-         "one-class tiles", "two-class tiles", "depth reductions", "pairwise mean", "record scalars"]
+names = ["prefetch wait", "codes into LDS", "prefetch issue", "trim, fence", "products",
+         "finalize", "depth reductions", "column stores", "mean", "record scalars"]
 for kind, base, nrec, kidx in (("single-strand", 0, 4 * nfam, 2), ("duplex", 16, 2 * nfam, 5)):
     tot = sum(st[base + k] for k in range(10))
     print(f"{kind}: kernel {kt[kidx] / K:.3f} ms; cycles per record per wave (s_memtime ticks):")
