@@ -1301,6 +1301,18 @@ __device__ __forceinline__ int opaque(int v) {
     return v;
 }
 
+// IEEE max / min of two doubles known not to be NaN (no canonicalising moves)
+__device__ __forceinline__ double vmax_f64(double x, double y) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+__device__ __forceinline__ double vmin_f64(double x, double y) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+
 __device__ __forceinline__ void lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1503,7 +1515,9 @@ constexpr int kHalf = 0x800;                               // (f.c, f.g) half-ro
 constexpr int kEtab = 0x15000;                             // e/d [d][e], d, e < 64
 constexpr int kSent = kEtab + 64 * 64 * 8;                 // u16 pad code (out-of-read sentinel)
 constexpr int kPtrs = kSent + 16;                          // u64 [10] record-scalar destinations, [4] rare-path pointers
-constexpr int kLdsBytes = kPtrs + 14 * 8;
+constexpr int kRm = kPtrs + 16 * 8;                        // per wave: u64 [64] the current record's read words
+constexpr int kMv = kRm + kWaves * kWave * 8;              // per wave: u32 [8] a later record's descriptor
+constexpr int kLdsBytes = kMv + kWaves * 32;
 static_assert(kStageElems * 2 == 0x1000, "one 4 KiB stage per wave");
 static_assert(16 * (kRowMax + 4) + kHalf <= 0x1000, "a class bank fits 4 KiB");
 static_assert(kLdsBytes <= 160 * 1024, "one block per CU");
@@ -1519,11 +1533,13 @@ constexpr int kStageQ = kStageElems / 16 / kWave;   // staged 16-byte quads per 
 struct FastStage {
     uint4 vb[kStageQ], vq[kStageQ];        // raw base / quality bytes
     uint2 rm;                              // this lane's read meta (lane < R)
+    uint32_t mv;                           // dword `lane` of a later record's descriptor (lanes < 8)
 };
 
 // issue a record's loads (consumed by the next process_fast call)
 template <bool DUPLEX>
-__device__ __forceinline__ void fast_load(const FastArgs &a, const RecMeta &m, int lane, FastStage &st) {
+__device__ __forceinline__ void fast_load(const FastArgs &a, const RecMeta &m, const RecMeta *mlater, int lane,
+                                          FastStage &st) {
     const uint8_t *gb = a.gb;
     const uint8_t *gq = a.gq;
     const int nq = ((int)(m.w >> 15) + 3) >> 2;
@@ -1539,6 +1555,7 @@ __device__ __forceinline__ void fast_load(const FastArgs &a, const RecMeta &m, i
     }
     const int R = (int)(m.w & 127u);
     st.rm = a.rmeta[m.g0 + min(lane, R - 1)];
+    st.mv = ((const uint32_t *)mlater)[lane & 7];
 }
 
 // Four element codes from four bases and qualities (SWAR).  The class comes
@@ -1691,33 +1708,25 @@ __device__ __forceinline__ Tp *lds_ptr(const uint8_t *lds, int slot) {
     return (Tp *)(uintptr_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
-template <bool DUPLEX, int NT>
-__device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m, FastStage &st, const bool has_next,
-                                             const RecMeta &mn, uint8_t *lds, const int stage_addr, const int lane_in,
-                                             uint64_t *stp) {
-    // lane-derived addresses are formed per record, not hoisted out of the
-    // record loop into registers held across it
-    const int lane = opaque(lane_in);
+// diagnostic phase clock (DCR_STAMP builds): cycles per phase, summed per wave
+struct Stamps {
     uint64_t t_prev = 0;
-    auto stamp = [&](int k) {
+    uint64_t acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    __device__ __forceinline__ void mark(int k) {
         if (DCR_STAMP) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
-            if (k > 0) stp[k - 1] += now - t_prev;
+            if (k > 0) acc[k - 1] += now - t_prev;
             t_prev = now;
         }
-    };
-    stamp(0);
-    if (DCR_STAMP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp(1);                          // [0] wait for this record's prefetched bytes
-    const dcr_out &O = a.O;
-    const int64_t rec = m.rec;
-    const int64_t off = m.off;
-    const int R = (int)(m.w & 127u);
-    int T = (int)((m.w >> 7) & 255u);  // single-strand: before the 3' trim, redone below
-    const int nq = ((int)(m.w >> 15) + 3) >> 2;
-    const int minpos = m.minpos;
+    }
+};
 
-    // phase 0: element codes into the stage
+// phase 0: element codes of the prefetched bytes into the stage; returns the
+// lanes' invalid-input flags
+template <bool DUPLEX>
+__device__ __forceinline__ uint32_t stage_codes(const FastArgs &a, const RecMeta &m, const FastStage &st, uint8_t *lds,
+                                                int stage_addr, int lane) {
+    const int nq = ((int)(m.w >> 15) + 3) >> 2;
     uint32_t bad = 0;
 #pragma unroll
     for (int u = 0; u < kStageQ; ++u) {
@@ -1731,26 +1740,48 @@ __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m
             *(uint4 *)(lds + stage_addr + 32 * d + 16) = make_uint4(c2.x, c2.y, c3.x, c3.y);
         }
     }
-    uint2 rm = st.rm;                  // this record's read meta; st is reused by the prefetch
-    const int msum = wave_sum(lane < R ? ((int)rm.x >> 16) & 255 : 0);
-    stamp(2);                          // [1] element codes into LDS
-    if (has_next) fast_load<DUPLEX>(a, mn, lane, st);
-    stamp(3);                          // [2] prefetch issue
-    auto to_general = [&]() {
-        // the general kernel reads the preprocessed reads (info, normalised runs)
-        if (!DUPLEX && lane < R) {
-            const int tl = ((int)rm.x >> 8) & 255;
-            uint32_t *norm_cig = lds_ptr<uint32_t>(lds, 10);
-            const int32_t *cig_off = lds_ptr<const int32_t>(lds, 11);
-            if (tl > 0) norm_cig[cig_off[m.g0 + lane]] = (uint32_t)tl << 4;   // one M run
-        }
-        int *ovf = lds_ptr<int>(lds, 12);
-        int *ovf_count = lds_ptr<int>(lds, 13);
-        if (lane == 0) {
-            const int idx = atomicAdd(ovf_count, 1);
-            ovf[idx] = (int)rec;
-        }
-    };
+    return bad;
+}
+
+// the general kernel takes the record: it reads the preprocessed reads (info,
+// normalised runs); pointers from the LDS cache
+template <bool DUPLEX>
+__device__ __forceinline__ void send_to_general_(int rec, int g0, int R, uint32_t rmx, const uint8_t *lds, int lane) {
+    if (!DUPLEX && lane < R) {
+        const int tl = ((int)rmx >> 8) & 255;
+        uint32_t *norm_cig = lds_ptr<uint32_t>(lds, 10);
+        const int32_t *cig_off = lds_ptr<const int32_t>(lds, 11);
+        if (tl > 0) norm_cig[cig_off[g0 + lane]] = (uint32_t)tl << 4;   // one M run
+    }
+    int *ovf = lds_ptr<int>(lds, 12);
+    int *ovf_count = lds_ptr<int>(lds, 13);
+    if (lane == 0) {
+        const int idx = atomicAdd(ovf_count, 1);
+        ovf[idx] = rec;
+    }
+}
+template <bool DUPLEX>
+__device__ __forceinline__ void send_to_general(const FastArgs &, const RecMeta &m, uint2 rm, const uint8_t *lds,
+                                                int lane) {
+    send_to_general_<DUPLEX>(m.rec, m.g0, (int)(m.w & 127u), rm.x, lds, lane);
+}
+
+struct Staged {
+    uint2 rm;      // the lane's read meta (single-strand: length after the 3' trim)
+    int T;         // columns (:458-459, on the trimmed reads)
+    int msum;      // sum of the reads' MAPQs
+    int state;     // 0 consensus here, 1 general kernel, 2 finished (status written)
+};
+
+// after the codes: 3' trim (single-strand), read info, T; invalid input -> general
+template <bool DUPLEX>
+__device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &m, uint2 rm, uint32_t bad,
+                                              const uint8_t *lds, int stage_addr, int lane) {
+    Staged s;
+    const int R = (int)(m.w & 127u);
+    s.T = (int)((m.w >> 7) & 255u);
+    s.msum = wave_sum(lane < R ? ((int)rm.x >> 16) & 255 : 0);
+    s.state = 0;
     lds_fence();
     if (!DUPLEX) {
         // trim_3prime_N (:292-325): drop each read's trailing 'N' (sequenced, or
@@ -1776,24 +1807,39 @@ __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m
             a.info[m.g0 + lane] = inf;
         }
         rm.x = (rm.x & ~0xFF00u) | ((uint32_t)tl << 8);
-        T = wave_max(lane < R ? col + tl : 0);                       // :458-459 on the trimmed reads
+        s.T = wave_max(lane < R ? col + tl : 0);
         if (__ballot(lane < R && tl == 0)) {
-            if (lane == 0) write_status_at(O, rec, DCR_ST_UPSTREAM);
-            return;
+            if (lane == 0) write_status_at(a.O, m.rec, DCR_ST_UPSTREAM);
+            s.state = 2;
         }
     }
-    if (__ballot(bad != 0)) { to_general(); return; }
+    s.rm = rm;
+    if (s.state == 0 && __ballot(bad != 0)) s.state = 1;
+    return s;
+}
+
+// products, finalize, outputs of a staged record of T <= 64 NT columns
+template <bool DUPLEX, int NT>
+__device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &m, const Staged &sg, uint8_t *lds,
+                                              const int stage_addr, const int lane, Stamps &sp) {
+    const dcr_out &O = a.O;
+    const int64_t rec = m.rec;
+    const int64_t off = m.off;
+    const int R = (int)(m.w & 127u);
+    const int T = sg.T;
+    const int msum = sg.msum;
+    const int minpos = m.minpos;
+    const uint2 rm = sg.rm;
     if (DCR_ABL == 1) {                 // diagnostic: staging only
         if (lane == 0) O.pos[rec] = *(const uint16_t *)(lds + stage_addr + 2 * (int)(rm.y & 7)) + msum;
         return;
     }
-    stamp(4);                          // [3] trim, fence
     const int colr = (int)(rm.x & 255u), lenr = (int)((rm.x >> 8) & 255u);
     const int crv = stage_addr + 2 * ((int)rm.y - colr);
     Chains4<NT> c;
     if (__ballot(lane < R && (colr != 0 || lenr < T)) == 0) run_chains4<NT, true>(c, lds, R, rm.x, crv, lane);
     else run_chains4<NT, false>(c, lds, R, rm.x, crv, lane);
-    stamp(5);                          // [4] products
+    sp.mark(5);                          // [4] products
     if (DCR_ABL == 2) {                 // diagnostic: staging + products
         double x = 0.0;
 #pragma unroll
@@ -1803,39 +1849,40 @@ __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m
         return;
     }
 
-    // finalize every tile in registers: call, depth d and errors e (:970-1021)
+    // finalize every tile in registers: call, depth d and errors e (:970-1021),
+    // straight-line (selects, no per-tile branches)
     const double *etab = (const double *)(lds + fk::kEtab);
-    bool outside = false;              // a live column outside the fast bound
+    uint32_t outside = 0;              // a live column outside the fast bound
     int dmax = -1, dmin = 0x7fffffff;
-    uint32_t ov[NT];                   // d | e << 8 | char << 16
+    uint32_t ov[NT];                   // d | e << 8 | call index << 16
     double ex[NT];                     // e/d of the lane's column (0 outside T)
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
         const int t = 64 * tt + lane;
         const bool live = t < T;
         const double LA = c.L[tt][0], LT = c.L[tt][1], LC = c.L[tt][2], LG = c.L[tt][3];
-        const double mx = __builtin_fmax(__builtin_fmax(LA, LT), __builtin_fmax(LC, LG));
-        const double mn = __builtin_fmin(__builtin_fmin(LA, LT), __builtin_fmin(LC, LG));
+        const double mx = vmax_f64(vmax_f64(LA, LT), vmax_f64(LC, LG));
+        const double mn = vmin_f64(vmin_f64(LA, LT), vmin_f64(LC, LG));
         const double other = (((LA + LT) + (LC + LG)) - mx) + (mn + mn);
-        outside |= live && !(other * a.ca < mx * a.cb);
-        // the call: the first chain equal to the largest ("ATCG"), its counter shift
-        const uint32_t kb = LA == mx ? 0u : LT == mx ? 1u : LC == mx ? 2u : 3u;
+        outside |= (uint32_t)(!(other * a.ca < mx * a.cb)) & (uint32_t)live;
+        // the call: the first chain equal to the largest ("ATCG")
+        uint32_t kb = LC == mx ? 2u : 3u;
+        kb = LT == mx ? 1u : kb;
+        kb = LA == mx ? 0u : kb;
         const uint32_t cnt = c.cnt[tt];
-        const int d = R - (int)(cnt & 63u);                          // rows that are not 'N'
-        const int e = R - (int)((cnt >> (6 * kb + 6)) & 63u);        // rows that differ from the call
+        const int d = R - (int)(cnt & 63u);                                       // rows that are not 'N'
+        const int e = R - (int)__builtin_amdgcn_ubfe(cnt, 6u * kb + 6u, 6u);      // rows that differ from the call
         const double etv = etab[64 * d + e];
         ov[tt] = (uint32_t)d | ((uint32_t)e << 8) | (kb << 16);
         ex[tt] = live ? etv : 0.0;
-        if (live) {
-            dmax = max(dmax, d);
-            dmin = min(dmin, d);
-        }
+        dmax = max(dmax, live ? d : -1);
+        dmin = min(dmin, live ? d : 0x7fffffff);
     }
-    if (__ballot(outside)) { to_general(); return; }
-    stamp(6);                          // [5] finalize
+    if (__ballot(outside)) { send_to_general<DUPLEX>(a, m, rm, lds, lane); return; }
+    sp.mark(6);                          // [5] finalize
     const int Dmax = wave_max(dmax);
     const int Dmin = wave_min(dmin);
-    stamp(7);                          // [6] depth reductions
+    sp.mark(7);                          // [6] depth reductions
     // d / e / seq / qual straight from registers; the region tail up to the
     // next 16 columns gets 'N' / quality 0 so a duplex record staging this
     // region never reads a byte that is not a valid letter
@@ -1860,7 +1907,7 @@ __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m
             }
         }
     }
-    stamp(8);                          // [7] per-column stores
+    sp.mark(8);                          // [7] per-column stores
     // E = round(mean(e/d), 3) (:1015-1018).  numpy's mean is a pairwise sum
     // divided by T, then rounded at 3 decimals.  Any summation order lands
     // within 1e-12 (relative) of it, so the rounding agrees unless mean x 1000
@@ -1890,7 +1937,7 @@ __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m
         const double total = 0.0 + pairwise_et(et, T, ln);
         E = __builtin_rint((total / (double)T) * 1000.0) / 1000.0;
     }
-    stamp(9);                          // [8] mean
+    sp.mark(9);                          // [8] mean
     // the record's scalar fields in one dword store (lane k writes field k,
     // lane 9 the single M run of the CIGAR) plus the status byte
     {
@@ -1911,7 +1958,7 @@ __device__ __forceinline__ void process_fast(const FastArgs &a, const RecMeta &m
         if (lane < 10) *(int *)(p + rec * (int64_t)((dst >> 56) & 15u) + off * (int64_t)(dst >> 60)) = v;
         if (lane == 0) O.status[rec] = DCR_ST_OK;
     }
-    stamp(10);                         // [9] record scalars
+    sp.mark(10);                         // [9] record scalars
 }
 
 __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
@@ -1927,7 +1974,8 @@ __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
 
 // Persistent, one 16-wave block per CU sharing the likelihood and e/d tables:
 // wave w of NW takes the contiguous fast-list range [n w / NW, n (w+1) / NW);
-// record i + 1's loads are issued while record i is processed, and the
+// record i + 1's loads are issued (at ONE site, so the prefetch registers are
+// never copied while in flight) as soon as record i's codes are in LDS, and the
 // descriptor of record i + 2 is fetched by a vector load (vmcnt, not lgkmcnt,
 // so LDS waits never drain it).
 template <bool DUPLEX>
@@ -1959,8 +2007,9 @@ __global__ __launch_bounds__(fk::kBlockThreads) void k_consensus_fast(FastArgs a
         *(uint64_t *)(lds + fk::kPtrs + 8 * k) = v;
     }
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
+    const int lane0 = threadIdx.x & 63;
     const int stage_addr = fk::stage_base(wave);
+    const int rm_addr = fk::kRm + wave * kWave * 8;
     __syncthreads();
     const int64_t n = *a.fast_count;
     const int64_t nw = (int64_t)gridDim.x * fk::kWaves;
@@ -1969,26 +2018,50 @@ __global__ __launch_bounds__(fk::kBlockThreads) void k_consensus_fast(FastArgs a
     const int iend = (int)(n * (gw + 1) / nw);
     if (i >= iend) return;
     const RecMeta *ML = a.meta;
+    const int ilast = iend - 1;
     RecMeta m0 = ML[i];
-    RecMeta m1 = ML[min(i + 1, iend - 1)];
+    RecMeta m1 = ML[min(i + 1, ilast)];
     FastStage st;
-    fast_load<DUPLEX>(a, m0, lane, st);
-    uint64_t stp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    fast_load<DUPLEX>(a, m0, ML + min(i + 2, ilast), lane0, st);
+    Stamps sp;
     for (;;) {
-        const bool has_next = i + 1 < iend;
-        const int i2 = min(i + 2, iend - 1);
-        const uint32_t mv = lane < 8 ? ((const uint32_t *)(ML + i2))[lane] : 0u;
-        const int T = (int)((m0.w >> 7) & 255u);
-        if (T <= 64) process_fast<DUPLEX, 1>(a, m0, st, has_next, m1, lds, stage_addr, lane, stp);
-        else if (T <= 128) process_fast<DUPLEX, 2>(a, m0, st, has_next, m1, lds, stage_addr, lane, stp);
-        else if (T <= 192) process_fast<DUPLEX, 3>(a, m0, st, has_next, m1, lds, stage_addr, lane, stp);
-        else process_fast<DUPLEX, 4>(a, m0, st, has_next, m1, lds, stage_addr, lane, stp);
+        // lane-derived addresses are formed per record, not hoisted out of the
+        // record loop into registers held across it
+        const int lane = opaque(lane0);
+        sp.mark(0);
+        if (DCR_STAMP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        sp.mark(1);                    // [0] wait for this record's prefetched bytes
+        const uint32_t bad = stage_codes<DUPLEX>(a, m0, st, lds, stage_addr, lane);
+        // the read words go through LDS: a register copy of them would live
+        // across the prefetch's refill of st and force a wait for it at the
+        // loop's back edge
+        *(uint2 *)(lds + rm_addr + 8 * lane) = st.rm;
+        if (lane < 8) *(uint32_t *)(lds + fk::kMv + 32 * wave + 4 * lane) = st.mv;
+        sp.mark(2);                    // [1] element codes into LDS
+        __builtin_amdgcn_sched_barrier(0);
+        // record i + 1's bytes and record i + 3's descriptor; unconditional (the
+        // last record re-loads itself) so the registers have one definition
+        fast_load<DUPLEX>(a, m1, ML + min(i + 3, ilast), lane, st);
+        sp.mark(3);                    // [2] prefetch issue
+        lds_fence();
+        const uint2 rm = *(const uint2 *)(lds + rm_addr + 8 * lane);
+        const RecMeta m2 = meta_from_lanes(*(const uint32_t *)(lds + fk::kMv + 32 * wave + 4 * (lane & 7)));   // record i + 2
+        const Staged sg = trim_record<DUPLEX>(a, m0, rm, bad, lds, stage_addr, lane);
+        sp.mark(4);                    // [3] trim, fence
+        if (sg.state == 1) {
+            send_to_general<DUPLEX>(a, m0, sg.rm, lds, lane);
+        } else if (sg.state == 0) {
+            if (sg.T <= 64) finish_record<DUPLEX, 1>(a, m0, sg, lds, stage_addr, lane, sp);
+            else if (sg.T <= 128) finish_record<DUPLEX, 2>(a, m0, sg, lds, stage_addr, lane, sp);
+            else if (sg.T <= 192) finish_record<DUPLEX, 3>(a, m0, sg, lds, stage_addr, lane, sp);
+            else finish_record<DUPLEX, 4>(a, m0, sg, lds, stage_addr, lane, sp);
+        }
         if (++i >= iend) break;
         m0 = m1;
-        m1 = meta_from_lanes(mv);
+        m1 = m2;
     }
-    if (DCR_STAMP && lane == 0)
-        for (int k = 0; k < 10; ++k) atomicAdd(&a.stamps[k + (DUPLEX ? 16 : 0)], (unsigned long long)stp[k]);
+    if (DCR_STAMP && lane0 == 0)
+        for (int k = 0; k < 10; ++k) atomicAdd(&a.stamps[k + (DUPLEX ? 16 : 0)], (unsigned long long)sp.acc[k]);
 }
 
 // persistent: drains the general list written by k_recmeta
