@@ -1517,7 +1517,8 @@ constexpr int kSent = kEtab + 64 * 64 * 8;                 // u16 pad code (out-
 constexpr int kPtrs = kSent + 16;                          // u64 [10] record-scalar destinations, [4] rare-path pointers
 constexpr int kRm = kPtrs + 16 * 8;                        // per wave: u64 [64] the current record's read words
 constexpr int kMv = kRm + kWaves * kWave * 8;              // per wave: u32 [8] a later record's descriptor
-constexpr int kLdsBytes = kMv + kWaves * 32;
+constexpr int kOv = kMv + kWaves * 32;                     // per wave: u16 [256] column words d | e << 6 | call << 12
+constexpr int kLdsBytes = kOv + kWaves * 512;
 static_assert(kStageElems * 2 == 0x1000, "one 4 KiB stage per wave");
 static_assert(16 * (kRowMax + 4) + kHalf <= 0x1000, "a class bank fits 4 KiB");
 static_assert(kLdsBytes <= 160 * 1024, "one block per CU");
@@ -1821,7 +1822,7 @@ __device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &
 // products, finalize, outputs of a staged record of T <= 64 NT columns
 template <bool DUPLEX, int NT>
 __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &m, const Staged &sg, uint8_t *lds,
-                                              const int stage_addr, const int lane, Stamps &sp) {
+                                              const int stage_addr, const int ov_addr, const int lane, Stamps &sp) {
     const dcr_out &O = a.O;
     const int64_t rec = m.rec;
     const int64_t off = m.off;
@@ -1854,7 +1855,7 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
     const double *etab = (const double *)(lds + fk::kEtab);
     uint32_t outside = 0;              // a live column outside the fast bound
     int dmax = -1, dmin = 0x7fffffff;
-    uint32_t ov[NT];                   // d | e << 8 | call index << 16
+    uint8_t *ov = lds + ov_addr;       // column words d | e << 6 | call << 12
     double ex[NT];                     // e/d of the lane's column (0 outside T)
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
@@ -1873,7 +1874,7 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
         const int d = R - (int)(cnt & 63u);                                       // rows that are not 'N'
         const int e = R - (int)__builtin_amdgcn_ubfe(cnt, 6u * kb + 6u, 6u);      // rows that differ from the call
         const double etv = etab[64 * d + e];
-        ov[tt] = (uint32_t)d | ((uint32_t)e << 8) | (kb << 16);
+        *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (kb << 12));
         ex[tt] = live ? etv : 0.0;
         dmax = max(dmax, live ? d : -1);
         dmin = min(dmin, live ? d : 0x7fffffff);
@@ -1883,28 +1884,25 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
     const int Dmax = wave_max(dmax);
     const int Dmin = wave_min(dmin);
     sp.mark(7);                          // [6] depth reductions
-    // d / e / seq / qual straight from registers; the region tail up to the
-    // next 16 columns gets 'N' / quality 0 so a duplex record staging this
-    // region never reads a byte that is not a valid letter
+    // d / e / seq / qual from the column words, four columns per lane (one
+    // 8-, 8-, 4- and 4-byte store each); the region tail up to the next 16
+    // columns gets 'N' / quality 0 so a duplex record staging this region never
+    // reads a byte that is not a valid letter (d / e there are don't-care)
+    lds_fence();
     if (DCR_ABL != 5) {                 // diagnostic 5: no per-column stores
         const int T16 = (T + 15) & ~15;
-        const int ln = lane;
-        uint16_t *od = O.d + off;
-        uint16_t *oe = O.e + off;
-        uint8_t *oseq = O.seq + off;
-        uint8_t *oqual = O.qual + off;
-#pragma unroll
-        for (int tt = 0; tt < NT; ++tt) {
-            const int t = 64 * tt + ln;
-            if (t < T) {
-                od[t] = (uint16_t)(ov[tt] & 255u);
-                oe[t] = (uint16_t)((ov[tt] >> 8) & 255u);
-                oseq[t] = (uint8_t)__builtin_amdgcn_perm(0u, 0x47435441u, ov[tt] >> 16);   // "ATCG"[kb]
-                oqual[t] = (uint8_t)a.maxq;
-            } else if (t < T16) {
-                oseq[t] = (uint8_t)'N';
-                oqual[t] = (uint8_t)0;
-            }
+        const int c0 = 4 * lane;
+        if (c0 < T16) {
+            const uint2 w = *(const uint2 *)(ov + 8 * lane);
+            *(uint2 *)(O.d + off + c0) = make_uint2(w.x & 0x003F003Fu, w.y & 0x003F003Fu);
+            *(uint2 *)(O.e + off + c0) = make_uint2((w.x >> 6) & 0x003F003Fu, (w.y >> 6) & 0x003F003Fu);
+            const uint32_t sel = ((w.x >> 12) & 3u) | ((w.x >> 20) & 0x300u) | ((w.y << 4) & 0x30000u) |
+                                 ((w.y >> 4) & 0x3000000u);
+            const int nl = min(max(T - c0, 0), 4);                       // live columns of the four
+            const uint32_t keep = nl == 4 ? 0xFFFFFFFFu : (1u << (8 * nl)) - 1u;
+            const uint32_t letters = __builtin_amdgcn_perm(0u, 0x47435441u, sel);   // "ATCG"[call]
+            *(uint32_t *)(O.seq + off + c0) = (letters & keep) | (0x4E4E4E4Eu & ~keep);
+            *(uint32_t *)(O.qual + off + c0) = ((uint32_t)a.maxq * 0x01010101u) & keep;
         }
     }
     sp.mark(8);                          // [7] per-column stores
@@ -2010,6 +2008,7 @@ __global__ __launch_bounds__(fk::kBlockThreads) void k_consensus_fast(FastArgs a
     const int lane0 = threadIdx.x & 63;
     const int stage_addr = fk::stage_base(wave);
     const int rm_addr = fk::kRm + wave * kWave * 8;
+    const int ov_addr = fk::kOv + wave * 512;
     __syncthreads();
     const int64_t n = *a.fast_count;
     const int64_t nw = (int64_t)gridDim.x * fk::kWaves;
@@ -2051,10 +2050,10 @@ __global__ __launch_bounds__(fk::kBlockThreads) void k_consensus_fast(FastArgs a
         if (sg.state == 1) {
             send_to_general<DUPLEX>(a, m0, sg.rm, lds, lane);
         } else if (sg.state == 0) {
-            if (sg.T <= 64) finish_record<DUPLEX, 1>(a, m0, sg, lds, stage_addr, lane, sp);
-            else if (sg.T <= 128) finish_record<DUPLEX, 2>(a, m0, sg, lds, stage_addr, lane, sp);
-            else if (sg.T <= 192) finish_record<DUPLEX, 3>(a, m0, sg, lds, stage_addr, lane, sp);
-            else finish_record<DUPLEX, 4>(a, m0, sg, lds, stage_addr, lane, sp);
+            if (sg.T <= 64) finish_record<DUPLEX, 1>(a, m0, sg, lds, stage_addr, ov_addr, lane, sp);
+            else if (sg.T <= 128) finish_record<DUPLEX, 2>(a, m0, sg, lds, stage_addr, ov_addr, lane, sp);
+            else if (sg.T <= 192) finish_record<DUPLEX, 3>(a, m0, sg, lds, stage_addr, ov_addr, lane, sp);
+            else finish_record<DUPLEX, 4>(a, m0, sg, lds, stage_addr, ov_addr, lane, sp);
         }
         if (++i >= iend) break;
         m0 = m1;
