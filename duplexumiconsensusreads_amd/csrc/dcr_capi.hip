@@ -257,6 +257,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         dcr::FastArgs f{};
         f.gb = duplex ? ss->seq : in->bases;
         f.gq = duplex ? ss->qual : in->quals;
+        f.nbytes = duplex ? in->ss_cols : in->n_bases;
         f.meta = c->w.meta;
         f.rmeta = c->w.rmeta;
         f.fast_count = c->w.fast_count + (duplex ? 1 : 0);

@@ -61,6 +61,7 @@ struct Args {
 // the fast kernel's compact arguments (one strand; fewer scalar registers than Args)
 struct FastArgs {
     const uint8_t *gb, *gq;         // staged bytes: input reads (single-strand) or single-strand consensus (duplex)
+    int64_t nbytes;                 // length of gb / gq (buffer-load range check)
     const RecMeta *meta;            // fast list descriptors
     const uint2 *rmeta;             // per-read words
     const int *fast_count;          // fast-list length

@@ -1529,30 +1529,36 @@ __device__ __forceinline__ int stage_base(int wave) {
 }
 }  // namespace fk
 
-constexpr int kStageQ = kStageElems / 16 / kWave;   // staged 16-byte quads per lane
+constexpr int kStageDw = kStageElems / 4 / kWave;   // staged dwords per lane
 
 struct FastStage {
-    uint4 vb[kStageQ], vq[kStageQ];        // raw base / quality bytes
+    uint32_t vb[kStageDw], vq[kStageDw];   // raw base / quality bytes, dword u * 64 + lane of the record
     uint2 rm;                              // this lane's read meta (lane < R)
     uint32_t mv;                           // dword `lane` of a later record's descriptor (lanes < 8)
 };
 
-// issue a record's loads (consumed by the next process_fast call)
+// issue a record's loads (consumed by the next record's stage_codes).  Buffer
+// loads on a resource based at the record's first byte: dword u * 64 + lane at
+// voffset 4 lane + immediate 256 u, no per-lane address arithmetic, and bytes
+// past the end of the array read as 0 (range-checked) instead of faulting.
 template <bool DUPLEX>
 __device__ __forceinline__ void fast_load(const FastArgs &a, const RecMeta &m, const RecMeta *mlater, int lane,
                                           FastStage &st) {
-    const uint8_t *gb = a.gb;
-    const uint8_t *gq = a.gq;
-    const int nq = ((int)(m.w >> 15) + 3) >> 2;
-    const uint4 *b16 = (const uint4 *)(gb + m.base_al);
-    const uint4 *q16 = (const uint4 *)(gq + m.base_al);
-    // unconditional loads (indices clamped into the record): a select on the
-    // loaded value would make the compiler wait for it right here
+    const int ndw = (int)(m.w >> 15);
+    // range: the array's last dword read whole (device allocations are padded
+    // to at least 16 bytes, as the 16-byte-aligned staging already assumes)
+    const int64_t left = ((a.nbytes + 3) & ~(int64_t)3) - m.base_al;
+    const int nrec = (int)min(left, (int64_t)0x7FFFFFF0);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void *)(a.gb + m.base_al), (short)0, nrec,
+                                                                        0x00020000);
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void *)(a.gq + m.base_al), (short)0, nrec,
+                                                                        0x00020000);
 #pragma unroll
-    for (int u = 0; u < kStageQ; ++u) {
-        const int d = min(u * kWave + lane, nq - 1);
-        st.vb[u] = b16[d];
-        st.vq[u] = q16[d];
+    for (int u = 0; u < kStageDw; ++u) {
+        if (u * kWave < ndw) {
+            st.vb[u] = __builtin_amdgcn_raw_buffer_load_b32(rb, 4 * lane + 256 * u, 0, 0);
+            st.vq[u] = __builtin_amdgcn_raw_buffer_load_b32(rq, 4 * lane + 256 * u, 0, 0);
+        }
     }
     const int R = (int)(m.w & 127u);
     st.rm = a.rmeta[m.g0 + min(lane, R - 1)];
@@ -1722,23 +1728,21 @@ struct Stamps {
     }
 };
 
-// phase 0: element codes of the prefetched bytes into the stage; returns the
-// lanes' invalid-input flags
+// phase 0: element codes of the prefetched bytes into the stage (dword d of
+// the record's bytes -> four codes at stage + 8 d); returns the lanes'
+// invalid-input flags
 template <bool DUPLEX>
 __device__ __forceinline__ uint32_t stage_codes(const FastArgs &a, const RecMeta &m, const FastStage &st, uint8_t *lds,
                                                 int stage_addr, int lane) {
-    const int nq = ((int)(m.w >> 15) + 3) >> 2;
+    const int ndw = (int)(m.w >> 15);
     uint32_t bad = 0;
 #pragma unroll
-    for (int u = 0; u < kStageQ; ++u) {
-        const int d = u * kWave + lane;
-        if (d < nq) {
-            const uint2 c0 = make_codes4<DUPLEX>(st.vb[u].x, st.vq[u].x, a.kq, a.kqlo, bad);
-            const uint2 c1 = make_codes4<DUPLEX>(st.vb[u].y, st.vq[u].y, a.kq, a.kqlo, bad);
-            const uint2 c2 = make_codes4<DUPLEX>(st.vb[u].z, st.vq[u].z, a.kq, a.kqlo, bad);
-            const uint2 c3 = make_codes4<DUPLEX>(st.vb[u].w, st.vq[u].w, a.kq, a.kqlo, bad);
-            *(uint4 *)(lds + stage_addr + 32 * d) = make_uint4(c0.x, c0.y, c1.x, c1.y);
-            *(uint4 *)(lds + stage_addr + 32 * d + 16) = make_uint4(c2.x, c2.y, c3.x, c3.y);
+    for (int u = 0; u < kStageDw; ++u) {
+        if (u * kWave < ndw) {
+            if (u * kWave + lane < ndw) {
+                const uint2 c = make_codes4<DUPLEX>(st.vb[u], st.vq[u], a.kq, a.kqlo, bad);
+                *(uint2 *)(lds + stage_addr + 8 * (u * kWave + lane)) = c;
+            }
         }
     }
     return bad;
@@ -2047,6 +2051,29 @@ __global__ __launch_bounds__(fk::kBlockThreads) void k_consensus_fast(FastArgs a
         const RecMeta m2 = meta_from_lanes(*(const uint32_t *)(lds + fk::kMv + 32 * wave + 4 * (lane & 7)));   // record i + 2
         const Staged sg = trim_record<DUPLEX>(a, m0, rm, bad, lds, stage_addr, lane);
         sp.mark(4);                    // [3] trim, fence
+        if (DCR_ABL == 6) {            // diagnostic: 128 extra independent VALU per record (issue-rate probe)
+            int d0 = lane, d1 = lane, d2 = lane, d3 = lane;
+#pragma unroll
+            for (int k = 0; k < 32; ++k)
+                asm volatile("v_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\tv_add_u32 %2, %2, 1\n\tv_add_u32 %3, %3, 1"
+                             : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
+            if ((d0 ^ d1 ^ d2 ^ d3) == 12345) a.O.status[0] = 9;
+        }
+        if (DCR_ABL == 7) {            // diagnostic: 128 extra SALU per record
+            int s0 = i, s1 = i;
+#pragma unroll
+            for (int k = 0; k < 64; ++k) asm volatile("s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 3" : "+s"(s0), "+s"(s1));
+            if ((s0 ^ s1) == 12345) a.O.status[0] = 9;
+        }
+        if (DCR_ABL == 8) {            // diagnostic: 32 extra ds_read_b128 of table rows per record
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < 32; ++k) {
+                const double2 f = *(const double2 *)(lds + 16 * ((lane + 7 * k) & 127) + 0x3000 * (k % 5));
+                acc += f.x;
+            }
+            if (acc == 12345.0) a.O.status[0] = 9;
+        }
         if (sg.state == 1) {
             send_to_general<DUPLEX>(a, m0, sg.rm, lds, lane);
         } else if (sg.state == 0) {
