@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -64,6 +65,10 @@ struct dcr_ctx {
     bool timed = false;
     int fast_ok = 0;    // fast_allowed(): the fast kernel may take records
     dcr_params host_params{};
+    // fast-kernel constants (fast_constants)
+    uint32_t fast_kq = 0, fast_kqlo = 0;
+    int fast_maxq = 0, fast_t16 = 0;
+    uint16_t *d_llr16 = nullptr;   // device [128]
     int n_cu = 256;     // compute units (persistent grid size)
     int fast_blocks[2] = {1, 1};   // resident k_consensus_fast blocks per CU (single-strand, duplex)
 };
@@ -78,6 +83,44 @@ static int fast_allowed(const dcr_params *p) {
             return 0;
     return p->error_rate_pre_labeling == 0 && p->error_rate_post_labeling == 0 && p->max_base_quality <= 255 &&
            p->min_base_quality <= 255;
+}
+
+// Host constants of the fast kernel's decision (dcr_kernels.hip, fast kernel v6):
+//   llr16[q] = floor(16 ln(match[q] / mismatch[q]) - 1e-6)  (a lower bound; + 1 an upper one)
+//   t16      = ceil(16 ln(5 / cc)) + 1,  cc = min(qthresh[maxQ], 1 - threshold, 1/4)
+//   fast_qlo = the lowest quality from which every row has match >= mismatch > 0
+// Returns 0 when the decision cannot be made for these parameters (then every
+// record takes the general kernel).
+static int fast_constants(const dcr_params &hp, uint16_t llr16[128], uint32_t &kq, uint32_t &kqlo, int &maxq,
+                          int &t16) {
+    const int mb = std::min(std::max(hp.min_base_quality, 0), 255);
+    kq = (uint32_t)(255 - mb) * 0x01010101u;
+    maxq = hp.max_base_quality;
+    int qlo = 123;
+    while (qlo > 0 && hp.mismatch[qlo - 1] > 0.0 && hp.match[qlo - 1] >= hp.mismatch[qlo - 1]) --qlo;
+    kqlo = (uint32_t)(0x80 - qlo) * 0x01010101u;
+    for (int q = 0; q < 128; ++q) {
+        llr16[q] = 0;
+        if (q >= qlo && q <= 122) {
+            const double v = std::floor(16.0 * std::log(hp.match[q] / hp.mismatch[q]) - 1e-6);
+            if (!(v <= 1040.0)) return 0;                  // 63 rows must fit a 16-bit field
+            llr16[q] = (uint16_t)std::max(v, 0.0);
+        }
+    }
+    const int mq = std::min(std::max(hp.max_base_quality, 0), DCR_MAX_QTHRESH - 1);
+    const double cc = std::min(std::min(hp.qthresh[mq], 1.0 - hp.post_threshold), 0.25);
+    if (!(cc > 1e-12)) return 0;
+    t16 = (int)std::ceil(16.0 * std::log(5.0 / cc)) + 1;
+    return 1;
+}
+
+static int upload_fast(dcr_ctx *c, const dcr_params *params) {
+    uint16_t llr[128];
+    const int ok = fast_constants(*params, llr, c->fast_kq, c->fast_kqlo, c->fast_maxq, c->fast_t16);
+    c->fast_ok = fast_allowed(params) && ok;
+    if (hipMemcpy(c->d_llr16, llr, sizeof(llr), hipMemcpyHostToDevice) != hipSuccess)
+        return fail(DCR_EHIP, "fast-kernel table upload failed");
+    return DCR_OK;
 }
 
 extern "C" {
@@ -112,7 +155,8 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
     c->device = device;
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->d_params, sizeof(dcr_params)) != hipSuccess) {
+        hipMalloc(&c->d_params, sizeof(dcr_params)) != hipSuccess ||
+        hipMalloc(&c->d_llr16, 128 * sizeof(uint16_t)) != hipSuccess) {
         fail(DCR_EHIP, "context allocation failed");
         delete c;
         return nullptr;
@@ -127,9 +171,9 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->fast_blocks[1], dcr::k_consensus_fast<true>, dcr::kFastBlock, 0) !=
             hipSuccess || c->fast_blocks[1] < 1)
         c->fast_blocks[1] = 1;
-    c->fast_ok = fast_allowed(params);
     c->host_params = *params;
-    if (hipMemcpy(c->d_params, params, sizeof(dcr_params), hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMemcpy(c->d_params, params, sizeof(dcr_params), hipMemcpyHostToDevice) != hipSuccess ||
+        upload_fast(c, params) != DCR_OK) {
         fail(DCR_EHIP, "params upload failed");
         dcr_destroy(c);
         return nullptr;
@@ -144,6 +188,7 @@ void dcr_destroy(dcr_ctx *c) {
     c->ws.release();
     c->io.release();
     if (c->d_params) (void)hipFree(c->d_params);
+    if (c->d_llr16) (void)hipFree(c->d_llr16);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -157,9 +202,8 @@ int dcr_set_params(dcr_ctx *c, const dcr_params *params) {
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemcpyAsync(c->d_params, params, sizeof(dcr_params), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    c->fast_ok = fast_allowed(params);
     c->host_params = *params;
-    return DCR_OK;
+    return upload_fast(c, params);
 }
 
 void *dcr_stream(dcr_ctx *c) { return c ? (void *)c->stream : nullptr; }
@@ -223,24 +267,6 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     a.ss = *ss;
     a.ds = *ds;
     a.fast_ok = c->fast_ok;
-    {
-        // fast finalize bound (dcr_kernels.hip, fast kernel v2): a column whose
-        // largest chain b and the rest of S satisfy rest (1 + 1e-9) < b cb has
-        // quality maxQ and is not masked
-        const dcr_params &hp = c->host_params;
-        const int mb = std::min(std::max(hp.min_base_quality, 0), 255);
-        a.fast_kq = (uint32_t)(255 - mb) * 0x01010101u;
-        a.fast_maxq = hp.max_base_quality;
-        const int mq = std::min(std::max(hp.max_base_quality, 0), DCR_MAX_QTHRESH - 1);
-        const double cc = std::min(std::min(hp.qthresh[mq], 1.0 - hp.post_threshold), 0.25);
-        a.fast_ca = 1.0 + 1e-9;
-        a.fast_cb = cc * (1.0 - 1e-9) - 4e-15;
-        // lowest quality from which every row has 1 - p' >= p'/5 (fast kernel v4:
-        // every chain >= U); a kept base below it sends its record to the general kernel
-        int qlo = 123;
-        while (qlo > 0 && hp.match[qlo - 1] >= hp.mismatch[qlo - 1]) --qlo;
-        a.fast_kqlo = (uint32_t)(0x80 - qlo) * 0x01010101u;
-    }
     // per strand: k_recmeta classifies every record (fast list / general list /
     // status written), then the fast kernel (8 records per wave) drains the fast list and
     // the persistent general kernel the rest (insertions, > 64 reads, wide layouts)
@@ -269,11 +295,11 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         f.O = duplex ? *ds : *ss;
         f.P = c->d_params;
         f.stamps = c->w.stamps;
-        f.kq = a.fast_kq;
-        f.kqlo = a.fast_kqlo;
-        f.maxq = a.fast_maxq;
-        f.ca = a.fast_ca;
-        f.cb = a.fast_cb;
+        f.kq = c->fast_kq;
+        f.kqlo = c->fast_kqlo;
+        f.maxq = c->fast_maxq;
+        f.t16 = c->fast_t16;
+        f.llr16 = c->d_llr16;
         return f;
     };
     auto strand = [&](bool duplex) -> int {

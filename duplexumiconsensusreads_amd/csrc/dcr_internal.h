@@ -50,12 +50,6 @@ struct Args {
     dcr_out ds;
     int64_t n_rec;
     int fast_ok;            // fast_allowed() (dcr_capi.hip): the fast kernel may take records
-    // fast-kernel constants (host-computed, dcr_capi.hip: fast_constants)
-    uint32_t fast_kq;       // bytes 255 - min_base_quality: v_lerp_u8 masking test
-    int fast_maxq;          // max_base_quality
-    double fast_ca;         // 1 + 1e-9
-    double fast_cb;         // min(qthresh[maxQ], 1 - threshold, 1/4) (1 - 1e-9) - 4e-15
-    uint32_t fast_kqlo;     // bytes 0x80 - fast_qlo
 };
 
 // the fast kernel's compact arguments (one strand; fewer scalar registers than Args)
@@ -76,7 +70,8 @@ struct FastArgs {
     uint32_t kq;                    // bytes 255 - min_base_quality
     uint32_t kqlo;                  // bytes 0x80 - fast_qlo (lowest quality with 1-p' >= p'/5 upward)
     int maxq;
-    double ca, cb;                  // fast finalize bound
+    int t16;                        // decision margin in 1/16 nat (dcr_capi.hip: fast_constants)
+    const uint16_t *llr16;          // [123] per-quality LLR term, 1/16 nat, rounded down
 };
 
 __global__ void k_prep(dcr_batch in, const dcr_params *P, Workspace ws);

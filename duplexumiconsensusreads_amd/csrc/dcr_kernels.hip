@@ -1468,7 +1468,7 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
     }
 }
 
-// ------------------------------------------------------- fast kernel (v4)
+// ------------------------------------------------------- fast kernel (v6)
 // Records of the dominant shape: every read a single M run (no insertion
 // column, no '-' row), <= 63 reads, bytes fit one LDS stage, T <= 240, every
 // staged quality <= 122, every staged base a valid letter and every kept base's
@@ -1477,42 +1477,39 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
 // CIGAR is one M run over the trimmed span (:797-848 yields M for every such
 // column).
 //
-// Products.  The reference keeps six products per column (:594-600) in the
-// order A T C G + -.  Without '+'/'-' rows the last two are one chain U (p'/5
-// from every read).  A lane keeps the four class chains of its column; the
-// four factors of an element are one 32-byte row of an LDS table indexed by the
-// element's code, so the products need no class compare or select:
-//     LA *= f.a   LT *= f.t   LC *= f.c   LG *= f.g
-// (f.k = 1-p' on a class-k row, p'/5 otherwise; an 'N' row is p'/5 for all).
-// Element codes ARE LDS byte addresses: code = (6k << 11) | 16 (q + k) for class
-// k (N 0, A 1, T 2, C 3, G 4); the half-row (f.a, f.t) is at code, (f.c, f.g)
-// at code + 0x800, and the 16 k shift spreads the classes over LDS banks.
-// code >> 11 = 6k is also the shift of the class's 6-bit counter in a packed
-// count word (R <= 63): cnt += 1 << (code >> 11).
+// The decision, not the products.  The reference keeps six likelihood products
+// per column (:594-600, order A T C G + -; without '+'/'-' rows the last two are
+// the chain U of p'/5 factors).  What the fast path writes depends only on the
+// call b and on whether the reference's finalize gives quality maxQ without
+// masking (:617, :699-709): then the record's fields are b, maxQ, d, e.  So the
+// fast kernel proves that decision instead of forming the products:
+//   L_k / L_b = exp(LLR_k - LLR_b),  U / L_b = exp(-LLR_b),
+//   LLR_k = sum over class-k rows of ln((1-p')/(p'/5))      ('N' rows add 0),
+// and S - L_b <= 5 exp(-gap) L_b with gap = LLR_b - max(LLR_k (k != b), 0).
+// The per-row terms are host-rounded DOWN to 1/16 nat (16-bit fields, exact
+// integer sums), so LLR_b >= L_b / 16 and LLR_k <= (L_k + n_k) / 16; the column
+// is decided when L_b - L_2nd - n_other >= T16 = ceil(16 ln(5 / cc)) + 1 with
+// cc = min(qthresh[maxQ], 1 - threshold, 1/4) -- a margin of 1/16 nat, far
+// beyond every rounding of the reference's double arithmetic.  Any column
+// outside sends its record to the general kernel (the reference's finalize).
 //
-// Finalize without division or phred search.  Every factor 1-p' >= p'/5 for
-// the qualities kept here (>= fast_qlo) and rounding is monotone, so each chain
-// is >= U and m = min(chains) >= U (= U when a class is absent).  With b the
-// largest chain, other = (sum of the four - b) + 2m bounds S - b from above
-// (the subtraction is exact when b dominates: Sterbenz), and the reference's
-// e = 1 - b/S <= (S - b)/b + 7 ulp.  If other (1 + 1e-9) < b cb with
-// cb = min(qthresh[maxQ], 1 - threshold, 1/4)(1 - 1e-9) - 4e-15 the reference's
-// quality is maxQ, its call is b and it is not masked (:699-709, :617).  A
-// record with any column outside the bound goes to the general kernel, which
-// runs the reference's full finalize.
+// Element codes ARE LDS byte addresses of 16-byte table rows: code = (k << 11)
+// | 16 (q + k) for class k (N 0, A 1, T 2, C 3, G 4; the 16 k shift spreads the
+// classes over LDS banks).  Row: u64 LLR increments (16-bit fields A T C G),
+// u32 count increment 1 << 6k (6-bit counters N A T C G, R <= 63).
 //
-// LDS of one 16-wave block (one per CU):
-//   class banks k = 0..4 at 0x3000 k (4 KiB each: two half-row tables)
-//   stages (4 KiB per wave): waves 0-7 in the holes between the banks,
-//   waves 8-15 from 0xD000; e/d table [d][e] (64 x 64 doubles) at 0x15000;
-//   pad sentinel at 0x1D000.
+// LDS of one 16-wave block (one per CU): table (10 KiB), per-wave stages,
+// e/d table [d][e], pad sentinel, pointer cache, per-wave read words, later
+// descriptor and column words.
 namespace fk {
 constexpr int kWaves = kFastWaves;                         // waves per block
 constexpr int kBlockThreads = kFastBlock;
 constexpr int kRowMax = 122;                               // quality rows 0..122
-constexpr uint32_t kPadCode = 16u * 2u;                    // bank N, quality 2 (:509-510, :543-544)
-constexpr int kHalf = 0x800;                               // (f.c, f.g) half-rows
-constexpr int kEtab = 0x15000;                             // e/d [d][e], d, e < 64
+constexpr uint32_t kPadCode = 16u * 2u;                    // class N, quality 2 (:509-510, :543-544)
+constexpr int kNMax = 0x800;                               // codes below: class N
+constexpr int kTable = 5 * 0x800;                          // 5 class banks of 2 KiB
+constexpr int kStage0 = kTable;                            // 4 KiB per wave
+constexpr int kEtab = kStage0 + kWaves * 0x1000;           // e/d [d][e], d, e < 64
 constexpr int kSent = kEtab + 64 * 64 * 8;                 // u16 pad code (out-of-read sentinel)
 constexpr int kPtrs = kSent + 16;                          // u64 [10] record-scalar destinations, [4] rare-path pointers
 constexpr int kRm = kPtrs + 16 * 8;                        // per wave: u64 [64] the current record's read words
@@ -1520,13 +1517,10 @@ constexpr int kMv = kRm + kWaves * kWave * 8;              // per wave: u32 [8] 
 constexpr int kOv = kMv + kWaves * 32;                     // per wave: u16 [256] column words d | e << 6 | call << 12
 constexpr int kLdsBytes = kOv + kWaves * 512;
 static_assert(kStageElems * 2 == 0x1000, "one 4 KiB stage per wave");
-static_assert(16 * (kRowMax + 4) + kHalf <= 0x1000, "a class bank fits 4 KiB");
+static_assert(16 * (kRowMax + 5) <= 0x800, "a class bank fits 2 KiB");
 static_assert(kLdsBytes <= 160 * 1024, "one block per CU");
 
-__device__ __forceinline__ int bank_base(int k) { return 0x3000 * k; }
-__device__ __forceinline__ int stage_base(int wave) {
-    return wave < 8 ? 0x1000 + 0x3000 * (wave >> 1) + 0x1000 * (wave & 1) : 0xD000 + ((wave - 8) << 12);
-}
+__device__ __forceinline__ int stage_base(int wave) { return kStage0 + (wave << 12); }
 }  // namespace fk
 
 constexpr int kStageDw = kStageElems / 4 / kWave;   // staged dwords per lane
@@ -1572,7 +1566,7 @@ __device__ __forceinline__ void fast_load(const FastArgs &a, const RecMeta &m, c
 // the general kernel, which reproduces the exit), as are a quality > 122 and a
 // kept base below fast_qlo.  Single-strand inputs mask qual < min_base_quality
 // to class N keeping the quality (:280): v_lerp_u8 computes (q + 256 - m) >> 1,
-// whose bit 7 is q >= m.  code = (6k << 11) | 16 (q + k) per byte.
+// whose bit 7 is q >= m.  code = (k << 11) | 16 (q + k) per byte.
 template <bool DUPLEX>
 __device__ __forceinline__ uint2 make_codes4(uint32_t B, uint32_t Q, uint32_t kq, uint32_t kqlo, uint32_t &bad) {
     const uint32_t h = (B >> 1) & 0x07070707u;
@@ -1588,30 +1582,29 @@ __device__ __forceinline__ uint2 make_codes4(uint32_t B, uint32_t Q, uint32_t kq
     }
     bad |= x | ((((Q + 0x05050505u) | Q) | lo) & 0x80808080u);
     const uint32_t w = k + Q;                                                     // per byte, <= 126
-    const uint32_t hi = ((w >> 4) & 0x07070707u) | __builtin_amdgcn_perm(0x000000C0u, 0x90603000u, k);   // 48 k
+    const uint32_t hi = ((w >> 4) & 0x07070707u) | (k << 3);
     const uint32_t lw = (w << 4) & 0xF0F0F0F0u;
     return make_uint2(__builtin_amdgcn_perm(hi, lw, 0x05010400u), __builtin_amdgcn_perm(hi, lw, 0x07030602u));
 }
 
 template <int NT>
-struct Chains4 {
-    double L[NT][4];       // A T C G
+struct Evidence {
+    uint64_t llr[NT];      // 16-bit fields A T C G: sums of the class rows' rounded-down LLR terms
     uint32_t cnt[NT];      // 6-bit counters: N A T C G
 };
 
-// Products in read order.  FULL: every read covers every column (the C2
-// shape), so a read's codes are one base address plus immediate offsets;
-// otherwise a column outside the read loads the pad sentinel.  Two reads per
-// step (NT <= 3): the table rows of reads r and r + 1 are in flight together
-// while the codes of r + 2 and r + 3 are read.
+// Evidence sums in read order (integer, so the order is free).  FULL: every
+// read covers every column (the C2 shape), so a read's codes are one base
+// address plus immediate offsets; otherwise a column outside the read loads
+// the pad sentinel.  Two reads per step: the table rows of reads r and r + 1
+// are in flight together while the codes of r + 2 and r + 3 are read.
 template <int NT, bool FULL>
-__device__ __forceinline__ void run_chains4(Chains4<NT> &c, const uint8_t *lds, int R, uint32_t rmx, int crv,
-                                            int lane) {
+__device__ __forceinline__ void run_evidence(Evidence<NT> &ev, const uint8_t *lds, int R, uint32_t rmx, int crv,
+                                             int lane) {
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) c.L[tt][k] = 1.0;
-        c.cnt[tt] = 0;
+        ev.llr[tt] = 0;
+        ev.cnt[tt] = 0;
     }
     auto codes = [&](int r, uint32_t (&cd)[NT]) {
         const int rr = min(r, R - 1);
@@ -1631,55 +1624,40 @@ __device__ __forceinline__ void run_chains4(Chains4<NT> &c, const uint8_t *lds, 
             }
         }
     };
-    auto rows = [&](const uint32_t (&cd)[NT], double2 (&f0)[NT], double2 (&f1)[NT]) {
+    auto rows = [&](const uint32_t (&cd)[NT], uint4 (&f)[NT]) {
 #pragma unroll
-        for (int tt = 0; tt < NT; ++tt) {
-            f0[tt] = *(const double2 *)(lds + cd[tt]);
-            f1[tt] = *(const double2 *)(lds + cd[tt] + fk::kHalf);
-        }
+        for (int tt = 0; tt < NT; ++tt) f[tt] = *(const uint4 *)(lds + cd[tt]);
     };
-    auto mul = [&](const uint32_t (&cd)[NT], const double2 (&f0)[NT], const double2 (&f1)[NT]) {
+    auto add = [&](const uint4 (&f)[NT]) {
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt) {
-            c.cnt[tt] += 1u << (cd[tt] >> 11);
-            c.L[tt][0] *= f0[tt].x;
-            c.L[tt][1] *= f0[tt].y;
-            c.L[tt][2] *= f1[tt].x;
-            c.L[tt][3] *= f1[tt].y;
+            ev.llr[tt] += ((uint64_t)f[tt].y << 32) | f[tt].x;
+            ev.cnt[tt] += f[tt].z;
         }
     };
     uint32_t c0[NT], c1[NT];
     codes(0, c0);
+    codes(1, c1);
     int r = 0;
-    if constexpr (NT <= DCR_PIPE2) {
-        codes(1, c1);
-#pragma unroll 1
-        for (; r + 2 <= R; r += 2) {
-            double2 f0[NT], g0[NT], f1[NT], g1[NT];
-            rows(c0, f0, g0);
-            rows(c1, f1, g1);
-            uint32_t n0[NT], n1[NT];
-            codes(r + 2, n0);
-            codes(r + 3, n1);
-            mul(c0, f0, g0);
-            mul(c1, f1, g1);
+    for (; r + 2 <= R; r += 2) {
+        uint4 f0[NT], f1[NT];
+        rows(c0, f0);
+        rows(c1, f1);
+        uint32_t n0[NT], n1[NT];
+        codes(r + 2, n0);
+        codes(r + 3, n1);
+        add(f0);
+        add(f1);
 #pragma unroll
-            for (int tt = 0; tt < NT; ++tt) {
-                c0[tt] = n0[tt];
-                c1[tt] = n1[tt];
-            }
+        for (int tt = 0; tt < NT; ++tt) {
+            c0[tt] = n0[tt];
+            c1[tt] = n1[tt];
         }
     }
-    // one read per step (NT = 4 keeps its registers for the chains)
-#pragma unroll 1
-    for (; r < R; ++r) {
-        double2 f0[NT], g0[NT];
-        rows(c0, f0, g0);
-        uint32_t n0[NT];
-        codes(r + 1, n0);
-        mul(c0, f0, g0);
-#pragma unroll
-        for (int tt = 0; tt < NT; ++tt) c0[tt] = n0[tt];
+    if (r < R) {
+        uint4 f0[NT];
+        rows(c0, f0);
+        add(f0);
     }
 }
 
@@ -1798,7 +1776,7 @@ __device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &
         while (__ballot(go)) {
             if (go) {
                 const uint32_t code = *(const uint16_t *)(lds + stage_addr + 2 * (y + tl - 1));
-                if (code < (uint32_t)fk::kHalf) --tl; else go = false;
+                if (code < (uint32_t)fk::kNMax) --tl; else go = false;
                 go = go && tl > 0;
             }
         }
@@ -1841,42 +1819,43 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
     }
     const int colr = (int)(rm.x & 255u), lenr = (int)((rm.x >> 8) & 255u);
     const int crv = stage_addr + 2 * ((int)rm.y - colr);
-    Chains4<NT> c;
-    if (__ballot(lane < R && (colr != 0 || lenr < T)) == 0) run_chains4<NT, true>(c, lds, R, rm.x, crv, lane);
-    else run_chains4<NT, false>(c, lds, R, rm.x, crv, lane);
+    Evidence<NT> ev;
+    if (__ballot(lane < R && (colr != 0 || lenr < T)) == 0) run_evidence<NT, true>(ev, lds, R, rm.x, crv, lane);
+    else run_evidence<NT, false>(ev, lds, R, rm.x, crv, lane);
     sp.mark(5);                          // [4] products
     if (DCR_ABL == 2) {                 // diagnostic: staging + products
-        double x = 0.0;
+        uint32_t x = 0;
 #pragma unroll
-        for (int tt = 0; tt < NT; ++tt)
-            x += (c.L[tt][0] + c.L[tt][1]) + (c.L[tt][2] + c.L[tt][3]) + (double)c.cnt[tt];
-        if (lane == 0) O.E[rec] = x;
+        for (int tt = 0; tt < NT; ++tt) x += (uint32_t)ev.llr[tt] ^ (uint32_t)(ev.llr[tt] >> 32) ^ ev.cnt[tt];
+        if (lane == 0) O.pos[rec] = (int)x;
         return;
     }
 
-    // finalize every tile in registers: call, depth d and errors e (:970-1021),
-    // straight-line (selects, no per-tile branches)
+    // decide every tile in registers (integer, straight-line): call, depth d
+    // and errors e (:970-1021) as the column word d | e << 6 | call << 12
     const double *etab = (const double *)(lds + fk::kEtab);
-    uint32_t outside = 0;              // a live column outside the fast bound
+    uint8_t *ov = lds + ov_addr;
+    uint32_t outside = 0;              // a live column not decided
     int dmax = -1, dmin = 0x7fffffff;
-    uint8_t *ov = lds + ov_addr;       // column words d | e << 6 | call << 12
     double ex[NT];                     // e/d of the lane's column (0 outside T)
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
         const int t = 64 * tt + lane;
         const bool live = t < T;
-        const double LA = c.L[tt][0], LT = c.L[tt][1], LC = c.L[tt][2], LG = c.L[tt][3];
-        const double mx = vmax_f64(vmax_f64(LA, LT), vmax_f64(LC, LG));
-        const double mn = vmin_f64(vmin_f64(LA, LT), vmin_f64(LC, LG));
-        const double other = (((LA + LT) + (LC + LG)) - mx) + (mn + mn);
-        outside |= (uint32_t)(!(other * a.ca < mx * a.cb)) & (uint32_t)live;
-        // the call: the first chain equal to the largest ("ATCG")
-        uint32_t kb = LC == mx ? 2u : 3u;
-        kb = LT == mx ? 1u : kb;
-        kb = LA == mx ? 0u : kb;
-        const uint32_t cnt = c.cnt[tt];
+        const uint32_t lo = (uint32_t)ev.llr[tt], hi = (uint32_t)(ev.llr[tt] >> 32);
+        const uint32_t LA = lo & 0xFFFFu, LT = lo >> 16, LC = hi & 0xFFFFu, LG = hi >> 16;
+        const uint32_t m1 = max(LA, LT), n1 = min(LA, LT), m2 = max(LC, LG), n2 = min(LC, LG);
+        const uint32_t Lb = max(m1, m2);
+        const uint32_t L2 = max(min(m1, m2), max(n1, n2));           // the second largest
+        uint32_t kb = LC == Lb ? 2u : 3u;                            // the first largest ("ATCG")
+        kb = LT == Lb ? 1u : kb;
+        kb = LA == Lb ? 0u : kb;
+        const uint32_t cnt = ev.cnt[tt];
         const int d = R - (int)(cnt & 63u);                                       // rows that are not 'N'
-        const int e = R - (int)__builtin_amdgcn_ubfe(cnt, 6u * kb + 6u, 6u);      // rows that differ from the call
+        const int nb = (int)__builtin_amdgcn_ubfe(cnt, 6u * kb + 6u, 6u);
+        const int e = R - nb;                                                     // rows that differ from the call
+        // decided: LLR_b - max(LLR_k, 0) >= (Lb - L2 - (d - nb)) / 16 >= T16 / 16
+        outside |= (uint32_t)((int)Lb - (int)L2 - (d - nb) < a.t16) & (uint32_t)live;
         const double etv = etab[64 * d + e];
         *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (kb << 12));
         ex[tt] = live ? etv : 0.0;
@@ -1983,13 +1962,10 @@ __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
 template <bool DUPLEX>
 __global__ __launch_bounds__(fk::kBlockThreads) void k_consensus_fast(FastArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[fk::kLdsBytes];
-    const dcr_params *P = a.P;
     for (int i = threadIdx.x; i < 5 * (fk::kRowMax + 1); i += fk::kBlockThreads) {
         const int k = i / (fk::kRowMax + 1), q = i % (fk::kRowMax + 1);
-        const double mm = P->mismatch[q], mt = P->match[q];
-        uint8_t *row = lds + fk::bank_base(k) + 16 * (q + k);
-        *(double2 *)row = make_double2(k == 1 ? mt : mm, k == 2 ? mt : mm);
-        *(double2 *)(row + fk::kHalf) = make_double2(k == 3 ? mt : mm, k == 4 ? mt : mm);
+        const uint64_t inc = k == 0 ? 0ull : (uint64_t)a.llr16[q] << (16 * (k - 1));
+        *(uint4 *)(lds + 0x800 * k + 16 * (q + k)) = make_uint4((uint32_t)inc, (uint32_t)(inc >> 32), 1u << (6 * k), 0u);
     }
     for (int i = threadIdx.x; i < 64 * 64; i += fk::kBlockThreads) {
         const int d = i >> 6, e = i & 63;
@@ -2065,14 +2041,14 @@ __global__ __launch_bounds__(fk::kBlockThreads) void k_consensus_fast(FastArgs a
             for (int k = 0; k < 64; ++k) asm volatile("s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 3" : "+s"(s0), "+s"(s1));
             if ((s0 ^ s1) == 12345) a.O.status[0] = 9;
         }
-        if (DCR_ABL == 8) {            // diagnostic: 32 extra ds_read_b128 of table rows per record
-            double acc = 0.0;
+        if (DCR_ABL == 8) {            // diagnostic: 24 extra ds_read_b128 of table rows per record
+            uint4 f[24];
 #pragma unroll
-            for (int k = 0; k < 32; ++k) {
-                const double2 f = *(const double2 *)(lds + 16 * ((lane + 7 * k) & 127) + 0x3000 * (k % 5));
-                acc += f.x;
-            }
-            if (acc == 12345.0) a.O.status[0] = 9;
+            for (int k = 0; k < 24; ++k) f[k] = *(const uint4 *)(lds + 16 * ((lane + 7 * k) & 127) + 0x3000 * (k % 5));
+            uint32_t x = 0;
+#pragma unroll
+            for (int k = 0; k < 24; k += 3) x ^= f[k].x ^ f[k + 1].y ^ f[k + 2].z;
+            if (x == 12345u) a.O.status[0] = 9;
         }
         if (sg.state == 1) {
             send_to_general<DUPLEX>(a, m0, sg.rm, lds, lane);
