@@ -1301,6 +1301,9 @@ __device__ __forceinline__ int opaque(int v) {
     return v;
 }
 
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+
 // IEEE max / min of two doubles known not to be NaN (no canonicalising moves)
 __device__ __forceinline__ double vmax_f64(double x, double y) {
     double r;
@@ -1515,7 +1518,9 @@ constexpr int kPtrs = kSent + 16;                          // u64 [10] record-sc
 constexpr int kRm = kPtrs + 16 * 8;                        // per wave: u64 [64] the current record's read words
 constexpr int kMv = kRm + kWaves * kWave * 8;              // per wave: u32 [8] a later record's descriptor
 constexpr int kOv = kMv + kWaves * 32;                     // per wave: u16 [256] column words d | e << 6 | call << 12
-constexpr int kLdsBytes = kOv + kWaves * 512;
+constexpr int kInvT = kOv + kWaves * 512;                  // f64 [256] 1000 / T
+constexpr int kDivR = kInvT + 256 * 8;                     // u32 [64] ceil(2^24 / R): msum / R = msum * [R] >> 24
+constexpr int kLdsBytes = kDivR + 64 * 4;
 static_assert(kStageElems * 2 == 0x1000, "one 4 KiB stage per wave");
 static_assert(16 * (kRowMax + 5) <= 0x800, "a class bank fits 2 KiB");
 static_assert(kLdsBytes <= 160 * 1024, "one block per CU");
@@ -1841,21 +1846,24 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
         const int t = 64 * tt + lane;
-        const bool live = t < T;
+        const bool live = tt < NT - 1 || t < T;                      // only the last tile is partial
         const uint32_t lo = (uint32_t)ev.llr[tt], hi = (uint32_t)(ev.llr[tt] >> 32);
-        const uint32_t LA = lo & 0xFFFFu, LT = lo >> 16, LC = hi & 0xFFFFu, LG = hi >> 16;
-        const uint32_t m1 = max(LA, LT), n1 = min(LA, LT), m2 = max(LC, LG), n2 = min(LC, LG);
-        const uint32_t Lb = max(m1, m2);
-        const uint32_t L2 = max(min(m1, m2), max(n1, n2));           // the second largest
-        uint32_t kb = LC == Lb ? 2u : 3u;                            // the first largest ("ATCG")
-        kb = LT == Lb ? 1u : kb;
-        kb = LA == Lb ? 0u : kb;
+        // (LA, LC) and (LT, LG) as 16-bit pairs: one packed max / min gives both halves
+        const u16x2 P1 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi, lo, 0x05040100u));
+        const u16x2 P2 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi, lo, 0x07060302u));
+        const u16x2 M = __builtin_elementwise_max(P1, P2), N = __builtin_elementwise_min(P1, P2);
+        const uint32_t Lb = max((uint32_t)M.x, (uint32_t)M.y);
+        const uint32_t L2 = max(min((uint32_t)M.x, (uint32_t)M.y), max((uint32_t)N.x, (uint32_t)N.y));   // second largest
+        uint32_t kb = (uint32_t)P1.y == Lb ? 2u : 3u;                // the first largest ("ATCG")
+        kb = (uint32_t)P2.x == Lb ? 1u : kb;
+        kb = (uint32_t)P1.x == Lb ? 0u : kb;
         const uint32_t cnt = ev.cnt[tt];
         const int d = R - (int)(cnt & 63u);                                       // rows that are not 'N'
         const int nb = (int)__builtin_amdgcn_ubfe(cnt, 6u * kb + 6u, 6u);
         const int e = R - nb;                                                     // rows that differ from the call
         // decided: LLR_b - max(LLR_k, 0) >= (Lb - L2 - (d - nb)) / 16 >= T16 / 16
-        outside |= (uint32_t)((int)Lb - (int)L2 - (d - nb) < a.t16) & (uint32_t)live;
+        const bool undecided = (int)(Lb - L2) - (d - nb) < a.t16;
+        outside |= (uint32_t)(live && undecided);
         const double etv = etab[64 * d + e];
         *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (kb << 12));
         ex[tt] = live ? etv : 0.0;
@@ -1903,7 +1911,7 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
     sum += dpp_f64<0x141>(sum);                  // row_half_mirror
     sum += dpp_f64<0x140>(sum);                  // row_mirror
     sum = (readlane_f64(sum, 0) + readlane_f64(sum, 16)) + (readlane_f64(sum, 32) + readlane_f64(sum, 48));
-    const double y = (sum / (double)T) * 1000.0;
+    const double y = sum * *(const double *)(lds + fk::kInvT + 8 * T);     // mean x 1000, to ~1e-15
     const double fr = y - __builtin_floor(y);
     double E;
     if (__builtin_expect(__builtin_fabs(fr - 0.5) > 1e-9 * (1.0 + y), 1) && DCR_ABL != 4) {
@@ -1924,8 +1932,10 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
     {
         const int E_lo = (int)(uint32_t)__double_as_longlong(E);
         const int E_hi = (int)(uint32_t)((uint64_t)__double_as_longlong(E) >> 32);
+        // MAPQ = msum / R (:874-889, :1377): exact as msum * ceil(2^24 / R) >> 24 for msum < 2^14
+        const int mapq = (int)(((uint64_t)(uint32_t)msum * *(const uint32_t *)(lds + fk::kDivR + 4 * R)) >> 24);
         const int v = lane == 0 ? minpos                       // pos (:790)
-                      : lane == 1 ? msum / R                   // MAPQ (:874-889, :1377)
+                      : lane == 1 ? mapq
                       : lane == 2 ? T                          // len
                       : lane == 3 ? 1                          // n_cig
                       : lane == 4 ? T                          // n_de
@@ -1972,6 +1982,11 @@ __global__ __launch_bounds__(fk::kBlockThreads) void k_consensus_fast(FastArgs a
         ((double *)(lds + fk::kEtab))[i] = d == 0 ? 1.0 : (double)e / (double)d;   // :1010-1012
     }
     if (threadIdx.x == 0) *(uint16_t *)(lds + fk::kSent) = (uint16_t)fk::kPadCode;
+    if (threadIdx.x < 256) {
+        const int t = threadIdx.x;
+        ((double *)(lds + fk::kInvT))[t] = t == 0 ? 0.0 : 1000.0 / (double)t;
+        if (t < 64) ((uint32_t *)(lds + fk::kDivR))[t] = t == 0 ? 0u : ((1u << 24) + (uint32_t)t - 1u) / (uint32_t)t;
+    }
     if (threadIdx.x < 14) {
         const int k = threadIdx.x;
         uint64_t v;

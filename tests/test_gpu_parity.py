@@ -104,3 +104,21 @@ def test_gpu_config2_shape_properties(ctx):
     assert (ds.D <= 2).all() and (ss.D <= 8).all()
     want = dcr_oracle_c.run(packed, params, n_threads=8)
     assert_same(packed, (ss, ds), want)
+
+
+@pytest.mark.parametrize("maxq,minbq,qhi,sub", [(60, 2, 20, 3), (40, 2, 14, 8), (93, 0, 30, 8), (20, 5, 12, 2),
+                                                (60, 13, 41, 8)])
+def test_gpu_fast_decision_borderline(ctx, maxq, minbq, qhi, sub):
+    """Low, mixed qualities put many columns within a few nats of the fast
+    kernel's decision margin (ln(5 / qthresh[maxQ])): the records the fast
+    kernel keeps and those it hands to the general kernel must both match the
+    oracle bit for bit."""
+    packed = synth.packed_fixed_size(400, sub_size=sub, read_len=150, seed=maxq + qhi)
+    rng = np.random.default_rng(maxq * 7 + qhi)
+    q = packed.quals
+    q[:] = rng.integers(max(minbq - 1, 0), qhi + 1, q.shape, dtype=np.uint8)
+    params = ConsensusParams(max_base_quality=maxq, min_base_quality=minbq)
+    ctx.set_params(params)
+    got = ctx.run_host(packed)
+    want = dcr_oracle_c.run(packed, params, n_threads=8)
+    assert_same(packed, got, want)
