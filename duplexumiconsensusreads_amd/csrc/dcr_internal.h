@@ -11,7 +11,7 @@ namespace dcr {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
-constexpr int kFastWaves = 16;              // k_consensus_fast: one 16-wave block per CU
+constexpr int kFastWaves = 4;               // k_consensus_fast: five 4-wave blocks per CU (5 waves per SIMD)
 constexpr int kFastBlock = kWave * kFastWaves;
 
 // Per-record launch metadata written by k_recmeta for the fast kernel, in

@@ -1512,18 +1512,17 @@ constexpr uint32_t kPadCode = 16u * 2u;                    // class N, quality 2
 constexpr int kNMax = 0x800;                               // codes below: class N
 constexpr int kTable = 5 * 0x800;                          // 5 class banks of 2 KiB
 constexpr int kStage0 = kTable;                            // 4 KiB per wave
-constexpr int kEtab = kStage0 + kWaves * 0x1000;           // e/d [d][e], d, e < 64
-constexpr int kSent = kEtab + 64 * 64 * 8;                 // u16 pad code (out-of-read sentinel)
+constexpr int kInvD = kStage0 + kWaves * 0x1000;           // f64 [64] 1 / d
+constexpr int kSent = kInvD + 64 * 8;                      // u16 pad code (out-of-read sentinel)
 constexpr int kPtrs = kSent + 16;                          // u64 [10] record-scalar destinations, [4] rare-path pointers
 constexpr int kRm = kPtrs + 16 * 8;                        // per wave: u64 [64] the current record's read words
 constexpr int kMv = kRm + kWaves * kWave * 8;              // per wave: u32 [8] a later record's descriptor
 constexpr int kOv = kMv + kWaves * 32;                     // per wave: u16 [256] column words d | e << 6 | call << 12
-constexpr int kInvT = kOv + kWaves * 512;                  // f64 [256] 1000 / T
-constexpr int kDivR = kInvT + 256 * 8;                     // u32 [64] ceil(2^24 / R): msum / R = msum * [R] >> 24
+constexpr int kDivR = kOv + kWaves * 512;                  // u32 [64] ceil(2^24 / R): msum / R = msum * [R] >> 24
 constexpr int kLdsBytes = kDivR + 64 * 4;
 static_assert(kStageElems * 2 == 0x1000, "one 4 KiB stage per wave");
 static_assert(16 * (kRowMax + 5) <= 0x800, "a class bank fits 2 KiB");
-static_assert(kLdsBytes <= 160 * 1024, "one block per CU");
+static_assert(5 * kLdsBytes <= 160 * 1024, "five blocks (20 waves) per CU");
 
 __device__ __forceinline__ int stage_base(int wave) { return kStage0 + (wave << 12); }
 }  // namespace fk
@@ -1642,8 +1641,9 @@ __device__ __forceinline__ void run_evidence(Evidence<NT> &ev, const uint8_t *ld
     };
     uint32_t c0[NT], c1[NT];
     codes(0, c0);
-    codes(1, c1);
     int r = 0;
+    if constexpr (NT <= 3) {
+    codes(1, c1);
     for (; r + 2 <= R; r += 2) {
         uint4 f0[NT], f1[NT];
         rows(c0, f0);
@@ -1659,10 +1659,16 @@ __device__ __forceinline__ void run_evidence(Evidence<NT> &ev, const uint8_t *ld
             c1[tt] = n1[tt];
         }
     }
-    if (r < R) {
+    }
+    // one read per step (NT = 4 keeps fewer rows in flight)
+    for (; r < R; ++r) {
         uint4 f0[NT];
         rows(c0, f0);
+        uint32_t n0[NT];
+        if (r + 1 < R) codes(r + 1, n0);
         add(f0);
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) c0[tt] = n0[tt];
     }
 }
 
@@ -1838,7 +1844,7 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
 
     // decide every tile in registers (integer, straight-line): call, depth d
     // and errors e (:970-1021) as the column word d | e << 6 | call << 12
-    const double *etab = (const double *)(lds + fk::kEtab);
+    const double *invd = (const double *)(lds + fk::kInvD);
     uint8_t *ov = lds + ov_addr;
     uint32_t outside = 0;              // a live column not decided
     int dmax = -1, dmin = 0x7fffffff;
@@ -1864,7 +1870,8 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
         // decided: LLR_b - max(LLR_k, 0) >= (Lb - L2 - (d - nb)) / 16 >= T16 / 16
         const bool undecided = (int)(Lb - L2) - (d - nb) < a.t16;
         outside |= (uint32_t)(live && undecided);
-        const double etv = etab[64 * d + e];
+        const double etv = (double)e * invd[d];                      // e/d to 1 ulp (the mean's decision
+                                                                     // tolerates 1e-9; the exact walk divides)
         *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (kb << 12));
         ex[tt] = live ? etv : 0.0;
         dmax = max(dmax, live ? d : -1);
@@ -1911,7 +1918,9 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
     sum += dpp_f64<0x141>(sum);                  // row_half_mirror
     sum += dpp_f64<0x140>(sum);                  // row_mirror
     sum = (readlane_f64(sum, 0) + readlane_f64(sum, 16)) + (readlane_f64(sum, 32) + readlane_f64(sum, 48));
-    const double y = sum * *(const double *)(lds + fk::kInvT + 8 * T);     // mean x 1000, to ~1e-15
+    double rt = __builtin_amdgcn_rcp((double)T);                             // 1 / T, then one Newton step
+    rt = __builtin_fma(__builtin_fma(-(double)T, rt, 1.0), rt, rt);
+    const double y = (sum * rt) * 1000.0;                                    // mean x 1000, to ~1e-15
     const double fr = y - __builtin_floor(y);
     double E;
     if (__builtin_expect(__builtin_fabs(fr - 0.5) > 1e-9 * (1.0 + y), 1) && DCR_ABL != 4) {
@@ -1919,9 +1928,15 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
     } else {
         double *et = (double *)(lds + stage_addr);
         const int ln = lane;
+        const uint8_t *ovr = lds + ov_addr;
 #pragma unroll
-        for (int tt = 0; tt < NT; ++tt)
-            if (64 * tt + ln < T) et[64 * tt + ln] = ex[tt];
+        for (int tt = 0; tt < NT; ++tt) {
+            const int t = 64 * tt + ln;
+            if (t < T) {
+                const uint32_t w = *(const uint16_t *)(ovr + 2 * t);
+                et[t] = (double)((w >> 6) & 63u) / (double)(w & 63u);   // e / d exactly (:1010-1012; d >= 1)
+            }
+        }
         lds_fence();
         const double total = 0.0 + pairwise_et(et, T, ln);
         E = __builtin_rint((total / (double)T) * 1000.0) / 1000.0;
@@ -1970,22 +1985,18 @@ __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
 // descriptor of record i + 2 is fetched by a vector load (vmcnt, not lgkmcnt,
 // so LDS waits never drain it).
 template <bool DUPLEX>
-__global__ __launch_bounds__(fk::kBlockThreads) void k_consensus_fast(FastArgs a) {
+__global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[fk::kLdsBytes];
     for (int i = threadIdx.x; i < 5 * (fk::kRowMax + 1); i += fk::kBlockThreads) {
         const int k = i / (fk::kRowMax + 1), q = i % (fk::kRowMax + 1);
         const uint64_t inc = k == 0 ? 0ull : (uint64_t)a.llr16[q] << (16 * (k - 1));
         *(uint4 *)(lds + 0x800 * k + 16 * (q + k)) = make_uint4((uint32_t)inc, (uint32_t)(inc >> 32), 1u << (6 * k), 0u);
     }
-    for (int i = threadIdx.x; i < 64 * 64; i += fk::kBlockThreads) {
-        const int d = i >> 6, e = i & 63;
-        ((double *)(lds + fk::kEtab))[i] = d == 0 ? 1.0 : (double)e / (double)d;   // :1010-1012
-    }
+    if (threadIdx.x < 64) ((double *)(lds + fk::kInvD))[threadIdx.x] = threadIdx.x == 0 ? 0.0 : 1.0 / (double)threadIdx.x;
     if (threadIdx.x == 0) *(uint16_t *)(lds + fk::kSent) = (uint16_t)fk::kPadCode;
-    if (threadIdx.x < 256) {
+    if (threadIdx.x < 64) {
         const int t = threadIdx.x;
-        ((double *)(lds + fk::kInvT))[t] = t == 0 ? 0.0 : 1000.0 / (double)t;
-        if (t < 64) ((uint32_t *)(lds + fk::kDivR))[t] = t == 0 ? 0u : ((1u << 24) + (uint32_t)t - 1u) / (uint32_t)t;
+        ((uint32_t *)(lds + fk::kDivR))[t] = t == 0 ? 0u : ((1u << 24) + (uint32_t)t - 1u) / (uint32_t)t;
     }
     if (threadIdx.x < 14) {
         const int k = threadIdx.x;
