@@ -17,7 +17,8 @@ constexpr int kFastBlock = kWave * kFastWaves;
 // Per-record launch metadata written by k_recmeta for the fast kernel, in
 // fast-list order (one scalar 32-byte load per record).
 struct RecMeta {
-    int64_t base_al;    // 4-aligned byte offset of the record's kept bases/quals
+    uint32_t base_al;   // 16-aligned byte offset of the record's kept bases/quals (< 2^32 - 4096)
+    int32_t d0;         // pos of the record's first read - min_pos
     int64_t off;        // output column offset (ss_col_off / ds_col_off)
     int32_t rec;        // record index
     int32_t g0;         // index of its first read in the read-meta array
@@ -39,7 +40,8 @@ struct Workspace {
     int *fast_count;        // [2] single-strand / duplex fast-list lengths
     unsigned long long *stamps;   // [32] diagnostic phase cycles (DCR_STAMP builds only)
     RecMeta *meta;          // [n_rec] fast list
-    uint2 *rmeta;           // [max(n_reads, 4F)] per read: col | len << 8 | mapq << 16, stage offset
+    uint2 *rmeta;           // [max(n_reads, 4F)] per read: len | mapq << 8 | (pos - pos of the record's
+                            // first read) << 16 (int16), seq_start (low 32 bits)
 };
 
 struct Args {

@@ -1334,12 +1334,15 @@ __device__ __forceinline__ int wave_scan_max(int v) {
 }
 
 // record (wave lane) owning read c + lane; records are contiguous runs of reads
-__device__ __forceinline__ int read_record(int64_t c, int g0, int R, int *mark, int lane, int &carry) {
+__device__ __forceinline__ int read_record(int64_t c, int g0, int R, int *mark, int lane, int &carry,
+                                           bool *starts = nullptr) {
     mark[lane] = -1;
     lds_fence();
     if (R > 0 && g0 >= c && g0 < c + kWave) atomicMax(&mark[g0 - c], lane);
     lds_fence();
-    const int k = max(wave_scan_max(mark[lane]), carry);
+    const int mk = mark[lane];
+    if (starts) *starts = mk >= 0;
+    const int k = max(wave_scan_max(mk), carry);
     carry = readlane(k, 63);
     return k;
 }
@@ -1347,6 +1350,7 @@ __device__ __forceinline__ int read_record(int64_t c, int g0, int R, int *mark, 
 struct RecAgg {
     int minpos, maxend, flags, kind;
     unsigned long long lo, hi;     // kept byte window; lo becomes base_al for fast records
+    int pos0, pad;                 // pos of the record's first read
 };
 
 template <bool DUPLEX>
@@ -1377,22 +1381,36 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
         gbeg = 2 * rb;
         gend = 2 * rend;
     }
-    agg[lane] = RecAgg{0x7fffffff, -0x7fffffff, 0, -1, ~0ull, 0ull};
+    agg[lane] = RecAgg{0x7fffffff, -0x7fffffff, 0, -1, ~0ull, 0ull, 0, 0};
     lds_fence();
-    // pass 1: fold every read into its record
+    // one pass: fold every read into its record, and write the read's word for
+    // the fast kernel (relative to the record's first read, so it needs no
+    // record-level result); a read whose offset from the first read does not fit
+    // 16 bits sends its record to the general kernel (flag 4)
     int carry = -1;
     for (int64_t c = gbeg; c < gend; c += kWave) {
-        const int k = read_record(c, g0, R, mark, lane, carry);
+        bool starts;
+        const int k = read_record(c, g0, R, mark, lane, carry, &starts);
         const int64_t gr = c + lane;
+        RdLite rd{};
         if (gr < gend) {
-            const RdLite rd = rd_lite<DUPLEX, true>(a, gr);
+            rd = rd_lite<DUPLEX, true>(a, gr);
+            if (starts) agg[k].pos0 = rd.pos;
+        }
+        lds_fence();
+        if (gr < gend) {
+            const int dpos = rd.pos - agg[k].pos0;
             const int fl = (rd.status != 0) | ((rd.len <= 0) << 1) |
-                           ((rd.ncig != 1 || (DUPLEX && rd.len > 0 && (rd.cig0 & 15u) != 0)) << 2);   // single M run only
+                           ((rd.ncig != 1 || (DUPLEX && rd.len > 0 && (rd.cig0 & 15u) != 0) || dpos < -32768 ||
+                             dpos > 32767) << 2);   // single M run only
             atomicMin(&agg[k].minpos, rd.pos);
             atomicMax(&agg[k].maxend, rd.pos + rd.len);
             if (fl) atomicOr(&agg[k].flags, fl);
             atomicMin(&agg[k].lo, (unsigned long long)rd.seq_start);
             atomicMax(&agg[k].hi, (unsigned long long)(rd.seq_start + rd.len));
+            a.ws.rmeta[gr] = make_uint2(((uint32_t)rd.len & 255u) | (((uint32_t)rd.mapq & 255u) << 8) |
+                                            ((uint32_t)dpos << 16),
+                                        (uint32_t)rd.seq_start);
         }
     }
     lds_fence();
@@ -1418,11 +1436,12 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
             const int64_t span = (int64_t)g.hi - base_al;
             const bool aligned = ((((uintptr_t)gb) | ((uintptr_t)gq)) & 15) == 0;
             if ((g.flags & 4) || !aligned || R > kFastMaxR || span > kStageElems || T > kFastMaxT || T > cap ||
-                !a.fast_ok) {
+                !a.fast_ok || base_al + span >= 0xFFFFF000ll) {
                 kind = 1;
             } else {
                 kind = 0;
-                m.base_al = base_al;
+                m.base_al = (uint32_t)base_al;
+                m.d0 = g.pos0 - g.minpos;
                 m.off = off;
                 m.rec = (int32_t)rk;
                 m.g0 = g0;
@@ -1448,26 +1467,13 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
     if (kind == 1) a.ws.ovf[baseg + __popcll(bg & lt)] = (int)rk;
     // single-strand reads of records the fast kernel does not take need the full
     // preprocessing (3' trim included) for the general kernel and the host
-    const bool prep = !DUPLEX && __ballot(vk && kind != 0) != 0;
-    if (!bf && !prep) return;
+    if (DUPLEX || __ballot(vk && kind != 0) == 0) return;
     lds_fence();
-    // pass 2: per-read metadata of fast records, preprocessing of the others
     carry = -1;
     for (int64_t c = gbeg; c < gend; c += kWave) {
         const int k = read_record(c, g0, R, mark, lane, carry);
         const int64_t gr = c + lane;
-        if (gr < gend) {
-            if (agg[k].kind == 0) {
-                const RdLite rd = rd_lite<DUPLEX, false>(a, gr);
-                const int minpos = agg[k].minpos;
-                const int64_t base_al = (int64_t)agg[k].lo;
-                a.ws.rmeta[gr] = make_uint2((uint32_t)(rd.pos - minpos) | ((uint32_t)rd.len << 8) |
-                                                ((uint32_t)rd.mapq << 16),
-                                            (uint32_t)(rd.seq_start - base_al));
-            } else if (!DUPLEX) {
-                prep_read(a.in, a.P, a.ws, gr);
-            }
-        }
+        if (gr < gend && agg[k].kind != 0) prep_read(a.in, a.P, a.ws, gr);
     }
 }
 
@@ -1969,7 +1975,8 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
 
 __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
     RecMeta m;
-    m.base_al = (int64_t)(((uint64_t)(uint32_t)readlane((int)v, 1) << 32) | (uint32_t)readlane((int)v, 0));
+    m.base_al = (uint32_t)readlane((int)v, 0);
+    m.d0 = readlane((int)v, 1);
     m.off = (int64_t)(((uint64_t)(uint32_t)readlane((int)v, 3) << 32) | (uint32_t)readlane((int)v, 2));
     m.rec = readlane((int)v, 4);
     m.g0 = readlane((int)v, 5);
@@ -2049,7 +2056,10 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
         fast_load<DUPLEX>(a, m1, ML + min(i + 3, ilast), lane, st);
         sp.mark(3);                    // [2] prefetch issue
         lds_fence();
-        const uint2 rm = *(const uint2 *)(lds + rm_addr + 8 * lane);
+        const uint2 rw = *(const uint2 *)(lds + rm_addr + 8 * lane);
+        // the read's word relative to this record: col | len << 8 | mapq << 16, stage offset
+        const uint2 rm = make_uint2((uint32_t)(((int)rw.x >> 16) + m0.d0) | (rw.x & 0xFFFFu) << 8,
+                                    rw.y - m0.base_al);
         const RecMeta m2 = meta_from_lanes(*(const uint32_t *)(lds + fk::kMv + 32 * wave + 4 * (lane & 7)));   // record i + 2
         const Staged sg = trim_record<DUPLEX>(a, m0, rm, bad, lds, stage_addr, lane);
         sp.mark(4);                    // [3] trim, fence
