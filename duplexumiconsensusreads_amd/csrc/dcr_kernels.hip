@@ -1168,10 +1168,11 @@ __device__ __forceinline__ double pairwise_small(const double *a, int n, int lan
 // 64-bit DPP move (two 32-bit halves)
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
+    // full-row permutations: every lane reads a valid source, so no "old" value
     const int2 h = __builtin_bit_cast(int2, v);
     int2 r;
-    r.x = __builtin_amdgcn_update_dpp(0, h.x, CTRL, 0xF, 0xF, false);
-    r.y = __builtin_amdgcn_update_dpp(0, h.y, CTRL, 0xF, 0xF, false);
+    r.x = __builtin_amdgcn_mov_dpp(h.x, CTRL, 0xF, 0xF, true);
+    r.y = __builtin_amdgcn_mov_dpp(h.y, CTRL, 0xF, 0xF, true);
     return __builtin_bit_cast(double, r);
 }
 
@@ -1821,7 +1822,8 @@ __device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &
 // products, finalize, outputs of a staged record of T <= 64 NT columns
 template <bool DUPLEX, int NT>
 __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &m, const Staged &sg, uint8_t *lds,
-                                              const int stage_addr, const int ov_addr, const int lane, Stamps &sp) {
+                                              const int stage_addr, const int ov_addr, const int rm_addr, const int lane,
+                                              Stamps &sp) {
     const dcr_out &O = a.O;
     const int64_t rec = m.rec;
     const int64_t off = m.off;
@@ -1955,16 +1957,16 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
         const int E_hi = (int)(uint32_t)((uint64_t)__double_as_longlong(E) >> 32);
         // MAPQ = msum / R (:874-889, :1377): exact as msum * ceil(2^24 / R) >> 24 for msum < 2^14
         const int mapq = (int)(((uint64_t)(uint32_t)msum * *(const uint32_t *)(lds + fk::kDivR + 4 * R)) >> 24);
-        const int v = lane == 0 ? minpos                       // pos (:790)
-                      : lane == 1 ? mapq
-                      : lane == 2 ? T                          // len
-                      : lane == 3 ? 1                          // n_cig
-                      : lane == 4 ? T                          // n_de
-                      : lane == 5 ? Dmax
-                      : lane == 6 ? Dmin
-                      : lane == 7 ? E_lo
-                      : lane == 8 ? E_hi
-                                  : (int)((uint32_t)T << 4);   // one M run of T
+        // lane k takes field k through the wave's (now free) read-word LDS:
+        // pos (:790), MAPQ, len, n_cig, n_de, D, M, E (two words), one M run of T
+        uint8_t *sc = lds + rm_addr;
+        if (lane == 0) {
+            *(int4 *)sc = make_int4(minpos, mapq, T, 1);
+            *(int4 *)(sc + 16) = make_int4(T, Dmax, Dmin, E_lo);
+            *(int2 *)(sc + 32) = make_int2(E_hi, (int)((uint32_t)T << 4));
+        }
+        lds_fence();
+        const int v = *(const int *)(sc + 4 * min(lane, 9));
         const uint64_t dst = *(const uint64_t *)(lds + fk::kPtrs + 8 * min(lane, 9));
         uint8_t *p = (uint8_t *)(uintptr_t)(dst & 0x00FFFFFFFFFFFFFFull);
         if (lane < 10) *(int *)(p + rec * (int64_t)((dst >> 56) & 15u) + off * (int64_t)(dst >> 60)) = v;
@@ -2089,10 +2091,10 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
         if (sg.state == 1) {
             send_to_general<DUPLEX>(a, m0, sg.rm, lds, lane);
         } else if (sg.state == 0) {
-            if (sg.T <= 64) finish_record<DUPLEX, 1>(a, m0, sg, lds, stage_addr, ov_addr, lane, sp);
-            else if (sg.T <= 128) finish_record<DUPLEX, 2>(a, m0, sg, lds, stage_addr, ov_addr, lane, sp);
-            else if (sg.T <= 192) finish_record<DUPLEX, 3>(a, m0, sg, lds, stage_addr, ov_addr, lane, sp);
-            else finish_record<DUPLEX, 4>(a, m0, sg, lds, stage_addr, ov_addr, lane, sp);
+            if (sg.T <= 64) finish_record<DUPLEX, 1>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
+            else if (sg.T <= 128) finish_record<DUPLEX, 2>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
+            else if (sg.T <= 192) finish_record<DUPLEX, 3>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
+            else finish_record<DUPLEX, 4>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
         }
         if (++i >= iend) break;
         m0 = m1;
