@@ -1280,6 +1280,70 @@ __device__ __forceinline__ RdLite rd_lite(const Args &a, int64_t k) {
     return r;
 }
 
+// rd_lite in two halves so that a wave keeps several 64-read chunks' loads in
+// flight: the independent per-read fields first, then the one dependent load
+// (the first CIGAR word); reads whose CIGAR is not one M/=/X run take the full
+// clip_view (rare)
+struct RdRaw {
+    int64_t seq_off;
+    int seq_len, pos, mapq, n, status;
+    int32_t cig_off;
+    uint32_t cig0;
+};
+
+template <bool DUPLEX>
+__device__ __forceinline__ void rd_raw_load(const Args &a, int64_t k, RdRaw &w) {
+    if (!DUPLEX) {
+        w.cig_off = a.in.cig_off[k];
+        w.n = a.in.cig_n[k];
+        w.seq_off = a.in.seq_off[k];
+        w.seq_len = a.in.seq_len[k];
+        w.pos = a.in.read_pos[k];
+        w.mapq = a.in.read_mapq[k];
+    } else {
+        w.pos = a.ss.pos[k];
+        w.seq_len = a.ss.len[k];
+        w.n = a.ss.n_cig[k];
+        w.status = a.ss.status[k];
+        w.mapq = a.ss.mapq[k];
+        w.seq_off = a.in.ss_col_off[k];
+    }
+}
+
+template <bool DUPLEX>
+__device__ __forceinline__ void rd_raw_cig(const Args &a, RdRaw &w) {
+    if (!DUPLEX) w.cig0 = w.n >= 1 ? a.in.cigar[w.cig_off] : 0u;
+    else w.cig0 = (w.status == 0 && w.n == 1 && w.seq_len > 0) ? a.ss.cigar[w.seq_off] : 0u;
+}
+
+template <bool DUPLEX>
+__device__ __forceinline__ RdLite rd_raw_finish(const Args &a, int64_t k, const RdRaw &w) {
+    RdLite r;
+    if (!DUPLEX) {
+        const uint32_t op = w.cig0 & 15u;
+        if (w.n == 1 && (op == 0 || op == 7 || op == 8)) {   // one M/=/X run: no clip (clip_view's fast case)
+            r.pos = w.pos;
+            r.len = w.seq_len;
+            r.ncig = (int)(w.cig0 >> 4) == w.seq_len ? 1 : 2;
+            r.status = w.seq_len <= 0 ? DCR_ST_TYPE_ERROR : 0;
+            r.mapq = w.mapq;
+            r.seq_start = w.seq_off;
+            r.cig0 = 0;
+        } else {
+            r = rd_lite<false, true>(a, k);
+        }
+    } else {
+        r.pos = w.pos;
+        r.len = w.seq_len;
+        r.ncig = w.n;
+        r.status = w.status;
+        r.mapq = w.mapq;
+        r.seq_start = w.seq_off;
+        r.cig0 = w.cig0;
+    }
+    return r;
+}
+
 __device__ __forceinline__ void write_status_at(const dcr_out &O, int64_t rec, int st) {
     O.status[rec] = (uint8_t)st;
     O.pos[rec] = 0;
@@ -1389,13 +1453,29 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
     // record-level result); a read whose offset from the first read does not fit
     // 16 bits sends its record to the general kernel (flag 4)
     int carry = -1;
-    for (int64_t c = gbeg; c < gend; c += kWave) {
+    constexpr int kBatch = 4;                     // 64-read chunks with their loads in flight together
+    for (int64_t cb = gbeg; cb < gend; cb += kBatch * kWave) {
+    RdRaw raw[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+        const int64_t gr = cb + j * kWave + lane;
+        if (gr < gend) rd_raw_load<DUPLEX>(a, gr, raw[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+        const int64_t gr = cb + j * kWave + lane;
+        if (gr < gend) rd_raw_cig<DUPLEX>(a, raw[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+        const int64_t c = cb + j * kWave;
+        if (c >= gend) break;
         bool starts;
         const int k = read_record(c, g0, R, mark, lane, carry, &starts);
         const int64_t gr = c + lane;
         RdLite rd{};
         if (gr < gend) {
-            rd = rd_lite<DUPLEX, true>(a, gr);
+            rd = rd_raw_finish<DUPLEX>(a, gr, raw[j]);
             if (starts) agg[k].pos0 = rd.pos;
         }
         lds_fence();
@@ -1413,6 +1493,7 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
                                             ((uint32_t)dpos << 16),
                                         (uint32_t)rd.seq_start);
         }
+    }
     }
     lds_fence();
     // per record: lane = record
