@@ -144,12 +144,9 @@ def main():
         tdist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        b = torch.tensor([bases, n_bad], dtype=torch.int64, device=dev)
-        tdist.all_reduce(b, op=tdist.ReduceOp.SUM)
-        total_bases, n_bad = int(b[0].item()), int(b[1].item())
+        from duplexumiconsensusreads_amd import shard
+        elapsed = shard.max_over_ranks(elapsed, device=dev)
+        total_bases, n_bad = shard.sum_over_ranks([bases, n_bad], device=dev)
     else:
         total_bases = bases
 

@@ -1,0 +1,76 @@
+"""End to end: the CLI drop-in (``cli.main``, mirroring the reference's
+``main`` DuplexUMIConsensusReads.py:1426-1650) on the committed small C1 BAM
+against the reference's own outputs for the same file and seed
+(tests/golden/e2e_c1_small.*, made by tests/golden/make_golden.py): the
+consensus BAM, both side BAMs and the summary lines, record for record.
+
+The CPU case runs the batch backend on the C oracle (test infrastructure); the
+GPU case runs the HIP library through its C-ABI."""
+import contextlib
+import io
+import os
+import random
+
+import pytest
+
+from duplexumiconsensusreads_amd import bam, cli
+from oracle import dcr_oracle_c
+from tests.golden_io import GOLDEN, load_e2e
+
+E2E = load_e2e()
+INPUT = os.path.join(GOLDEN, "e2e_c1_small.bam")
+
+
+def run_cli(tmp_path, backend, extra=()):
+    out = str(tmp_path / "cons.bam")
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        rc = cli.main(["-i", INPUT, "-o", out, *extra], backend=backend, rng=random.Random(E2E["random_seed"]))
+    assert rc == 0
+    res = {"stdout": buf.getvalue()}
+    for key, path in (("consensus", out), ("filteredreads", out[:-4] + "_filteredreads.bam"),
+                      ("filteredfamilies", out[:-4] + "_filteredfamilies.bam")):
+        with bam.AlignmentFile(path, "rb") as f:
+            res[key] = [r.to_dict() for r in f]
+    return res
+
+
+def assert_matches_reference(res):
+    assert res["stdout"] == E2E["stdout"]
+    for key in ("consensus", "filteredreads", "filteredfamilies"):
+        got, want = res[key], E2E[key]
+        assert len(got) == len(want), key
+        for i, (g, w) in enumerate(zip(got, want)):
+            assert g == w, (key, i, {k: (g.get(k), w.get(k)) for k in w if g.get(k) != w.get(k)})
+
+
+@pytest.mark.parametrize("batch", ["65536", "7"])
+def test_cli_matches_reference_main_oracle_backend(tmp_path, batch):
+    # batch size must not change any output (7: several device calls per file)
+    res = run_cli(tmp_path, dcr_oracle_c.run, ("--batch_families", batch))
+    assert_matches_reference(res)
+
+
+def test_cli_flags_are_the_reference_flags():
+    a = cli.parse_args(["-i", "x.bam"])
+    assert (a.min_map_quality, a.min_base_quality, a.min_reads, a.max_reads, a.max_base_quality,
+            a.base_quality_shift, a.error_rate_post_labeling, a.error_rate_pre_labeling, a.deletion_score,
+            a.no_insertion_score, a.output_file, a.verbose) == (20, 20, 1, 100, 60, 0, 0, 0, 30, 30, None, False)
+
+
+def test_cli_rejects_non_bam_output(tmp_path, capsys):
+    with pytest.raises(SystemExit):
+        cli.main(["-i", INPUT, "-o", str(tmp_path / "x.sam")], backend=dcr_oracle_c.run)
+    assert "ERROR: output file is not specified" in capsys.readouterr().out
+
+
+@pytest.mark.gpu
+def test_cli_matches_reference_main_gpu(tmp_path):
+    from duplexumiconsensusreads_amd import _lib
+    from duplexumiconsensusreads_amd.params import ConsensusParams
+    ctx = _lib.Context(ConsensusParams(), device=0)
+    try:
+        res = run_cli(tmp_path, _lib.backend(ctx))
+    finally:
+        ctx.close()
+    assert_matches_reference(res)
