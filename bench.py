@@ -34,6 +34,31 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 METRIC = "consensus bases/sec (whole node) + SSCS kernel HBM GB/s vs peak, 1/2/4/8 GPUs"
 
 
+# families per GPU for each workload shape (weak scaling: every rank its own shard)
+CONFIG_FAMILIES = {
+    "C2": 312_500,     # 10 M reads: 4 subfamilies x 8 reads
+    "C3": 400_000,     # ~12.5 M reads = C3's 100 M reads / 8 GPUs; Zipf(1.5) 1..100, 5% indels, 3% clips
+    "C4": 1_000,       # 20 loci x 50 families, subfamilies log-uniform 100..1000 (--max_reads 1000)
+    "C5": 200_000,     # one 4 M-read streaming chunk of the 1 B-read run: Poisson(4)+1
+}
+WORKLOAD = {
+    "C2": "C2 (BASELINE.json configs[1]): 10M-read synthetic duplex batch per GPU, 312,500 MI families x "
+          "4 subfamilies x 8 reads, 2x150bp, no indels",
+    "C3": "C3 shape (BASELINE.json configs[2]) per GPU: skewed subfamilies Zipf(1.5) on 1..100, 5% of reads with "
+          "a 1-3 bp indel, 3% soft-clipped, 2x150bp",
+    "C4": "C4 shape (BASELINE.json configs[3]): 20 loci x 50 families, subfamilies log-uniform 100..1000 reads "
+          "(--max_reads 1000), 2x150bp",
+    "C5": "C5 shape (BASELINE.json configs[4]): one 4M-read chunk, subfamilies Poisson(4)+1, 2x150bp",
+}
+
+
+def make_batch(config, families, seed):
+    from duplexumiconsensusreads_amd import synth
+    if config == "C2":
+        return synth.packed_fixed_size(families, seed=seed)
+    return synth.packed_config(synth.CONFIGS[config], families, seed=seed, max_reads=1000)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -91,7 +116,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--families", type=int, default=312_500, help="families per GPU (C2: 312,500)")
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIG_FAMILIES),
+                    help="workload shape (SURVEY.md §8d); C2 is the headline line, the others are "
+                         "per-GPU shards of C3 / C4 / C5 reported for coverage")
+    ap.add_argument("--families", type=int, default=None, help="families per GPU (C2: 312,500)")
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--cpu-reps", type=int, default=2, help="passes of the CPU baseline over the batch")
     ap.add_argument("--no-cpu", action="store_true")
@@ -106,16 +134,19 @@ def main():
         import torch.distributed as tdist
         torch.cuda.set_device(local)
         tdist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    from duplexumiconsensusreads_amd import _lib, synth
+    from duplexumiconsensusreads_amd import _lib
     from duplexumiconsensusreads_amd.device import DeviceBatch
     from duplexumiconsensusreads_amd.params import ConsensusParams
 
     t0 = time.perf_counter()
-    packed = synth.packed_fixed_size(args.families, seed=args.seed + 1000 * rank)
+    families = args.families or CONFIG_FAMILIES[args.config]
+    packed = make_batch(args.config, families, args.seed + 1000 * rank)
     log(f"[rank {rank}] generated {packed.n_reads} reads in {time.perf_counter() - t0:.1f} s")
     dev = f"cuda:{local}"
     db = DeviceBatch(packed, device=dev)
-    ctx = _lib.Context(ConsensusParams(), device=local)
+    # C4 runs with --max_reads 1000; the batch is already downsampled
+    params = ConsensusParams(max_reads=1000) if args.config == "C4" else ConsensusParams()
+    ctx = _lib.Context(params, device=local)
     ctx.reserve(db.batch_struct)
     torch.cuda.synchronize()
 
@@ -154,17 +185,23 @@ def main():
         ms_step = elapsed * 1000.0 / args.steps
         value = total_bases * args.steps / elapsed
         kavg = {k: v / args.steps for k, v in kms.items()}
-        dom = "k_consensus_fast<ss>"
         alg = sscs_algorithmic_bytes(packed)
-        achieved = alg / (kavg[dom] / 1000.0) / 1e9
-        traffic, tsrc = load_traffic("k_consensus_fast<false>", packed.n_fam)
+        if args.config == "C2":
+            dom, dom_label = "k_consensus_fast<ss>", "k_consensus_fast<false> (single-strand consensus)"
+            dom_ms = kavg[dom]
+            traffic, tsrc = load_traffic("k_consensus_fast<false>", packed.n_fam)
+        else:
+            # records split between the fast and general kernels: the whole single-strand stage
+            dom_label = "single-strand stage (k_recmeta<ss> + k_consensus_fast<ss> + k_consensus_general<ss>)"
+            dom_ms = sum(kavg[k] for k in _lib.KERNELS[1:4])
+            traffic, tsrc = None, None
+        achieved = alg / (dom_ms / 1000.0) / 1e9
         res = {
             "metric": METRIC, "value": value, "unit": "consensus bases/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": "C2 (BASELINE.json configs[1]): 10M-read synthetic duplex batch per GPU, "
-                                   "312,500 MI families x 4 subfamilies x 8 reads, 2x150bp, no indels",
+            "config": {"workload": WORKLOAD[args.config],
                        "families_per_gpu": packed.n_fam, "reads_per_gpu": packed.n_reads,
                        "input_bytes_per_gpu": packed.nbytes(),
                        "kernel_ms": kavg,
@@ -173,8 +210,8 @@ def main():
                        "parallelism": f"family-sharded x{world}, no data-path collective"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_consensus_fast<false> (single-strand consensus)",
-                         "kernel_ms": kavg[dom], "algorithmic_bytes_per_launch": alg,
+                         "kernel": dom_label,
+                         "kernel_ms": dom_ms, "algorithmic_bytes_per_launch": alg,
                          "traffic_source": (f"profiles/traffic.json ({tsrc.get('source', '')})" if tsrc else None)},
         }
         if not args.no_cpu and world == 1:

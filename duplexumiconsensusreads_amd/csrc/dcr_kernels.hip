@@ -440,7 +440,10 @@ __device__ __forceinline__ bool acc_step(Acc &A, uint32_t e, double2 f) {
 // Element codes and LUT factors are fetched four reads ahead of their use.
 template <class Src>
 __device__ __forceinline__ void accumulate(Acc &A, int R, const Src &src, const double2 *lut) {
-    bool wide = false;
+    // a later 64-read chunk of the same columns continues the slots: start wide
+    // when some lane already holds more than two (else a third class would be
+    // matched against slots 0-1 only and opened a second time)
+    bool wide = __ballot(A.ns > 2) != 0;
     int r = 0;
     auto step = [&](uint32_t e, double2 f) {
         if (!wide) wide = acc_step<2>(A, e, f);

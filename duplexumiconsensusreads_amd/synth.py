@@ -262,3 +262,106 @@ def packed_fixed_size(n_families, sub_size=8, read_len=150, seed=2, chunk_reads=
     cig_n = np.ones(n, np.int32)
     cigar = np.full(n, (L << 4) | 0, np.uint32)
     return finish_batch(sub_off, read_pos, mapq, seq_off, seq_len, cig_off, cig_n, cigar, bases, quals)
+
+
+def packed_config(cfg: SynthConfig, n_families=None, seed=None, max_reads=None, chunk_reads=1 << 18,
+                  threads=None):
+    """Vectorised generator for any config shape: subfamily
+    sizes from ``cfg.sub_size`` (capped at ``max_reads``, the downsampling the
+    host would have applied), one I or D of 1-3 bp at offset 20-130 on
+    ``indel_frac`` of the reads, a 1-10 bp soft clip at either end on
+    ``softclip_frac`` of them, deep-panel loci when ``cfg.n_loci``.  Same base
+    / quality / substitution model as ``family_records``; reads are the ones
+    that passed ``pass_filters`` (MAPQ 20..60).  For bench-scale batches of
+    the C3 / C4 / C5 shapes, where the per-record generator is too slow."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from .batch import finish_batch
+    rng = np.random.default_rng(cfg.seed if seed is None else seed)
+    F = cfg.n_families if n_families is None else n_families
+    L = cfg.read_len
+    sizes = _sub_sizes(rng, cfg, 4 * F).astype(np.int64)
+    if max_reads is not None:
+        sizes = np.minimum(sizes, max_reads)
+    sub_off = np.zeros(4 * F + 1, np.int64)
+    sub_off[1:] = np.cumsum(sizes)
+    n = int(sub_off[-1])
+    sub_of = np.repeat(np.arange(4 * F), sizes)
+    fam = sub_of // 4
+    rev = (sub_of % 4) >= 2
+    ins = np.maximum(np.clip(rng.normal(300, 30, F), 200, 500).astype(np.int64), L + 10)
+    if cfg.n_loci:
+        P = 1_000_000 + 10_000 * (np.arange(F) % cfg.n_loci)
+    else:
+        P = rng.integers(1000, 100_000_000, F)
+    start = np.where(rev, ins[fam] - L, 0)
+    # indels: kind 0 none, 1 insertion, 2 deletion
+    kind = np.where(rng.random(n) < cfg.indel_frac, np.where(rng.random(n) < 0.5, 1, 2), 0)
+    ioff = rng.integers(20, min(131, L - 5), n)
+    iln = rng.integers(1, 4, n)
+    clip = np.where(rng.random(n) < cfg.softclip_frac, rng.integers(1, 11, n), 0)
+    cleft = rng.random(n) < 0.5
+    # CIGAR ops per read: [S] M [I|D M] [S]
+    ops = np.full((n, 5), -1, np.int64)
+    lens = np.zeros((n, 5), np.int64)
+    m1 = np.where(kind == 0, L, ioff)
+    m2 = np.where(kind == 1, L - ioff - iln, L - ioff)
+    ops[:, 1], lens[:, 1] = 0, m1
+    has2 = kind > 0
+    ops[has2, 2], lens[has2, 2] = kind[has2], iln[has2]
+    ops[has2, 3], lens[has2, 3] = 0, m2[has2]
+    lc = (clip > 0) & cleft
+    rc = (clip > 0) & ~cleft
+    ops[lc, 0], lens[lc, 0] = 4, clip[lc]
+    lens[lc, 1] -= clip[lc]
+    ops[rc, 4], lens[rc, 4] = 4, clip[rc]
+    last = np.where(has2, 3, 1)
+    lens[rc, last[rc]] -= clip[rc]
+    live = ops >= 0
+    cig_n = live.sum(1).astype(np.int32)
+    cigar = ((lens[live] << 4) | ops[live]).astype(np.uint32)
+    cig_off = np.zeros(n, np.int32)
+    cig_off[1:] = np.cumsum(cig_n[:-1])
+    read_pos = (P[fam] + start + np.where(lc, clip, 0)).astype(np.int32)
+    mapq = rng.integers(20, 61, n).astype(np.uint8)
+    seq_len = np.full(n, L, np.int32)
+    seq_off = np.arange(n, dtype=np.int64) * L
+    bases = np.empty(n * L, np.uint8)
+    quals = np.empty(n * L, np.uint8)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    err_lut = np.zeros(256, np.uint16)
+    for q, v in _ERR_P16.items():
+        err_lut[q] = v
+    tw = int(ins.max()) + 20 if F else L
+    ar = np.arange(L)
+    # chunks of whole families, each from its own generator
+    fam_first_read = sub_off[0::4]
+    fam_chunk = max(1, chunk_reads // max(1, int(np.mean(sizes)) * 4))
+    n_chunks = (F + fam_chunk - 1) // fam_chunk
+
+    def fill(ci):
+        f0, f1 = ci * fam_chunk, min(F, (ci + 1) * fam_chunk)
+        r0, r1 = int(fam_first_read[f0]), int(fam_first_read[f1])
+        if r1 == r0:
+            return
+        g = np.random.default_rng([cfg.seed if seed is None else seed, ci])
+        tmpl = acgt[g.integers(0, 4, (f1 - f0) * tw, dtype=np.uint8)]
+        k, o, ln = kind[r0:r1, None], ioff[r0:r1, None], iln[r0:r1, None]
+        delta = np.where((k == 1) & (ar >= o + ln), -ln, 0) + np.where((k == 2) & (ar >= o), ln, 0)
+        idx = ((fam[r0:r1] - f0) * tw + start[r0:r1])[:, None] + ar[None, :] + delta
+        seq = tmpl[idx]
+        inserted = (k == 1) & (ar >= o) & (ar < o + ln)
+        if inserted.any():
+            seq[inserted] = acgt[g.integers(0, 4, int(inserted.sum()))]
+        q = _QLUT[g.integers(0, 100, (r1 - r0, L), dtype=np.uint8)]
+        err = g.integers(0, 65536, (r1 - r0, L), dtype=np.uint16) < err_lut[q]
+        if err.any():
+            code = np.searchsorted(acgt, seq[err])
+            seq[err] = acgt[(code + g.integers(1, 4, int(err.sum()))) % 4]
+        bases[r0 * L:r1 * L] = seq.reshape(-1)
+        quals[r0 * L:r1 * L] = q.reshape(-1)
+
+    with ThreadPoolExecutor(threads or min(16, os.cpu_count() or 1)) as ex:
+        list(ex.map(fill, range(n_chunks)))
+    return finish_batch(sub_off.astype(np.int32), read_pos, mapq, seq_off, seq_len, cig_off, cig_n, cigar, bases,
+                        quals)

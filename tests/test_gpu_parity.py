@@ -122,3 +122,35 @@ def test_gpu_fast_decision_borderline(ctx, maxq, minbq, qhi, sub):
     got = ctx.run_host(packed)
     want = dcr_oracle_c.run(packed, params, n_threads=8)
     assert_same(packed, got, want)
+
+
+@pytest.mark.parametrize("config,families", [("C3", 3000), ("C4", 24), ("C5", 3000)])
+def test_gpu_config_shapes_match_oracle(ctx, config, families):
+    """The bench shapes of C3 (skewed sizes, indels, clips), C4 (100..1000
+    reads per subfamily) and C5, from the vectorised generator the bench uses,
+    bit-exact against the C oracle."""
+    packed = synth.packed_config(synth.CONFIGS[config], families, seed=21, max_reads=1000)
+    params = ConsensusParams(max_reads=1000)
+    ctx.set_params(params)
+    got = ctx.run_host(packed)
+    want = dcr_oracle_c.run(packed, params, n_threads=8)
+    assert_same(packed, got, want)
+    for k in ("seq_start", "len", "status", "has_ins"):
+        assert np.array_equal(got[2][k], want[2][k]), k
+
+
+def test_gpu_deep_insertion_columns_many_classes(ctx):
+    """> 64 reads with insertion columns (the general kernel's 64-read chunks)
+    and error-heavy columns holding 3+ classes in several chunks: the
+    per-class likelihood slots must carry across chunks."""
+    cfg = synth.SynthConfig("t", 8, sub_size="loguniform", logu_lo=65, logu_hi=300, indel_frac=0.3,
+                            softclip_frac=0.1, n_loci=2, seed=31)
+    packed = synth.packed_config(cfg, seed=31, max_reads=1000)
+    rng = np.random.default_rng(31)
+    err = rng.random(packed.bases.shape) < 0.15
+    packed.bases[err] = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, int(err.sum()))]
+    params = ConsensusParams(max_reads=1000, min_base_quality=10)
+    ctx.set_params(params)
+    got = ctx.run_host(packed)
+    want = dcr_oracle_c.run(packed, params, n_threads=8)
+    assert_same(packed, got, want)
