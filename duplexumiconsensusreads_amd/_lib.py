@@ -34,8 +34,8 @@ EXPORTS = {
     "dcr_last_kernel_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
 }
 
-KERNELS = ("k_prep", "k_recmeta<ss>", "k_consensus_fast<ss>", "k_consensus_general<ss>",
-           "k_recmeta<ds>", "k_consensus_fast<ds>", "k_consensus_general<ds>")
+KERNELS = ("k_prep", "k_recmeta<ss>", "k_consensus_fast<ss>", "k_consensus_exact<ss>", "k_consensus_general<ss>",
+           "k_recmeta<ds>", "k_consensus_fast<ds>", "k_consensus_exact<ds>", "k_consensus_general<ds>")
 
 _lib = None
 

@@ -54,8 +54,8 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 struct dcr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    // ev[0] batch start, ev[1..7] after (fused) prep, k_recmeta<ss>, fast<ss>, general<ss>,
-    // k_recmeta<ds>, fast<ds>, general<ds>
+    // ev[0] batch start, ev[1..9] after (fused) prep, k_recmeta<ss>, fast<ss>, exact<ss>,
+    // general<ss>, k_recmeta<ds>, fast<ds>, exact<ds>, general<ds>
     hipEvent_t ev[DCR_N_KERNEL_TIMES + 1] = {};
     dcr_params *d_params = nullptr;
     DevBuf ws;          // workspace
@@ -70,7 +70,7 @@ struct dcr_ctx {
     int fast_maxq = 0, fast_t16 = 0;
     uint16_t *d_llr16 = nullptr;   // device [128]
     int n_cu = 256;     // compute units (persistent grid size)
-    int fast_blocks[2] = {1, 1};   // resident k_consensus_fast blocks per CU (single-strand, duplex)
+    int fast_blocks[4] = {1, 1, 1, 1};   // resident k_consensus_fast blocks per CU (ss, ds; exact ss, exact ds)
 };
 
 // The fast kernel's assumptions (dcr_kernels.hip, fast kernel v2): every
@@ -165,12 +165,12 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
     (void)hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device);
     // the persistent fast kernel's grid = what is resident at once (a block
     // beyond that would start only when a resident one has finished its range)
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->fast_blocks[0], dcr::k_consensus_fast<false>, dcr::kFastBlock, 0) !=
-            hipSuccess || c->fast_blocks[0] < 1)
-        c->fast_blocks[0] = 1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->fast_blocks[1], dcr::k_consensus_fast<true>, dcr::kFastBlock, 0) !=
-            hipSuccess || c->fast_blocks[1] < 1)
-        c->fast_blocks[1] = 1;
+    const void *fk[4] = {(const void *)dcr::k_consensus_fast<false, false>, (const void *)dcr::k_consensus_fast<true, false>,
+                         (const void *)dcr::k_consensus_fast<false, true>, (const void *)dcr::k_consensus_fast<true, true>};
+    for (int k = 0; k < 4; ++k)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->fast_blocks[k], fk[k], dcr::kFastBlock, 0) != hipSuccess ||
+            c->fast_blocks[k] < 1)
+            c->fast_blocks[k] = 1;
     c->host_params = *params;
     if (hipMemcpy(c->d_params, params, sizeof(dcr_params), hipMemcpyHostToDevice) != hipSuccess ||
         upload_fast(c, params) != DCR_OK) {
@@ -223,6 +223,7 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     const size_t o_stamp = o; o = align_up(o + 32 * sizeof(unsigned long long));
     const size_t n_rec = (size_t)std::max<int64_t>(4LL * s->n_fam, 1);
     const size_t o_ovf = o;  o = align_up(o + sizeof(int) * n_rec);
+    const size_t o_xl = o;   o = align_up(o + sizeof(int) * n_rec);
     const size_t o_meta = o; o = align_up(o + sizeof(dcr::RecMeta) * n_rec);
     const size_t o_rm = o;   o = align_up(o + sizeof(uint2) * std::max<size_t>((size_t)s->n_reads, n_rec));
     if (o > c->ws.cap) {
@@ -237,8 +238,10 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     c->w.insflag = (uint8_t *)(b + o_ins);
     c->w.state = (int4 *)(b + o_st);
     c->w.err = (int *)(b + o_err);
-    c->w.ovf_count = (int *)(b + o_err) + 1;     // err, ovf_count[2], fast_count[2]: one 32-byte block
+    c->w.ovf_count = (int *)(b + o_err) + 1;     // err, ovf_count[2], fast_count[2], xcount[2]: one 32-byte block
     c->w.fast_count = (int *)(b + o_err) + 3;
+    c->w.xcount = (int *)(b + o_err) + 5;
+    c->w.xlist = (int *)(b + o_xl);
     c->w.stamps = (unsigned long long *)(b + o_stamp);
     c->w.ovf = (int *)(b + o_ovf);
     c->w.meta = (dcr::RecMeta *)(b + o_meta);
@@ -275,9 +278,8 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     };
     // persistent fast kernel: the resident blocks (16 waves each), at least
     // ~8 records per wave
-    auto fast_grid = [&](int64_t n_rec, bool duplex) {
-        return (unsigned)std::max<int64_t>(
-            1, std::min<int64_t>((n_rec + 127) / 128, (int64_t)c->fast_blocks[duplex ? 1 : 0] * c->n_cu));
+    auto fast_grid = [&](int64_t n_rec, int k) {
+        return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_rec + 127) / 128, (int64_t)c->fast_blocks[k] * c->n_cu));
     };
     auto fast_args = [&](bool duplex) {
         dcr::FastArgs f{};
@@ -292,6 +294,8 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         f.cig_off = in->cig_off;
         f.ovf = c->w.ovf;
         f.ovf_count = c->w.ovf_count + (duplex ? 1 : 0);
+        f.xlist = c->w.xlist;
+        f.xcount = c->w.xcount + (duplex ? 1 : 0);
         f.O = duplex ? *ds : *ss;
         f.P = c->d_params;
         f.stamps = c->w.stamps;
@@ -306,26 +310,33 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         a.n_rec = (duplex ? 2LL : 4LL) * in->n_fam;
         const dcr::FastArgs fa = fast_args(duplex);
         const unsigned nb = (unsigned)((a.n_rec + 255) / 256);    // k_recmeta: 64 records per wave
-        hipEvent_t *ev = c->ev + (duplex ? 5 : 2);
+        hipEvent_t *ev = c->ev + (duplex ? 6 : 2);
+        // the exact queue is filled by the common kernel; its length is only
+        // known on the device, so the exact kernel gets the resident grid
+        const unsigned gx = (unsigned)((int64_t)c->fast_blocks[duplex ? 3 : 2] * c->n_cu);
         if (duplex) {
             hipLaunchKernelGGL(dcr::k_recmeta<true>, dim3(nb), dim3(256), 0, c->stream, a);
             HIP_TRY(hipEventRecord(ev[0], c->stream));
-            hipLaunchKernelGGL(dcr::k_consensus_fast<true>, dim3(fast_grid(a.n_rec, true)), dim3(dcr::kFastBlock), 0,
-                               c->stream, fa);
+            hipLaunchKernelGGL((dcr::k_consensus_fast<true, false>), dim3(fast_grid(a.n_rec, 1)), dim3(dcr::kFastBlock),
+                               0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[1], c->stream));
+            hipLaunchKernelGGL((dcr::k_consensus_fast<true, true>), dim3(gx), dim3(dcr::kFastBlock), 0, c->stream, fa);
+            HIP_TRY(hipEventRecord(ev[2], c->stream));
             hipLaunchKernelGGL(dcr::k_consensus_general<true>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
                                c->stream, a);
         } else {
             hipLaunchKernelGGL(dcr::k_recmeta<false>, dim3(nb), dim3(256), 0, c->stream, a);
             HIP_TRY(hipEventRecord(ev[0], c->stream));
-            hipLaunchKernelGGL(dcr::k_consensus_fast<false>, dim3(fast_grid(a.n_rec, false)), dim3(dcr::kFastBlock), 0,
-                               c->stream, fa);
+            hipLaunchKernelGGL((dcr::k_consensus_fast<false, false>), dim3(fast_grid(a.n_rec, 0)),
+                               dim3(dcr::kFastBlock), 0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[1], c->stream));
+            hipLaunchKernelGGL((dcr::k_consensus_fast<false, true>), dim3(gx), dim3(dcr::kFastBlock), 0, c->stream, fa);
+            HIP_TRY(hipEventRecord(ev[2], c->stream));
             hipLaunchKernelGGL(dcr::k_consensus_general<false>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
                                c->stream, a);
         }
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(ev[2], c->stream));
+        HIP_TRY(hipEventRecord(ev[3], c->stream));
         return DCR_OK;
     };
     if (in->n_fam > 0) {
@@ -356,8 +367,8 @@ int dcr_last_timing(dcr_ctx *c, float *ms4) {
     const int last = DCR_N_KERNEL_TIMES;
     HIP_TRY(hipEventSynchronize(c->ev[last]));
     HIP_TRY(hipEventElapsedTime(&ms4[0], c->ev[0], c->ev[1]));
-    HIP_TRY(hipEventElapsedTime(&ms4[1], c->ev[1], c->ev[4]));
-    HIP_TRY(hipEventElapsedTime(&ms4[2], c->ev[4], c->ev[last]));
+    HIP_TRY(hipEventElapsedTime(&ms4[1], c->ev[1], c->ev[5]));
+    HIP_TRY(hipEventElapsedTime(&ms4[2], c->ev[5], c->ev[last]));
     HIP_TRY(hipEventElapsedTime(&ms4[3], c->ev[0], c->ev[last]));
     return DCR_OK;
 }

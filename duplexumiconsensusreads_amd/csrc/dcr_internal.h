@@ -38,6 +38,8 @@ struct Workspace {
     int *ovf;               // [n_rec] records for the general kernel
     int *ovf_count;         // [2] single-strand / duplex general-list lengths
     int *fast_count;        // [2] single-strand / duplex fast-list lengths
+    int *xcount;            // [2] single-strand / duplex exact-queue lengths
+    int *xlist;             // [n_rec] exact queue: fast-list indices (k_consensus_fast<., true>)
     unsigned long long *stamps;   // [32] diagnostic phase cycles (DCR_STAMP builds only)
     RecMeta *meta;          // [n_rec] fast list
     uint2 *rmeta;           // [max(n_reads, 4F)] per read: len | mapq << 8 | (pos - pos of the record's
@@ -66,6 +68,8 @@ struct FastArgs {
     const int32_t *cig_off;         // single-strand: batch cig_off
     int *ovf;                       // general list of this strand
     int *ovf_count;
+    int *xlist;                     // exact queue (fast-list indices) and its length
+    int *xcount;
     dcr_out O;                      // this strand's outputs
     const dcr_params *P;
     unsigned long long *stamps;     // diagnostic builds
@@ -78,7 +82,7 @@ struct FastArgs {
 
 __global__ void k_prep(dcr_batch in, const dcr_params *P, Workspace ws);
 template <bool DUPLEX> __global__ void k_recmeta(Args a);
-template <bool DUPLEX> __global__ void k_consensus_fast(FastArgs a);
+template <bool DUPLEX, bool EXACT> __global__ void k_consensus_fast(FastArgs a);
 template <bool DUPLEX> __global__ void k_consensus_general(Args a);
 
 }  // namespace dcr

@@ -489,29 +489,21 @@ __device__ __forceinline__ int phred_from_table(double x, int maxq, const double
     return q;
 }
 
-// posterior, mask, output quality (:603-621, :699-709), depth/errors (:1001-1012)
-__device__ __forceinline__ ColOut finalize(const Acc &A, int nsw, int R, bool ins_col, const dcr_params *P,
-                                           const double *qthr, bool simple_q) {
-    double L[6];
-    int c[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        L[i] = A.U;
-        c[i] = 0;
-    }
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        if (j < nsw) {
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                const bool m = A.k[j] == i;
-                L[i] = m ? A.s[j] : L[i];
-                c[i] = m ? A.n[j] : c[i];
-            }
-        }
-    }
-    const int cN = R - c[0] - c[1] - c[2] - c[3] - c[4] - c[5] - A.nbad;
-    ColOut o;
+// posterior, mask and output quality of one column from its six likelihoods
+// (:603-621, :699-709): S summed left to right (:608), np.argmax (first max,
+// first NaN wins) and np.max, masking below the threshold (NaN never), then
+// Q = int(round(-10 log10(e'))) capped at maxQ (ValueError -> maxQ).
+struct Posterior {
+    int best;        // argmax class index (A T C G + -)
+    int ch;          // consensus character
+    int q;           // consensus quality
+    bool masked;
+    bool overflow;   // int(-inf): the reference raises OverflowError
+};
+
+__device__ __forceinline__ Posterior posterior(const double (&L)[6], bool has_plus, const dcr_params *P,
+                                               const double *qthr, bool simple_q) {
+    Posterior o;
     double S = L[0] + L[1];                      // np.sum of 6: left to right (:608)
     S = S + L[2];
     S = S + L[3];
@@ -562,7 +554,6 @@ __device__ __forceinline__ ColOut finalize(const Acc &A, int nsw, int R, bool in
             }
         }
     }
-    const bool has_plus = c[4] > 0;              // '+' in nucleotides (:613, :618)
     const bool masked = pm < P->post_threshold;  // NaN is never masked (:617)
     const int kc = masked ? 6 : best;
     const bool lower = has_plus && (kc < 4 || kc == 6);
@@ -585,6 +576,43 @@ __device__ __forceinline__ ColOut finalize(const Acc &A, int nsw, int R, bool in
         if (__builtin_isinf(x)) o.overflow = true;
         else q = phred_from_table(x, P->max_base_quality, qthr);
     }
+    o.best = best;
+    o.ch = ch;
+    o.q = q;
+    o.masked = masked;
+    return o;
+}
+
+// posterior, mask, output quality (:603-621, :699-709), depth/errors (:1001-1012)
+__device__ __forceinline__ ColOut finalize(const Acc &A, int nsw, int R, bool ins_col, const dcr_params *P,
+                                           const double *qthr, bool simple_q) {
+    double L[6];
+    int c[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        L[i] = A.U;
+        c[i] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        if (j < nsw) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const bool m = A.k[j] == i;
+                L[i] = m ? A.s[j] : L[i];
+                c[i] = m ? A.n[j] : c[i];
+            }
+        }
+    }
+    const int cN = R - c[0] - c[1] - c[2] - c[3] - c[4] - c[5] - A.nbad;
+    ColOut o;
+    const bool has_plus = c[4] > 0;              // '+' in nucleotides (:613, :618)
+    const Posterior po = posterior(L, has_plus, P, qthr, simple_q);
+    const int kc = po.masked ? 6 : po.best;
+    const bool lower = has_plus && (kc < 4 || kc == 6);
+    const int ch = po.ch;
+    const int q = po.q;
+    o.overflow = po.overflow;
     o.ch = ch;
     o.q = q;
     // depth: rows not in {N, n, +}; errors: rows != consensus char (case-sensitive)
@@ -1605,7 +1633,7 @@ constexpr int kTable = 5 * 0x800;                          // 5 class banks of 2
 constexpr int kStage0 = kTable;                            // 4 KiB per wave
 constexpr int kInvD = kStage0 + kWaves * 0x1000;           // f64 [64] 1 / d
 constexpr int kSent = kInvD + 64 * 8;                      // u16 pad code (out-of-read sentinel)
-constexpr int kPtrs = kSent + 16;                          // u64 [10] record-scalar destinations, [4] rare-path pointers
+constexpr int kPtrs = kSent + 16;                          // u64 [10] record-scalar destinations, [6] rare-path pointers
 constexpr int kRm = kPtrs + 16 * 8;                        // per wave: u64 [64] the current record's read words
 constexpr int kMv = kRm + kWaves * kWave * 8;              // per wave: u32 [8] a later record's descriptor
 constexpr int kOv = kMv + kWaves * 32;                     // per wave: u16 [256] column words d | e << 6 | call << 12
@@ -1903,9 +1931,12 @@ __device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &
     return s;
 }
 
-// products, finalize, outputs of a staged record of T <= 64 NT columns
-template <bool DUPLEX, int NT>
-__device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &m, const Staged &sg, uint8_t *lds,
+// products, finalize, outputs of a staged record of T <= 64 NT columns.
+// Returns false (nothing written) when the record has a column the bound does
+// not decide and this is not the EXACT instantiation: the caller queues it for
+// the EXACT kernel, which computes those columns in the reference's arithmetic.
+template <bool DUPLEX, int NT, bool EXACT>
+__device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &m, const Staged &sg, uint8_t *lds,
                                               const int stage_addr, const int ov_addr, const int rm_addr, const int lane,
                                               Stamps &sp) {
     const dcr_out &O = a.O;
@@ -1918,7 +1949,7 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
     const uint2 rm = sg.rm;
     if (DCR_ABL == 1) {                 // diagnostic: staging only
         if (lane == 0) O.pos[rec] = *(const uint16_t *)(lds + stage_addr + 2 * (int)(rm.y & 7)) + msum;
-        return;
+        return true;
     }
     const int colr = (int)(rm.x & 255u), lenr = (int)((rm.x >> 8) & 255u);
     const int crv = stage_addr + 2 * ((int)rm.y - colr);
@@ -1931,14 +1962,14 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt) x += (uint32_t)ev.llr[tt] ^ (uint32_t)(ev.llr[tt] >> 32) ^ ev.cnt[tt];
         if (lane == 0) O.pos[rec] = (int)x;
-        return;
+        return true;
     }
 
     // decide every tile in registers (integer, straight-line): call, depth d
     // and errors e (:970-1021) as the column word d | e << 6 | call << 12
     const double *invd = (const double *)(lds + fk::kInvD);
     uint8_t *ov = lds + ov_addr;
-    uint32_t outside = 0;              // a live column not decided
+    uint32_t und = 0;                  // bit tt: the lane's live column is not decided
     int dmax = -1, dmin = 0x7fffffff;
     double ex[NT];                     // e/d of the lane's column (0 outside T)
 #pragma unroll
@@ -1961,7 +1992,7 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
         const int e = R - nb;                                                     // rows that differ from the call
         // decided: LLR_b - max(LLR_k, 0) >= (Lb - L2 - (d - nb)) / 16 >= T16 / 16
         const bool undecided = (int)(Lb - L2) - (d - nb) < a.t16;
-        outside |= (uint32_t)(live && undecided);
+        und |= (uint32_t)(live && undecided) << tt;
         const double etv = (double)e * invd[d];                      // e/d to 1 ulp (the mean's decision
                                                                      // tolerates 1e-9; the exact walk divides)
         *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (kb << 12));
@@ -1969,10 +2000,100 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
         dmax = max(dmax, live ? d : -1);
         dmin = min(dmin, live ? d : 0x7fffffff);
     }
-    if (__ballot(outside)) { send_to_general<DUPLEX>(a, m, rm, lds, lane); return; }
+    // Columns the bound does not decide get the reference's own arithmetic
+    // here (most_likely_nucleotide :594-621 in read order, IEEE binary64, then
+    // the quality of :699-709): their call may be masked 'N' and their quality
+    // below maxQ.  The kept span then runs from the first to the last column
+    // that is not 'N' (:770-790), still one M run (no '+' / '-' rows here).
+    int first = 0, last = T - 1;
+    const bool exact = __ballot(und) != 0;
+    if (!EXACT && exact) return false;
+    // exact columns' character | quality << 8, as u16 per column in the wave's
+    // read-word LDS (free once the read words are in registers)
+    uint16_t *chq = (uint16_t *)(lds + rm_addr);
+    if (exact) {
+        const dcr_params *P = a.P;
+        const double *qthr = P->qthresh;
+        bool fail = false;             // '+' / '-' call or int(-inf) quality: general kernel
+#pragma unroll 1
+        for (int tt = 0; tt < NT; ++tt) {
+            const bool mine = (und >> tt) & 1u;
+            if (__ballot(mine) == 0) continue;
+            const int t = 64 * tt + lane;
+            double L4[4] = {1.0, 1.0, 1.0, 1.0};
+            double U = 1.0;
+            uint32_t cnt = 0;          // 8-bit row counts of A T C G
+            for (int r = 0; r < R; ++r) {
+                const int cr = readlane(crv, r);
+                const int x = readlane((int)rm.x, r);
+                const int col = x & 255, len = (x >> 8) & 255;
+                const uint32_t ad = (uint32_t)(t - col) < (uint32_t)len ? (uint32_t)(cr + 2 * t) : (uint32_t)fk::kSent;
+                const uint32_t code = *(const uint16_t *)(lds + ad);
+                const uint32_t k = code >> 11;                       // N 0, A 1, T 2, C 3, G 4
+                const uint32_t q = ((code >> 4) & 127u) - k;         // raw quality (pad 'N': 2)
+                const double fm = P->match[q], fx = P->mismatch[q];
+                U = U * fx;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) L4[i] = L4[i] * (k == (uint32_t)(i + 1) ? fm : fx);
+                cnt += k ? 1u << (8 * (k - 1)) : 0u;
+            }
+            const double L[6] = {L4[0], L4[1], L4[2], L4[3], U, U};
+            const Posterior po = posterior(L, false, P, qthr, true);
+            if (mine) {
+                fail |= po.overflow || (!po.masked && po.best > 3);
+                const uint32_t w = *(const uint16_t *)(ov + 2 * t);
+                const int d = (int)(w & 63u);
+                const int nb = po.best <= 3 ? (int)((cnt >> (8 * po.best)) & 255u) : 0;
+                const int e = po.masked ? d : R - nb;               // rows != the consensus character
+                *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6));
+                chq[t] = (uint16_t)((uint32_t)po.ch | ((uint32_t)po.q << 8));
+            }
+        }
+        lds_fence();
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            if ((und >> tt) & 1u) {
+                const uint32_t w = *(const uint16_t *)(ov + 2 * (64 * tt + lane));
+                const uint32_t d = w & 63u;
+                ex[tt] = d == 0 ? 1.0 : (double)((w >> 6) & 63u) * invd[d];   // e/d, d == 0 -> 1 (:1010-1012)
+            }
+        }
+        // kept span: first / last column whose character is not 'N'
+        int fst = 0x7fffffff, lst = -1;
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            const int t = 64 * tt + lane;
+            const bool live = tt < NT - 1 || t < T;
+            const bool isn = (und >> tt) & 1u ? (chq[t] & 255u) == 'N' : false;
+            if (live && !isn) {
+                fst = min(fst, t);
+                lst = max(lst, t);
+            }
+        }
+        first = wave_min(fst);
+        last = wave_max(lst);
+        // all 'N' (compress_cigarlist([]) :740 raises) or an unrepresentable column
+        if (__ballot(fail) || last < 0) { send_to_general<DUPLEX>(a, m, rm, lds, lane); return true; }
+        // characters / qualities of the kept span into the (now free) stage, shifted to its start
+        lds_fence();
+        uint8_t *sb = lds + stage_addr + 0x800;
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            const int t = 64 * tt + lane;
+            if (t >= first && t <= last) {
+                const uint32_t wv = *(const uint16_t *)(ov + 2 * t);
+                const uint32_t v = (und >> tt) & 1u ? (uint32_t)chq[t]
+                                                   : (uint32_t)((0x47435441u >> (8 * (wv >> 12))) & 255u) |
+                                                         ((uint32_t)a.maxq << 8);
+                sb[t - first] = (uint8_t)v;
+                sb[0x100 + t - first] = (uint8_t)(v >> 8);
+            }
+        }
+    }
     sp.mark(6);                          // [5] finalize
     const int Dmax = wave_max(dmax);
     const int Dmin = wave_min(dmin);
+    const int klen = last - first + 1;   // kept columns
     sp.mark(7);                          // [6] depth reductions
     // d / e / seq / qual from the column words, four columns per lane (one
     // 8-, 8-, 4- and 4-byte store each); the region tail up to the next 16
@@ -1986,13 +2107,21 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
             const uint2 w = *(const uint2 *)(ov + 8 * lane);
             *(uint2 *)(O.d + off + c0) = make_uint2(w.x & 0x003F003Fu, w.y & 0x003F003Fu);
             *(uint2 *)(O.e + off + c0) = make_uint2((w.x >> 6) & 0x003F003Fu, (w.y >> 6) & 0x003F003Fu);
-            const uint32_t sel = ((w.x >> 12) & 3u) | ((w.x >> 20) & 0x300u) | ((w.y << 4) & 0x30000u) |
-                                 ((w.y >> 4) & 0x3000000u);
-            const int nl = min(max(T - c0, 0), 4);                       // live columns of the four
+            const int nl = min(max(klen - c0, 0), 4);                    // kept columns of the four
             const uint32_t keep = nl == 4 ? 0xFFFFFFFFu : (1u << (8 * nl)) - 1u;
-            const uint32_t letters = __builtin_amdgcn_perm(0u, 0x47435441u, sel);   // "ATCG"[call]
+            uint32_t letters, quals;
+            if (!exact) {
+                const uint32_t sel = ((w.x >> 12) & 3u) | ((w.x >> 20) & 0x300u) | ((w.y << 4) & 0x30000u) |
+                                     ((w.y >> 4) & 0x3000000u);
+                letters = __builtin_amdgcn_perm(0u, 0x47435441u, sel);  // "ATCG"[call]
+                quals = (uint32_t)a.maxq * 0x01010101u;
+            } else {
+                const uint8_t *sb = lds + stage_addr + 0x800;
+                letters = *(const uint32_t *)(sb + c0);
+                quals = *(const uint32_t *)(sb + 0x100 + c0);
+            }
             *(uint32_t *)(O.seq + off + c0) = (letters & keep) | (0x4E4E4E4Eu & ~keep);
-            *(uint32_t *)(O.qual + off + c0) = ((uint32_t)a.maxq * 0x01010101u) & keep;
+            *(uint32_t *)(O.qual + off + c0) = quals & keep;
         }
     }
     sp.mark(8);                          // [7] per-column stores
@@ -2018,6 +2147,7 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
     if (__builtin_expect(__builtin_fabs(fr - 0.5) > 1e-9 * (1.0 + y), 1) && DCR_ABL != 4) {
         E = __builtin_rint(y) / 1000.0;
     } else {
+        lds_fence();
         double *et = (double *)(lds + stage_addr);
         const int ln = lane;
         const uint8_t *ovr = lds + ov_addr;
@@ -2026,7 +2156,8 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
             const int t = 64 * tt + ln;
             if (t < T) {
                 const uint32_t w = *(const uint16_t *)(ovr + 2 * t);
-                et[t] = (double)((w >> 6) & 63u) / (double)(w & 63u);   // e / d exactly (:1010-1012; d >= 1)
+                const uint32_t dd = w & 63u;
+                et[t] = dd == 0 ? 1.0 : (double)((w >> 6) & 63u) / (double)dd;   // e / d exactly (:1010-1012)
             }
         }
         lds_fence();
@@ -2042,12 +2173,12 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
         // MAPQ = msum / R (:874-889, :1377): exact as msum * ceil(2^24 / R) >> 24 for msum < 2^14
         const int mapq = (int)(((uint64_t)(uint32_t)msum * *(const uint32_t *)(lds + fk::kDivR + 4 * R)) >> 24);
         // lane k takes field k through the wave's (now free) read-word LDS:
-        // pos (:790), MAPQ, len, n_cig, n_de, D, M, E (two words), one M run of T
+        // pos (:790), MAPQ, len, n_cig, n_de, D, M, E (two words), one M run of the kept columns
         uint8_t *sc = lds + rm_addr;
         if (lane == 0) {
-            *(int4 *)sc = make_int4(minpos, mapq, T, 1);
+            *(int4 *)sc = make_int4(minpos + first, mapq, klen, 1);
             *(int4 *)(sc + 16) = make_int4(T, Dmax, Dmin, E_lo);
-            *(int2 *)(sc + 32) = make_int2(E_hi, (int)((uint32_t)T << 4));
+            *(int2 *)(sc + 32) = make_int2(E_hi, (int)((uint32_t)klen << 4));
         }
         lds_fence();
         const int v = *(const int *)(sc + 4 * min(lane, 9));
@@ -2057,6 +2188,7 @@ __device__ __forceinline__ void finish_record(const FastArgs &a, const RecMeta &
         if (lane == 0) O.status[rec] = DCR_ST_OK;
     }
     sp.mark(10);                         // [9] record scalars
+    return true;
 }
 
 __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
@@ -2077,7 +2209,13 @@ __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
 // never copied while in flight) as soon as record i's codes are in LDS, and the
 // descriptor of record i + 2 is fetched by a vector load (vmcnt, not lgkmcnt,
 // so LDS waits never drain it).
-template <bool DUPLEX>
+//
+// EXACT = false drains the fast list; a record with a column the integer bound
+// does not decide is queued (its fast-list index, 64 at a time per wave) for
+// the EXACT = true instantiation, which drains that queue and computes such
+// columns in the reference's double arithmetic.  The common kernel thus keeps
+// none of the exact path's code or registers.
+template <bool DUPLEX, bool EXACT>
 __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[fk::kLdsBytes];
     for (int i = threadIdx.x; i < 5 * (fk::kRowMax + 1); i += fk::kBlockThreads) {
@@ -2091,7 +2229,7 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
         const int t = threadIdx.x;
         ((uint32_t *)(lds + fk::kDivR))[t] = t == 0 ? 0u : ((1u << 24) + (uint32_t)t - 1u) / (uint32_t)t;
     }
-    if (threadIdx.x < 14) {
+    if (threadIdx.x < 16) {
         const int k = threadIdx.x;
         uint64_t v;
         switch (k) {
@@ -2099,6 +2237,8 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
         case 11: v = (uint64_t)(uintptr_t)a.cig_off; break;
         case 12: v = (uint64_t)(uintptr_t)a.ovf; break;
         case 13: v = (uint64_t)(uintptr_t)a.ovf_count; break;
+        case 14: v = (uint64_t)(uintptr_t)a.xlist; break;
+        case 15: v = (uint64_t)(uintptr_t)a.xcount; break;
         default: v = scalar_dest(a.O, k); break;
         }
         *(uint64_t *)(lds + fk::kPtrs + 8 * k) = v;
@@ -2109,7 +2249,7 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
     const int rm_addr = fk::kRm + wave * kWave * 8;
     const int ov_addr = fk::kOv + wave * 512;
     __syncthreads();
-    const int64_t n = *a.fast_count;
+    const int64_t n = EXACT ? *a.xcount : *a.fast_count;
     const int64_t nw = (int64_t)gridDim.x * fk::kWaves;
     const int64_t gw = (int64_t)blockIdx.x * fk::kWaves + wave;
     int i = (int)(n * gw / nw);
@@ -2117,11 +2257,20 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
     if (i >= iend) return;
     const RecMeta *ML = a.meta;
     const int ilast = iend - 1;
-    RecMeta m0 = ML[i];
-    RecMeta m1 = ML[min(i + 1, ilast)];
+    auto midx = [&](int j) { return EXACT ? a.xlist[j] : j; };   // EXACT: the queue holds fast-list indices
+    RecMeta m0 = ML[midx(i)];
+    RecMeta m1 = ML[midx(min(i + 1, ilast))];
     FastStage st;
-    fast_load<DUPLEX>(a, m0, ML + min(i + 2, ilast), lane0, st);
+    fast_load<DUPLEX>(a, m0, ML + midx(min(i + 2, ilast)), lane0, st);
     Stamps sp;
+    int pend = 0, npend = 0;           // !EXACT: queued fast-list indices (lane p holds the p-th)
+    auto flush = [&](int ln) {         // queue pointers from the LDS cache (no scalar registers held)
+        int base = 0;
+        if (ln == 0) base = atomicAdd(lds_ptr<int>(lds, 15), npend);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (ln < npend) lds_ptr<int>(lds, 14)[base + ln] = pend;
+        npend = 0;
+    };
     for (;;) {
         // lane-derived addresses are formed per record, not hoisted out of the
         // record loop into registers held across it
@@ -2139,7 +2288,7 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
         __builtin_amdgcn_sched_barrier(0);
         // record i + 1's bytes and record i + 3's descriptor; unconditional (the
         // last record re-loads itself) so the registers have one definition
-        fast_load<DUPLEX>(a, m1, ML + min(i + 3, ilast), lane, st);
+        fast_load<DUPLEX>(a, m1, ML + midx(min(i + 3, ilast)), lane, st);
         sp.mark(3);                    // [2] prefetch issue
         lds_fence();
         const uint2 rw = *(const uint2 *)(lds + rm_addr + 8 * lane);
@@ -2175,15 +2324,21 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
         if (sg.state == 1) {
             send_to_general<DUPLEX>(a, m0, sg.rm, lds, lane);
         } else if (sg.state == 0) {
-            if (sg.T <= 64) finish_record<DUPLEX, 1>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
-            else if (sg.T <= 128) finish_record<DUPLEX, 2>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
-            else if (sg.T <= 192) finish_record<DUPLEX, 3>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
-            else finish_record<DUPLEX, 4>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
+            bool done;
+            if (sg.T <= 64) done = finish_record<DUPLEX, 1, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
+            else if (sg.T <= 128) done = finish_record<DUPLEX, 2, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
+            else if (sg.T <= 192) done = finish_record<DUPLEX, 3, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
+            else done = finish_record<DUPLEX, 4, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
+            if (!EXACT && !done) {
+                if (lane == npend) pend = i;
+                if (++npend == kWave) flush(lane);
+            }
         }
         if (++i >= iend) break;
         m0 = m1;
         m1 = m2;
     }
+    if (!EXACT && npend) flush(lane0);
     if (DCR_STAMP && lane0 == 0)
         for (int k = 0; k < 10; ++k) atomicAdd(&a.stamps[k + (DUPLEX ? 16 : 0)], (unsigned long long)sp.acc[k]);
 }
@@ -2209,8 +2364,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_consensus_general(Args a) {
 
 template __global__ void k_recmeta<false>(Args);
 template __global__ void k_recmeta<true>(Args);
-template __global__ void k_consensus_fast<false>(FastArgs);
-template __global__ void k_consensus_fast<true>(FastArgs);
+template __global__ void k_consensus_fast<false, false>(FastArgs);
+template __global__ void k_consensus_fast<true, false>(FastArgs);
+template __global__ void k_consensus_fast<false, true>(FastArgs);
+template __global__ void k_consensus_fast<true, true>(FastArgs);
 template __global__ void k_consensus_general<false>(Args);
 template __global__ void k_consensus_general<true>(Args);
 

@@ -162,9 +162,10 @@ int dcr_read_info_host(dcr_ctx *ctx, dcr_read_info *out, int64_t n_reads);
 int dcr_last_timing(dcr_ctx *ctx, float *ms4);
 /* per-kernel timing of the last dcr_run_batch (HIP events between launches on
    the context stream), ms: k_prep, then per strand (single-strand, duplex)
-   k_recmeta, k_consensus_fast, k_consensus_general */
-#define DCR_N_KERNEL_TIMES 7
-int dcr_last_kernel_timing(dcr_ctx *ctx, float *ms7);
+   k_recmeta, k_consensus_fast, k_consensus_fast (exact queue),
+   k_consensus_general */
+#define DCR_N_KERNEL_TIMES 9
+int dcr_last_kernel_timing(dcr_ctx *ctx, float *ms9);
 
 /* CPU restatement with the same contract (oracle/, test infrastructure):
    host pointers, single thread (or n_threads > 1) */

@@ -35,12 +35,11 @@ for rnd in range(6):
         assert lib.dcr_run_batch(ctx, ctypes.byref(db.batch_struct), ctypes.byref(db.ss_struct),
                                  ctypes.byref(db.ds_struct)) == 0
         assert lib.dcr_sync(ctx) in (0, 3)
-        ms = (ctypes.c_float * 7)()
+        ms = (ctypes.c_float * 9)()
         lib.dcr_last_kernel_timing(ctx, ms)
         if rnd:
-            res[path].append((ms[2], ms[5]))
+            res[path].append(list(ms))
 for path in libs:
     v = res[path]
-    ss = sorted(x[0] for x in v)[len(v) // 2]
-    ds = sorted(x[1] for x in v)[len(v) // 2]
-    print(f"{os.path.basename(path):24s} fast<ss> {ss:8.3f} ms  fast<ds> {ds:8.3f} ms")
+    med = [sorted(x[k] for x in v)[len(v) // 2] for k in range(9)]
+    print(f"{os.path.basename(path):24s} slots(ms): " + " ".join(f"{m:7.3f}" for m in med) + f"  sum {sum(med):7.3f}")

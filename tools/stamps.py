@@ -34,7 +34,7 @@ K = 3
 kt = [0.0] * 7
 for _ in range(K):
     assert run() == 0
-    ms = (ctypes.c_float * 7)()
+    ms = (ctypes.c_float * 9)()
     lib.dcr_last_kernel_timing(ctx, ms)
     kt = [a + b for a, b in zip(kt, ms)]
 lib.dcr_debug_stamps(ctx, st, 32, 0)
