@@ -175,11 +175,37 @@ def pack_families(families):
                         cig_off, cig_n, np.asarray(cigs, np.uint32), bases, qualv)
 
 
+def _end_soft_clips(cigar, cig_off, cig_n):
+    """Per read: length of the soft clip at the 5' end plus the one at the 3'
+    end (each the first / last op, or the op inside a hard clip there)."""
+    n = len(cig_n)
+    out = np.zeros(n, np.int64)
+    if n == 0 or len(cigar) == 0:
+        return out
+    cig = np.asarray(cigar, np.uint32)
+    off = np.asarray(cig_off, np.int64)
+    cn = np.asarray(cig_n, np.int64)
+    has = cn > 0
+    op = lambda i: (cig[np.clip(i, 0, len(cig) - 1)] & 15).astype(np.int64)
+    ln = lambda i: (cig[np.clip(i, 0, len(cig) - 1)] >> 4).astype(np.int64)
+    first, last = off, off + cn - 1
+    c5 = np.where(op(first) == 4, ln(first), np.where((op(first) == 5) & (cn > 1) & (op(first + 1) == 4),
+                                                      ln(first + 1), 0))
+    i5 = np.where(op(first) == 4, first, first + 1)          # the op counted at the 5' end
+    c3i = np.where(op(last) == 4, last, np.where((op(last) == 5) & (cn > 1), last - 1, -1))
+    c3 = np.where((c3i >= first) & (op(c3i) == 4) & ~((c5 > 0) & (c3i == i5)), ln(c3i), 0)
+    return np.where(has, c5 + c3, 0)
+
+
 def finish_batch(sub_off, read_pos, read_mapq, seq_off, seq_len, cig_off, cig_n, cigar, bases, quals):
     """Compute the output-region offsets (vectorised) and build the batch."""
     n_sub = len(sub_off) - 1
     F = n_sub // 4
-    ends = read_pos.astype(np.int64) + seq_len
+    # kept length after remove_clipping (:191-265): a soft clip at either end
+    # (inside a hard clip) drops its bases, so T below is the device's T before
+    # the 3' N trim, exactly (regions are then exactly what the kernels fill)
+    kept = seq_len.astype(np.int64) - _end_soft_clips(cigar, cig_off, cig_n)
+    ends = read_pos.astype(np.int64) + kept
     cnt = np.diff(sub_off)
     if len(read_pos) and (cnt > 0).all():
         mn = np.minimum.reduceat(read_pos.astype(np.int64), sub_off[:-1])

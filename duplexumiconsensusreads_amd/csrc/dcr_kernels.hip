@@ -57,10 +57,8 @@ constexpr uint32_t kDel = (5u << 9) | DCR_LUT_DEL;
 
 struct WaveLds {
     uint16_t pad_code[4];                  // [0] = kPad: sentinel the fast layout loads outside a read (8 B keeps stage 8-aligned)
-    union {
-        uint16_t stage[kStageElems];       // fast layout: element codes of the record's bytes
-        uint16_t tile[kWave][kTileIns];    // insertion layout: 64 reads x 32 columns
-    };
+    uint16_t stage[kStageElems];           // element codes of the record's bytes (records that fit)
+    uint16_t tile[kWave][kTileIns];        // insertion layout: 64 reads x 32 columns
     int32_t cons[kColsLds];
     double et[kColsLds];
     // uniform stack of the pairwise-sum walk (phase 3)
@@ -313,15 +311,16 @@ __device__ __forceinline__ void sim_advance(Sim &s, const ReadRef &rd) {
     }
 }
 
-// one column of :473-545 for one read; returns the element code
-template <bool DUPLEX>
-__device__ __forceinline__ uint32_t sim_step(Sim &s, const ReadRef &rd, int p, bool ins_col,
-                                             int minbq, bool &idx_err) {
+// one column of :473-545 for one read; returns the element code.  `elem(is)`
+// gives the code of the read's base is (from HBM, or from the LDS stage)
+template <bool DUPLEX, class Elem>
+__device__ __forceinline__ uint32_t sim_step_e(Sim &s, const ReadRef &rd, int p, bool ins_col, bool &idx_err,
+                                               const Elem &elem) {
     uint32_t e;
     if (ins_col) {                                   // :478-499
         if (s.curop == 1) {
             if (s.is >= rd.len) { idx_err = true; return kPad; }
-            e = base_elem<DUPLEX>(rd, s.is, minbq);
+            e = elem(s.is);
             ++s.is;
             sim_advance(s, rd);
         } else {
@@ -334,7 +333,7 @@ __device__ __forceinline__ uint32_t sim_step(Sim &s, const ReadRef &rd, int p, b
         if (s.curop == 2) {
             e = kDel;
         } else {
-            e = base_elem<DUPLEX>(rd, s.is, minbq);
+            e = elem(s.is);
             ++s.is;
         }
         sim_advance(s, rd);
@@ -342,6 +341,12 @@ __device__ __forceinline__ uint32_t sim_step(Sim &s, const ReadRef &rd, int p, b
         e = kPad;
     }
     return e;
+}
+template <bool DUPLEX>
+__device__ __forceinline__ uint32_t sim_step(Sim &s, const ReadRef &rd, int p, bool ins_col,
+                                             int minbq, bool &idx_err) {
+    return sim_step_e<DUPLEX>(s, rd, p, ins_col, idx_err,
+                              [&](int is) { return base_elem<DUPLEX>(rd, is, minbq); });
 }
 
 // position of op index j of a read without I ops: (op, seq index), or pad.
@@ -761,8 +766,9 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
         }
     }
 
-    // ---- phase 0: element codes into LDS
-    if (staged) {
+    // ---- phase 0: element codes into LDS (every record whose bytes fit: the
+    // fast layout reads them by column, the insertion layout by read)
+    if (fits) {
 #pragma unroll
         for (int u = 0; u < kStageDw; ++u) {
             const int d = u * kWave + lane;
@@ -894,7 +900,17 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
                 const bool isI = lane < R && sim.curop == 1;
                 const bool any = __ballot(isI) != 0;
                 insmask |= (uint64_t)any << tt;
-                if (lane < R) W.tile[lane][tt] = (uint16_t)sim_step<DUPLEX>(sim, myrd, minpos + c0 + tt, any, minbq, idx_err);
+                if (lane < R) {
+                    uint32_t e;
+                    if (fits) {
+                        const int so = (int)(myrd.seq_start - base_al);
+                        e = sim_step_e<DUPLEX>(sim, myrd, minpos + c0 + tt, any, idx_err,
+                                               [&](int is) { return (uint32_t)W.stage[so + is]; });
+                    } else {
+                        e = sim_step<DUPLEX>(sim, myrd, minpos + c0 + tt, any, minbq, idx_err);
+                    }
+                    W.tile[lane][tt] = (uint16_t)e;
+                }
             }
             wave_fence();
             ins_col = live && ((insmask >> lane) & 1);
@@ -1043,6 +1059,14 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
     if (nruns == 0) { write_status(DCR_ST_INDEX_ERROR); return; }   // compress_cigarlist([])
     if (n_de == 0) { write_status(DCR_ST_VALUE_ERROR); return; }     // max([]) at :1005
     if (kept_overflow) { write_status(DCR_ST_OVERFLOW_ERROR); return; }
+    // single-strand: the rest of the region reads 'N' / quality 0, so the duplex
+    // pass, which stages this region whole, never sees a byte that is not a
+    // valid letter (the fast kernel pads its records the same way)
+    if (!DUPLEX)
+        for (int64_t i = nlen + lane; i < cap; i += kWave) {
+            oseq[i] = 'N';
+            oqual[i] = 0;
+        }
     wave_fence();
     for (int i0 = 0; i0 < nruns; i0 += kWave) {
         const int i = i0 + lane;
@@ -1548,7 +1572,10 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
             const int64_t base_al = (int64_t)g.lo & ~(int64_t)15;     // 16-byte staging loads
             const int64_t span = (int64_t)g.hi - base_al;
             const bool aligned = ((((uintptr_t)gb) | ((uintptr_t)gq)) & 15) == 0;
-            if ((g.flags & 4) || !aligned || R > kFastMaxR || span > kStageElems || T > kFastMaxT || T > cap ||
+            // single-strand: the fast kernel pads its region to T rounded to 16
+            // columns, which must be the whole region (the duplex pass stages it)
+            const bool region_ok = DUPLEX ? T <= cap : cap == (((int64_t)T + 15) & ~(int64_t)15);
+            if ((g.flags & 4) || !aligned || R > kFastMaxR || span > kStageElems || T > kFastMaxT || !region_ok ||
                 !a.fast_ok || base_al + span >= 0xFFFFF000ll) {
                 kind = 1;
             } else {
@@ -2101,7 +2128,8 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     // reads a byte that is not a valid letter (d / e there are don't-care)
     lds_fence();
     if (DCR_ABL != 5) {                 // diagnostic 5: no per-column stores
-        const int T16 = (T + 15) & ~15;
+        // up to the region's end: the untrimmed T (k_recmeta) rounded to 16 columns
+        const int T16 = ((int)((m.w >> 7) & 255u) + 15) & ~15;
         const int c0 = 4 * lane;
         if (c0 < T16) {
             const uint2 w = *(const uint2 *)(ov + 8 * lane);
