@@ -67,7 +67,7 @@ struct dcr_ctx {
     dcr_params host_params{};
     // fast-kernel constants (fast_constants)
     uint32_t fast_kq = 0, fast_kqlo = 0;
-    int fast_maxq = 0, fast_t16 = 0;
+    int fast_maxq = 0, fast_t16 = 0, fast_r_safe = 0;
     uint16_t *d_llr16 = nullptr;   // device [128]
     int n_cu = 256;     // compute units (persistent grid size)
     int fast_blocks[4] = {1, 1, 1, 1};   // resident k_consensus_fast blocks per CU (ss, ds; exact ss, exact ds)
@@ -89,10 +89,16 @@ static int fast_allowed(const dcr_params *p) {
 //   llr16[q] = floor(16 ln(match[q] / mismatch[q]) - 1e-6)  (a lower bound; + 1 an upper one)
 //   t16      = ceil(16 ln(5 / cc)) + 1,  cc = min(qthresh[maxQ], 1 - threshold, 1/4)
 //   fast_qlo = the lowest quality from which every row has match >= mismatch > 0
+//   r_safe   = the most reads R with R c_max <= 700 nats, c_max bounding -ln of either factor of
+//              the rows a fast record can hold (q <= 122; the call's rows have q >= fast_qlo).
+//              ln L_b >= -R c_max, so up to r_safe reads the call's likelihood stays a normal
+//              double (e^-700 > DBL_MIN = e^-708.4).
+//              Above it the reference's products can underflow to 0 (S = 0, NaN posterior, call
+//              'A' :613), which the LLR bound does not see: every column then takes the exact path.
 // Returns 0 when the decision cannot be made for these parameters (then every
 // record takes the general kernel).
 static int fast_constants(const dcr_params &hp, uint16_t llr16[128], uint32_t &kq, uint32_t &kqlo, int &maxq,
-                          int &t16) {
+                          int &t16, int &r_safe) {
     const int mb = std::min(std::max(hp.min_base_quality, 0), 255);
     kq = (uint32_t)(255 - mb) * 0x01010101u;
     maxq = hp.max_base_quality;
@@ -111,12 +117,19 @@ static int fast_constants(const dcr_params &hp, uint16_t llr16[128], uint32_t &k
     const double cc = std::min(std::min(hp.qthresh[mq], 1.0 - hp.post_threshold), 0.25);
     if (!(cc > 1e-12)) return 0;
     t16 = (int)std::ceil(16.0 * std::log(5.0 / cc)) + 1;
+    double cmax = 0.0;                                 // per-row bound on -ln(factor), either factor
+    for (int q = 0; q <= 122; ++q) {
+        cmax = std::max(cmax, -std::log(hp.mismatch[q]));
+        if (q >= qlo) cmax = std::max(cmax, -std::log(hp.match[q]));
+    }
+    r_safe = cmax > 0.0 ? (int)std::min(1e6, std::floor(700.0 / cmax)) : 1000000;
     return 1;
 }
 
 static int upload_fast(dcr_ctx *c, const dcr_params *params) {
     uint16_t llr[128];
-    const int ok = fast_constants(*params, llr, c->fast_kq, c->fast_kqlo, c->fast_maxq, c->fast_t16);
+    const int ok = fast_constants(*params, llr, c->fast_kq, c->fast_kqlo, c->fast_maxq, c->fast_t16,
+                                 c->fast_r_safe);
     c->fast_ok = fast_allowed(params) && ok;
     if (hipMemcpy(c->d_llr16, llr, sizeof(llr), hipMemcpyHostToDevice) != hipSuccess)
         return fail(DCR_EHIP, "fast-kernel table upload failed");
@@ -303,6 +316,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         f.kqlo = c->fast_kqlo;
         f.maxq = c->fast_maxq;
         f.t16 = c->fast_t16;
+        f.r_safe = c->fast_r_safe;
         f.llr16 = c->d_llr16;
         return f;
     };

@@ -77,6 +77,7 @@ struct FastArgs {
     uint32_t kqlo;                  // bytes 0x80 - fast_qlo (lowest quality with 1-p' >= p'/5 upward)
     int maxq;
     int t16;                        // decision margin in 1/16 nat (dcr_capi.hip: fast_constants)
+    int r_safe;                     // most reads for which no decided column's L_b can underflow
     const uint16_t *llr16;          // [123] per-quality LLR term, 1/16 nat, rounded down
 };
 

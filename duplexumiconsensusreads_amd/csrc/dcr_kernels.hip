@@ -1997,6 +1997,8 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     const double *invd = (const double *)(lds + fk::kInvD);
     uint8_t *ov = lds + ov_addr;
     uint32_t und = 0;                  // bit tt: the lane's live column is not decided
+    // more reads than r_safe: L_b may underflow (fast_constants), no column is decided here
+    const bool force = R > a.r_safe;
     int dmax = -1, dmin = 0x7fffffff;
     double ex[NT];                     // e/d of the lane's column (0 outside T)
 #pragma unroll
@@ -2018,7 +2020,7 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         const int nb = (int)__builtin_amdgcn_ubfe(cnt, 6u * kb + 6u, 6u);
         const int e = R - nb;                                                     // rows that differ from the call
         // decided: LLR_b - max(LLR_k, 0) >= (Lb - L2 - (d - nb)) / 16 >= T16 / 16
-        const bool undecided = (int)(Lb - L2) - (d - nb) < a.t16;
+        const bool undecided = (int)(Lb - L2) - (d - nb) < a.t16 || force;
         und |= (uint32_t)(live && undecided) << tt;
         const double etv = (double)e * invd[d];                      // e/d to 1 ulp (the mean's decision
                                                                      // tolerates 1e-9; the exact walk divides)

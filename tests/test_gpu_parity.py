@@ -154,3 +154,37 @@ def test_gpu_deep_insertion_columns_many_classes(ctx):
     got = ctx.run_host(packed)
     want = dcr_oracle_c.run(packed, params, n_threads=8)
     assert_same(packed, got, want)
+
+
+@pytest.mark.parametrize("maxq", [60, 93])
+def test_gpu_underflow_columns(ctx, maxq):
+    """Deep high-quality columns where the reference's products underflow:
+    one 'G' row beside 62 sequenced 'N' rows at maxQ gives L = 0 for every
+    class, a NaN posterior and the call 'A' (:603-618) although the LLR bound
+    would decide 'G'; and a 4-way split of 60 rows (18/15/15/12) at Q93 whose
+    call likelihood underflows.  Records above r_safe take the exact path."""
+    L = 40
+    packed = synth.packed_fixed_size(4, sub_size=63, read_len=L, seed=3)
+    packed.quals[:] = maxq
+    n_sub = len(packed.sub_off) - 1
+    for s in range(n_sub):
+        g0 = int(packed.sub_off[s])
+        b0 = int(packed.seq_off[g0])
+        tmpl = packed.bases[b0:b0 + L].copy()
+        for r in range(63):
+            o = int(packed.seq_off[g0 + r])
+            packed.bases[o:o + L] = tmpl
+        if s % 2 == 0:
+            packed.bases[b0 + 10] = ord("G")
+            for r in range(1, 63):
+                packed.bases[int(packed.seq_off[g0 + r]) + 10] = ord("N")
+        else:
+            col = b"G" * 18 + b"A" * 15 + b"T" * 15 + b"C" * 12 + b"N" * 3
+            for r in range(63):
+                packed.bases[int(packed.seq_off[g0 + r]) + 20] = col[r]
+    params = ConsensusParams(max_base_quality=maxq, max_reads=1000)
+    ctx.set_params(params)
+    got = ctx.run_host(packed)
+    want = dcr_oracle_c.run(packed, params, n_threads=8)
+    assert want[0].record(0, packed.ss_col_off)["seq"][10] == "A"
+    assert_same(packed, got, want)
