@@ -64,11 +64,13 @@ struct dcr_ctx {
     int64_t last_reads = 0;
     bool timed = false;
     int fast_ok = 0;    // fast_allowed(): the fast kernel may take records
+    int wide_ok = 0;    // the general kernel's decision pass may run (wide_table)
     dcr_params host_params{};
     // fast-kernel constants (fast_constants)
     uint32_t fast_kq = 0, fast_kqlo = 0;
     int fast_maxq = 0, fast_t16 = 0, fast_r_safe = 0;
     uint16_t *d_llr16 = nullptr;   // device [128]
+    uint32_t *d_wtab = nullptr;    // device [DCR_LUT_N] (general kernel's decision pass)
     int n_cu = 256;     // compute units (persistent grid size)
     int fast_blocks[4] = {1, 1, 1, 1};   // resident k_consensus_fast blocks per CU (ss, ds; exact ss, exact ds)
 };
@@ -126,12 +128,43 @@ static int fast_constants(const dcr_params &hp, uint16_t llr16[128], uint32_t &k
     return 1;
 }
 
+// The general kernel's decision pass (dcr_kernels.hip: decide_record) per LUT
+// row v (quality byte, '+' 256, '-' 257):
+//   bits 0-15   llr16 = floor(16 ln(match[v] / mismatch[v]) - 1e-6), a lower bound
+//   bits 16-30  z16   = ceil(16 (-ln mismatch[v]) + 1e-6), an upper bound
+//   bit 31      the row cannot be a call's row (quality above 122 or below fast_qlo, '+')
+// Returns 0 when some z16 does not fit (then the pass is not used).
+static int wide_table(const dcr_params &hp, uint32_t wtab[DCR_LUT_N]) {
+    int qlo = 123;
+    while (qlo > 0 && hp.mismatch[qlo - 1] > 0.0 && hp.match[qlo - 1] >= hp.mismatch[qlo - 1]) --qlo;
+    for (int v = 0; v < DCR_LUT_N; ++v) {
+        const double mm = hp.mismatch[v], m = hp.match[v];
+        if (!(mm > 0.0)) return 0;
+        const double z = std::ceil(-16.0 * std::log(mm) + 1e-6);
+        if (!(z >= 0.0 && z <= 32767.0)) return 0;
+        uint32_t w = (uint32_t)z << 16;
+        const bool call_row = v == DCR_LUT_DEL ? m >= mm : (v >= qlo && v <= 122);
+        if (call_row) {
+            const double l = std::floor(16.0 * std::log(m / mm) - 1e-6);
+            if (!(l <= 1040.0)) return 0;
+            w |= (uint32_t)std::max(l, 0.0);
+        } else {
+            w |= 1u << 31;
+        }
+        wtab[v] = w;
+    }
+    return 1;
+}
+
 static int upload_fast(dcr_ctx *c, const dcr_params *params) {
     uint16_t llr[128];
+    uint32_t wtab[DCR_LUT_N];
     const int ok = fast_constants(*params, llr, c->fast_kq, c->fast_kqlo, c->fast_maxq, c->fast_t16,
                                  c->fast_r_safe);
     c->fast_ok = fast_allowed(params) && ok;
-    if (hipMemcpy(c->d_llr16, llr, sizeof(llr), hipMemcpyHostToDevice) != hipSuccess)
+    c->wide_ok = c->fast_ok && wide_table(*params, wtab);
+    if (hipMemcpy(c->d_llr16, llr, sizeof(llr), hipMemcpyHostToDevice) != hipSuccess ||
+        (c->wide_ok && hipMemcpy(c->d_wtab, wtab, sizeof(wtab), hipMemcpyHostToDevice) != hipSuccess))
         return fail(DCR_EHIP, "fast-kernel table upload failed");
     return DCR_OK;
 }
@@ -169,7 +202,8 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_params, sizeof(dcr_params)) != hipSuccess ||
-        hipMalloc(&c->d_llr16, 128 * sizeof(uint16_t)) != hipSuccess) {
+        hipMalloc(&c->d_llr16, 128 * sizeof(uint16_t)) != hipSuccess ||
+        hipMalloc(&c->d_wtab, DCR_LUT_N * sizeof(uint32_t)) != hipSuccess) {
         fail(DCR_EHIP, "context allocation failed");
         delete c;
         return nullptr;
@@ -202,6 +236,7 @@ void dcr_destroy(dcr_ctx *c) {
     c->io.release();
     if (c->d_params) (void)hipFree(c->d_params);
     if (c->d_llr16) (void)hipFree(c->d_llr16);
+    if (c->d_wtab) (void)hipFree(c->d_wtab);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -283,6 +318,8 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     a.ss = *ss;
     a.ds = *ds;
     a.fast_ok = c->fast_ok;
+    a.t16 = c->wide_ok ? c->fast_t16 : -1;     // -1: no decision pass
+    a.wtab = c->d_wtab;
     // per strand: k_recmeta classifies every record (fast list / general list /
     // status written), then the fast kernel (8 records per wave) drains the fast list and
     // the persistent general kernel the rest (insertions, > 64 reads, wide layouts)
@@ -336,16 +373,19 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL((dcr::k_consensus_fast<true, true>), dim3(gx), dim3(dcr::kFastBlock), 0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[2], c->stream));
+            hipLaunchKernelGGL(dcr::k_decide<true>, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
             hipLaunchKernelGGL(dcr::k_consensus_general<true>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
                                c->stream, a);
         } else {
             hipLaunchKernelGGL(dcr::k_recmeta<false>, dim3(nb), dim3(256), 0, c->stream, a);
+            hipLaunchKernelGGL(dcr::k_prep_big, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
             HIP_TRY(hipEventRecord(ev[0], c->stream));
             hipLaunchKernelGGL((dcr::k_consensus_fast<false, false>), dim3(fast_grid(a.n_rec, 0)),
                                dim3(dcr::kFastBlock), 0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL((dcr::k_consensus_fast<false, true>), dim3(gx), dim3(dcr::kFastBlock), 0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[2], c->stream));
+            hipLaunchKernelGGL(dcr::k_decide<false>, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
             hipLaunchKernelGGL(dcr::k_consensus_general<false>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
                                c->stream, a);
         }

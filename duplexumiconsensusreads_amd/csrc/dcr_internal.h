@@ -54,6 +54,8 @@ struct Args {
     dcr_out ds;
     int64_t n_rec;
     int fast_ok;            // fast_allowed() (dcr_capi.hip): the fast kernel may take records
+    int t16;                // decision margin in 1/16 nat (fast_constants)
+    const uint32_t *wtab;   // [DCR_LUT_N] per LUT row: LLR term | -ln(p'/5) bound << 16 | not-a-call-row << 31
 };
 
 // the fast kernel's compact arguments (one strand; fewer scalar registers than Args)
@@ -83,7 +85,9 @@ struct FastArgs {
 
 __global__ void k_prep(dcr_batch in, const dcr_params *P, Workspace ws);
 template <bool DUPLEX> __global__ void k_recmeta(Args a);
+__global__ void k_prep_big(Args a);
 template <bool DUPLEX, bool EXACT> __global__ void k_consensus_fast(FastArgs a);
 template <bool DUPLEX> __global__ void k_consensus_general(Args a);
+template <bool DUPLEX> __global__ void k_decide(Args a);
 
 }  // namespace dcr

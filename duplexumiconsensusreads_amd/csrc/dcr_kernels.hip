@@ -635,6 +635,183 @@ __device__ __forceinline__ ColOut finalize(const Acc &A, int nsw, int R, bool in
     return o;
 }
 
+// ------------------------------------------------- decision pass (general)
+// The fast kernel's integer decision (see k_consensus_fast below), for the
+// general kernel's records without insertion columns: any number of reads,
+// reads of one M run or of M D M runs ('-' rows), T <= 256.  Per column:
+// 32-bit sums of the rounded-down LLR terms of A T C G '-', row counts and
+// Z = the rounded-up sum of -ln(p'/5) over every row.  A column is decided
+// when L_b - L_2nd - n_other >= T16 (the call is b with quality maxQ, unmasked)
+// and Z - L_b <= 16 * 700: ln L_b = LLR_b - sum(-ln(p'/5)) >= -700, so the
+// reference's product L_b stays a normal double (no underflow to a NaN
+// posterior, :603-618).
+//
+// The sums are order-free, so reads are visited in staging order: the bytes of
+// the record's reads (contiguous in HBM) go through the wave's LDS stage as
+// element codes, 2 KiB per round trip (dword loads, 16 per lane), and every
+// read in the stage adds its row to all NT column tiles (lane = column).
+// Writes kb | d << 3 | e << 15 per column into `cw` and returns true when every
+// column is decided; false (the caller then runs the reference's double
+// arithmetic) on any undecided column, an invalid letter, a row quality the
+// bound does not cover, or another read layout.
+struct DecideAcc {
+    uint32_t s[5];          // LLR sums A T C G '-'
+    uint32_t n[6];          // rows A T C G '-' N
+    uint32_t z;
+};
+
+template <bool DUPLEX, int NT>
+__device__ bool decide_tiles(const Args &a, const int64_t rec, const int R, const int T, const int minpos,
+                             int32_t *cw, uint16_t *stage, const uint32_t *s_wtab, const int lane) {
+    const int minbq = a.P->min_base_quality;
+    const uint8_t *gb = DUPLEX ? a.ss.seq : a.in.bases;
+    const uint8_t *gq = DUPLEX ? a.ss.qual : a.in.quals;
+    DecideAcc A[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) A[tt].s[k] = 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) A[tt].n[k] = 0;
+        A[tt].z = 0;
+    }
+    bool bad = false;
+    for (int cb = 0; cb < R; cb += kWave) {
+        // lane r: read cb + r -- first column, kept length, first byte, and
+        // the runs M a1, D b1 (a1 = len, b1 = 0 for one M run)
+        int col = 0, len = 0, a1 = 0, b1 = 0;
+        int64_t ss = 0;
+        bool other = false;
+        const int nr = min(kWave, R - cb);
+        if (lane < nr) {
+            const ReadRef rd = get_read<DUPLEX>(a, rec, cb + lane);
+            col = rd.pos - minpos;
+            len = rd.len;
+            ss = rd.seq_start;
+            a1 = len;
+            if (rd.ncig == 3) {
+                const uint32_t r0 = rd.cig[0], r1 = rd.cig[1], r2 = rd.cig[2];
+                other = (r0 & 15u) != 0 || (r1 & 15u) != 2 || (r2 & 15u) != 0;
+                a1 = (int)(r0 >> 4);
+                b1 = (int)(r1 >> 4);
+            } else {
+                other = rd.ncig != 1 || (rd.cig[0] & 15u) != 0;
+            }
+            other |= len > kStageElems - 4;
+        }
+        if (__ballot(other)) return false;
+        int rr = 0;                                   // reads of this chunk done
+        while (rr < nr) {
+            // stage [base, base + 2 KiB): the reads rr.. that end inside it
+            const int64_t base = (int64_t)(((uint64_t)(uint32_t)readlane((int)((uint64_t)ss >> 32), rr) << 32) |
+                                           (uint32_t)readlane((int)(uint32_t)ss, rr)) & ~(int64_t)3;
+            const bool in = lane >= rr && lane < nr && ss + len - base <= kStageElems;
+            const uint64_t fm = ~__ballot(in) >> rr;      // first read past the stage
+            const int nfit = fm ? min((int)__builtin_ctzll(fm), nr - rr) : nr - rr;
+            const int rlast = rr + nfit - 1;
+            const int64_t ssl = (int64_t)(((uint64_t)(uint32_t)readlane((int)((uint64_t)ss >> 32), rlast) << 32) |
+                                          (uint32_t)readlane((int)(uint32_t)ss, rlast));
+            const int span = (int)(ssl + readlane(len, rlast) - base);
+            const int nd = (span + 3) >> 2;
+            const uint32_t *b4 = (const uint32_t *)(gb + base);
+            const uint32_t *q4 = (const uint32_t *)(gq + base);
+            uint32_t vb[kStageElems / 4 / kWave], vq[kStageElems / 4 / kWave];
+#pragma unroll
+            for (int u = 0; u < kStageElems / 4 / kWave; ++u) {
+                const int d = u * kWave + lane;
+                vb[u] = d < nd ? b4[d] : 0u;
+                vq[u] = d < nd ? q4[d] : 0u;
+            }
+            wave_fence();                             // the previous stage's readers are done
+#pragma unroll
+            for (int u = 0; u < kStageElems / 4 / kWave; ++u) {
+                const int d = u * kWave + lane;
+                if (d < nd) {
+                    uint32_t cc[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        cc[k] = make_code<DUPLEX>((vb[u] >> (8 * k)) & 255u, (vq[u] >> (8 * k)) & 255u, minbq);
+                    *(uint2 *)&stage[4 * d] = make_uint2(cc[0] | (cc[1] << 16), cc[2] | (cc[3] << 16));
+                }
+            }
+            wave_fence();
+            for (int r = rr; r <= rlast; ++r) {
+                const int cr = readlane(col, r), lr = readlane(len, r);
+                const int ar = readlane(a1, r), br = readlane(b1, r);
+                const int so = (int)((int64_t)(((uint64_t)(uint32_t)readlane((int)((uint64_t)ss >> 32), r) << 32) |
+                                               (uint32_t)readlane((int)(uint32_t)ss, r)) - base);
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt) {
+                    const int t = 64 * tt + lane;
+                    const int j = t - cr;
+                    const bool del = j >= ar && j < ar + br;
+                    const int is = j < ar ? j : j - br;
+                    uint32_t e;
+                    if (t >= T || j < 0 || (del ? ar : is) >= lr) e = kPad;   // is >= len: pad (:514, :540)
+                    else e = del ? kDel : (uint32_t)stage[so + is];
+                    const uint32_t cls = e >> 9;
+                    const uint32_t w = s_wtab[e & 511u];
+                    bad |= cls == 7 || (cls != 6 && (w >> 31) != 0);
+                    const uint32_t l = w & 0xFFFFu;
+                    A[tt].s[0] += cls == 0 ? l : 0u;
+                    A[tt].s[1] += cls == 1 ? l : 0u;
+                    A[tt].s[2] += cls == 2 ? l : 0u;
+                    A[tt].s[3] += cls == 3 ? l : 0u;
+                    A[tt].s[4] += cls == 5 ? l : 0u;
+                    A[tt].z += (w >> 16) & 0x7FFFu;
+                    A[tt].n[0] += cls == 0;
+                    A[tt].n[1] += cls == 1;
+                    A[tt].n[2] += cls == 2;
+                    A[tt].n[3] += cls == 3;
+                    A[tt].n[4] += cls == 5;
+                    A[tt].n[5] += cls == 6;
+                }
+            }
+            if (__ballot(bad)) return false;
+            rr += nfit;
+        }
+    }
+    bool undecided = false;
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+        const int t = 64 * tt + lane;
+        const uint32_t S[5] = {A[tt].s[0], A[tt].s[1], A[tt].s[2], A[tt].s[3], A[tt].s[4]};
+        const uint32_t N[6] = {A[tt].n[0], A[tt].n[1], A[tt].n[2], A[tt].n[3], A[tt].n[4], A[tt].n[5]};
+        // the first largest in the reference's order A T C G + - ('+' absent: 0)
+        uint32_t Lb = S[0], kb = 0, nb = N[0];
+        if (S[1] > Lb) { Lb = S[1]; kb = 1; nb = N[1]; }
+        if (S[2] > Lb) { Lb = S[2]; kb = 2; nb = N[2]; }
+        if (S[3] > Lb) { Lb = S[3]; kb = 3; nb = N[3]; }
+        if (S[4] > Lb) { Lb = S[4]; kb = 5; nb = N[4]; }
+        uint32_t L2 = 0;
+        L2 = max(L2, kb != 0 ? S[0] : 0u);
+        L2 = max(L2, kb != 1 ? S[1] : 0u);
+        L2 = max(L2, kb != 2 ? S[2] : 0u);
+        L2 = max(L2, kb != 3 ? S[3] : 0u);
+        L2 = max(L2, kb != 5 ? S[4] : 0u);
+        const int d = R - (int)N[5];                     // rows not 'N' ('-' counts, :1001)
+        const int e = R - (int)nb;                       // rows != the call (:1011)
+        const bool ok = (int)(Lb - L2) - (d - (int)nb) >= a.t16 && (int)A[tt].z - (int)Lb <= 16 * 700;
+        if (t < T) {
+            undecided |= !ok;
+            cw[t] = (int32_t)(kb | ((uint32_t)d << 3) | ((uint32_t)e << 15));
+        }
+    }
+    return __ballot(undecided) == 0;
+}
+
+template <bool DUPLEX>
+__device__ bool decide_record(const Args &a, const int64_t rec, const int R, const int T, const int minpos,
+                              int32_t *cw, uint16_t *stage, const uint32_t *s_wtab, const int lane) {
+    const uint8_t *gb = DUPLEX ? a.ss.seq : a.in.bases;
+    const uint8_t *gq = DUPLEX ? a.ss.qual : a.in.quals;
+    if (a.t16 < 0 || R > 4095 || T > 256 || T <= 0 || ((((uintptr_t)gb) | ((uintptr_t)gq)) & 3) != 0) return false;
+    if (T <= 64) return decide_tiles<DUPLEX, 1>(a, rec, R, T, minpos, cw, stage, s_wtab, lane);
+    if (T <= 128) return decide_tiles<DUPLEX, 2>(a, rec, R, T, minpos, cw, stage, s_wtab, lane);
+    if (T <= 192) return decide_tiles<DUPLEX, 3>(a, rec, R, T, minpos, cw, stage, s_wtab, lane);
+    return decide_tiles<DUPLEX, 4>(a, rec, R, T, minpos, cw, stage, s_wtab, lane);
+}
+
 // --------------------------------------------------- per-read register view
 // lane r of these registers holds read r (R <= 64); read back with readlane
 struct LaneReads {
@@ -649,7 +826,7 @@ struct LaneReads {
 // and processed by the general kernel.
 template <bool DUPLEX, bool FAST>
 __device__ __forceinline__ void process_record(const Args &a, const int64_t rec, WaveLds &W, const double2 *s_lut,
-                                               const double *s_qthr, const int lane) {
+                                               const double *s_qthr, const bool dec, const int lane) {
     const dcr_params *P = a.P;
 
     const dcr_out &O = DUPLEX ? a.ds : a.ss;
@@ -766,9 +943,14 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
         }
     }
 
+    // ---- k_decide proved every column's call from integer LLR bounds: the
+    // tiles below take call / d / e from its column words instead of forming
+    // the products
+    const bool decided = !FAST && dec;
+
     // ---- phase 0: element codes into LDS (every record whose bytes fit: the
     // fast layout reads them by column, the insertion layout by read)
-    if (fits) {
+    if (fits && !decided) {
 #pragma unroll
         for (int u = 0; u < kStageDw; ++u) {
             const int d = u * kWave + lane;
@@ -860,7 +1042,9 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
         Acc A;
         acc_init(A);
         bool ins_col = false;
-        if (staged) {
+        if (decided) {
+            // the call, d and e of a decided column; quality maxQ (kb: A T C G + -)
+        } else if (staged) {
             // fast layout from LDS: op index j = t - col of read r (:473-545 without I)
             auto src = [&](int r) -> uint32_t {
                 const int cl = readlane(lr.cl, r);
@@ -938,13 +1122,23 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
                 wave_fence();
             }
         }
-        nbad += live ? A.nbad : 0;
-        const int nsw = wave_max(A.ns);
-        if (DCR_ABL == 2) {
-            if (live) cons[t] = (int)(A.U * 1e9) + nsw + A.n[0];
-            continue;
+        ColOut co;
+        if (decided) {
+            const uint32_t w = live ? (uint32_t)a.ws.cons[off + t] : 0u;
+            co.ch = (int)((0x2D2B47435441ull >> (8 * (w & 7u))) & 0xffu);   // "ATCG+-"
+            co.q = P->max_base_quality;
+            co.d = (int)((w >> 3) & 4095u);
+            co.e = (int)((w >> 15) & 4095u);
+            co.overflow = false;
+        } else {
+            nbad += live ? A.nbad : 0;
+            const int nsw = wave_max(A.ns);
+            if (DCR_ABL == 2) {
+                if (live) cons[t] = (int)(A.U * 1e9) + nsw + A.n[0];
+                continue;
+            }
+            co = finalize(A, nsw, R, ins_col, P, s_qthr, simple_q);
         }
-        const ColOut co = finalize(A, nsw, R, ins_col, P, s_qthr, simple_q);
         if (live) {
             cons[t] = co.ch | (co.q << 8);
             qoverflow |= co.overflow;
@@ -1606,14 +1800,30 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
     if (kind == 0) a.ws.meta[basef + __popcll(bf & lt)] = m;
     if (kind == 1) a.ws.ovf[baseg + __popcll(bg & lt)] = (int)rk;
     // single-strand reads of records the fast kernel does not take need the full
-    // preprocessing (3' trim included) for the general kernel and the host
-    if (DUPLEX || __ballot(vk && kind != 0) == 0) return;
+    // preprocessing (3' trim included) for the general kernel and the host;
+    // records of more than 64 reads are left to k_prep_big (a block per record,
+    // not one wave walking every read of 64 records)
+    if (!DUPLEX) agg[lane].kind = (vk && R > kWave) ? 2 : kind;
+    if (DUPLEX || __ballot(vk && kind != 0 && R <= kWave) == 0) return;
     lds_fence();
     carry = -1;
     for (int64_t c = gbeg; c < gend; c += kWave) {
         const int k = read_record(c, g0, R, mark, lane, carry);
         const int64_t gr = c + lane;
-        if (gr < gend && agg[k].kind != 0) prep_read(a.in, a.P, a.ws, gr);
+        if (gr < gend && agg[k].kind != 0 && agg[k].kind != 2) prep_read(a.in, a.P, a.ws, gr);
+    }
+}
+
+// per-read preprocessing of the general list's records of more than 64 reads
+// (k_recmeta leaves them out): one block per record, 256 reads at a time
+__global__ __launch_bounds__(256) void k_prep_big(Args a) {
+    const int n = a.ws.ovf_count[0];
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int64_t rec = a.ws.ovf[i];
+        const int g0 = a.in.sub_off[rec];
+        const int R = a.in.sub_off[rec + 1] - g0;
+        if (R <= kWave) continue;
+        for (int r = threadIdx.x; r < R; r += blockDim.x) prep_read(a.in, a.P, a.ws, g0 + r);
     }
 }
 
@@ -2387,8 +2597,48 @@ __global__ __launch_bounds__(kBlock, 2) void k_consensus_general(Args a) {
     const int n = a.ws.ovf_count[DUPLEX ? 1 : 0];
     const int nw = gridDim.x * kWavesPerBlock;
     for (int i = blockIdx.x * kWavesPerBlock + wave; i < n; i += nw) {
+        const int v = a.ws.ovf[i];                  // bit 31: k_decide decided every column
+        process_record<DUPLEX, false>(a, v & 0x7fffffff, s_wave[wave], s_lut, s_qthr, v < 0, threadIdx.x & 63);
+    }
+}
+
+// decision pass over the general list (decide_record), one wave per record:
+// marks the records whose every column it decides (ovf entry | bit 31) and
+// leaves their column words in the workspace column scratch (ws.cons)
+template <bool DUPLEX>
+__global__ __launch_bounds__(256) void k_decide(Args a) {
+    __shared__ uint32_t s_wtab[DCR_LUT_N];
+    __shared__ __attribute__((aligned(16))) uint16_t s_stage[kWavesPerBlock][kStageElems];
+    if (a.t16 < 0) return;
+    for (int i = threadIdx.x; i < DCR_LUT_N; i += kBlock) s_wtab[i] = a.wtab[i];
+    __syncthreads();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int n = a.ws.ovf_count[DUPLEX ? 1 : 0];
+    const int nw = gridDim.x * kWavesPerBlock;
+    for (int i = blockIdx.x * kWavesPerBlock + wave; i < n; i += nw) {
         const int64_t rec = a.ws.ovf[i];
-        process_record<DUPLEX, false>(a, rec, s_wave[wave], s_lut, s_qthr, threadIdx.x & 63);
+        const int R = DUPLEX ? 2 : (a.in.sub_off[rec + 1] - a.in.sub_off[rec]);
+        if (R <= 0) continue;
+        int minpos = 0x7fffffff, maxend = -0x7fffffff, up = 0;
+        for (int c = 0; c < R; c += kWave) {
+            const int r = c + lane;
+            if (r < R) {
+                const ReadRef rd = get_read<DUPLEX>(a, rec, r);
+                up |= rd.status != 0 || rd.len <= 0;
+                if (!DUPLEX) up |= a.ws.info[a.in.sub_off[rec] + r].has_ins;
+                minpos = min(minpos, rd.pos);
+                maxend = max(maxend, rd.pos + rd.len);
+            }
+        }
+        if (__ballot(up)) continue;
+        minpos = wave_min(minpos);
+        const int T = wave_max(maxend) - minpos;          // :458-459
+        const int64_t *col_off = DUPLEX ? a.in.ds_col_off : a.in.ss_col_off;
+        const int64_t off = col_off[rec];
+        if (T > col_off[rec + 1] - off) continue;
+        if (decide_record<DUPLEX>(a, rec, R, T, minpos, a.ws.cons + off, s_stage[wave], s_wtab, lane) && lane == 0)
+            a.ws.ovf[i] = (int)rec | (int)0x80000000u;
     }
 }
 
@@ -2399,6 +2649,8 @@ template __global__ void k_consensus_fast<true, false>(FastArgs);
 template __global__ void k_consensus_fast<false, true>(FastArgs);
 template __global__ void k_consensus_fast<true, true>(FastArgs);
 template __global__ void k_consensus_general<false>(Args);
+template __global__ void k_decide<false>(Args);
+template __global__ void k_decide<true>(Args);
 template __global__ void k_consensus_general<true>(Args);
 
 }  // namespace dcr
