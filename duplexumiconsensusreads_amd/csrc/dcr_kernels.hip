@@ -58,7 +58,8 @@ constexpr uint32_t kDel = (5u << 9) | DCR_LUT_DEL;
 struct WaveLds {
     uint16_t pad_code[4];                  // [0] = kPad: sentinel the fast layout loads outside a read (8 B keeps stage 8-aligned)
     uint16_t stage[kStageElems];           // element codes of the record's bytes (records that fit)
-    uint16_t tile[kWave][kTileIns];        // insertion layout: 64 reads x 32 columns
+    uint16_t tile[kWave][kTileIns + 2];    // insertion layout: 64 reads x 32 columns (rows padded to 17 dwords:
+                                           // a column write by 64 lanes hits distinct banks)
     int32_t cons[kColsLds];
     double et[kColsLds];
     // uniform stack of the pairwise-sum walk (phase 3)
@@ -109,6 +110,13 @@ __device__ __forceinline__ int readlane(int v, int l) { return __builtin_amdgcn_
 // wave-local ordering of global/LDS traffic between phases of one wavefront
 __device__ __forceinline__ void wave_fence() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// wave-local LDS ordering: a wave's DS instructions execute in order, so only
+// the compiler must be kept from reordering (no vmcnt drain of prefetches)
+__device__ __forceinline__ void lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -291,23 +299,29 @@ __device__ __forceinline__ uint32_t base_elem(const ReadRef &rd, int is, int min
 // lane = read.  Mirrors idx_cigar / idx_seq (:465-466) with run-length CIGAR.
 struct Sim {
     int k, o, is, curop, curlen;
+    uint32_t nxt;         // run k + 1, loaded one transition ahead (0: none)
 };
 
-__device__ __forceinline__ void sim_load_run(Sim &s, const ReadRef &rd) {
+__device__ __forceinline__ void sim_set_run(Sim &s, const ReadRef &rd, uint32_t v) {
     if (s.k < rd.ncig) {
-        const uint32_t v = rd.cig[s.k];
         s.curop = v & 15;
         s.curlen = v >> 4;
     } else {
         s.curop = -1;     // exhausted: get_current_CIGAR_operations reports 0 (:424-425)
         s.curlen = 0;
     }
+    s.nxt = s.k + 1 < rd.ncig ? rd.cig[s.k + 1] : 0u;
 }
+__device__ __forceinline__ void sim_load_run(Sim &s, const ReadRef &rd) {
+    sim_set_run(s, rd, s.k < rd.ncig ? rd.cig[s.k] : 0u);
+}
+// the next run comes from the register loaded at the previous transition, so a
+// column step never waits on HBM for it
 __device__ __forceinline__ void sim_advance(Sim &s, const ReadRef &rd) {
     if (++s.o == s.curlen) {
         ++s.k;
         s.o = 0;
-        sim_load_run(s, rd);
+        sim_set_run(s, rd, s.nxt);
     }
 }
 
@@ -920,6 +934,13 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
     }
 
     const bool cols_lds = T <= kColsLds;
+    // ordering of the record's scratch between lanes: LDS only (wave-local DS
+    // order) when the columns live in LDS, else also the global scratch (a
+    // vmcnt drain, which also waits for every output store in flight)
+    auto sfence = [&]() {
+        if (cols_lds) lds_fence();
+        else wave_fence();
+    };
     int32_t *cons = cols_lds ? W.cons : a.ws.cons + off;
     double *et = cols_lds ? W.et : a.ws.et + off;
     uint16_t *od = O.d + off;
@@ -933,6 +954,8 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
 
     const bool big = R > kWave;
     const bool staged = fits && !ins;
+    if (DCR_ABL == 9 && ins && big) return;       // diagnostic: general kernel without the > 64-read insertion layout
+    if (DCR_ABL == 10 && ins && !big) return;     // diagnostic: ... without the <= 64-read insertion layout
     if constexpr (FAST) {
         if (!staged || !cols_lds) {          // general kernel takes it
             if (lane == 0) {
@@ -965,7 +988,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
                 *(uint2 *)&W.stage[4 * d] = w;
             }
         }
-        wave_fence();
+        sfence();
     }
     if (DCR_ABL == 1) {
         if (lane == 0) O.pos[rec] = minpos + nd + (int)W.stage[lane];
@@ -980,7 +1003,59 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
     // layout state in global scratch between column tiles.
     uint8_t *insflag = a.ws.insflag + off;
     int4 *gstate = DUPLEX ? nullptr : a.ws.state + a.in.sub_off[rec];
-    if (!FAST && ins && big && !DUPLEX) {
+    // up to kBigCh * 64 reads the layout state stays in registers (lane = read
+    // within 64-read chunk c): the flags pass walks the runs without touching
+    // HBM, and the tiles stage each chunk's next 32 bytes per read
+    constexpr int kBigCh = 4;
+    const bool regbig = !FAST && ins && big && !DUPLEX && R <= kBigCh * kWave;
+    struct SlimRead {
+        int pos, len, ncig;
+        const uint32_t *cig;
+        int64_t seq_start;
+    };
+    SlimRead brd[kBigCh];
+    Sim bs[kBigCh];
+    auto slim_ref = [&](const SlimRead &b) {
+        ReadRef rd{};
+        rd.pos = b.pos;
+        rd.len = b.len;
+        rd.ncig = b.ncig;
+        rd.cig = b.cig;
+        rd.seq_start = b.seq_start;
+        return rd;
+    };
+    if (regbig) {
+#pragma unroll
+        for (int c = 0; c < kBigCh; ++c) {
+            brd[c] = SlimRead{0x7fffffff, 0, 0, nullptr, 0};
+            bs[c] = Sim{0, 0, 0, -1, 0, 0u};
+            const int r = c * kWave + lane;
+            if (c * kWave < R && r < R) {
+                const ReadRef rd = get_read<DUPLEX>(a, rec, r);
+                brd[c] = SlimRead{rd.pos, rd.len, rd.ncig, rd.cig, rd.seq_start};
+                sim_load_run(bs[c], rd);
+            }
+        }
+        for (int t = 0; t < T; ++t) {
+            bool any = false;
+#pragma unroll
+            for (int c = 0; c < kBigCh; ++c)
+                if (c * kWave < R) any |= __ballot(c * kWave + lane < R && bs[c].curop == 1) != 0;
+#pragma unroll
+            for (int c = 0; c < kBigCh; ++c)
+                if (c * kWave < R && c * kWave + lane < R)
+                    (void)sim_step_e<DUPLEX>(bs[c], slim_ref(brd[c]), minpos + t, any, idx_err,
+                                             [](int) { return 0u; });
+            if (lane == 0) insflag[t] = any;
+        }
+#pragma unroll
+        for (int c = 0; c < kBigCh; ++c) {
+            bs[c] = Sim{0, 0, 0, -1, 0, 0u};
+            if (c * kWave < R && c * kWave + lane < R) sim_load_run(bs[c], slim_ref(brd[c]));
+        }
+        wave_fence();
+    }
+    if (!FAST && ins && big && !DUPLEX && !regbig) {
         for (int c = 0; c < R; c += kWave) {
             const int r = c + lane;
             if (r < R) {
@@ -1033,6 +1108,37 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
     Sim sim{0, 0, 0, 0, 0};
     if (ins && !big && lane < R) sim_load_run(sim, myrd);
 
+    // the next 32 bytes of a read from seq index is0 (the most a 32-column tile
+    // consumes) as codes in the stage, [k][lane], from 9 range-checked dword
+    // loads per lane issued together (records whose bytes do not fit the stage)
+    auto stage_window = [&](bool on, int64_t seq_start, int is0) {
+        if (!on) return;
+        const int64_t o = seq_start + is0 - base_al;      // >= 0: base_al is the first read's byte
+        const int64_t left = (DUPLEX ? a.in.ss_cols : a.in.n_bases) - base_al;
+        const int nrec = (int)min(left, (int64_t)0x7FFFFFF0);
+        const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void *)(gb + base_al), (short)0, nrec,
+                                                                            0x00020000);
+        const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void *)(gq + base_al), (short)0, nrec,
+                                                                            0x00020000);
+        const int oa = (int)(o & ~(int64_t)3);
+        const uint32_t sh = (uint32_t)(o & 3);
+        uint32_t db[9], dq[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            db[i] = __builtin_amdgcn_raw_buffer_load_b32(rb, oa + 4 * i, 0, 0);
+            dq[i] = __builtin_amdgcn_raw_buffer_load_b32(rq, oa + 4 * i, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t wb = __builtin_amdgcn_alignbyte(db[i + 1], db[i], sh);
+            const uint32_t wq = __builtin_amdgcn_alignbyte(dq[i + 1], dq[i], sh);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                W.stage[((4 * i + j) << 6) + lane] =
+                    (uint16_t)make_code<DUPLEX>((wb >> (8 * j)) & 255u, (wq >> (8 * j)) & 255u, minbq);
+        }
+    };
+
     // ---- phases 1+2: column tiles (lane = column)
     const int tw = ins ? kTileIns : kWave;       // insertion layout: 32-column tiles
     for (int c0 = 0; c0 < T; c0 += tw) {
@@ -1080,6 +1186,15 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
             accumulate(A, R, src, s_lut);
         } else if (!big) {
             uint64_t insmask = 0;
+            // bytes that do not fit the stage: each read's next 32 bytes (the
+            // most a 32-column tile consumes) as codes in the stage, [k][lane],
+            // from 9 range-checked dword loads per lane issued together
+            const int is0 = sim.is;
+            if (!fits) {
+                sfence();
+                stage_window(lane < R, myrd.seq_start, is0);
+                sfence();
+            }
             for (int tt = 0; tt < ncol; ++tt) {
                 const bool isI = lane < R && sim.curop == 1;
                 const bool any = __ballot(isI) != 0;
@@ -1091,16 +1206,42 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
                         e = sim_step_e<DUPLEX>(sim, myrd, minpos + c0 + tt, any, idx_err,
                                                [&](int is) { return (uint32_t)W.stage[so + is]; });
                     } else {
-                        e = sim_step<DUPLEX>(sim, myrd, minpos + c0 + tt, any, minbq, idx_err);
+                        e = sim_step_e<DUPLEX>(sim, myrd, minpos + c0 + tt, any, idx_err,
+                                               [&](int is) { return (uint32_t)W.stage[((is - is0) << 6) + lane]; });
                     }
                     W.tile[lane][tt] = (uint16_t)e;
                 }
             }
-            wave_fence();
+            sfence();
             ins_col = live && ((insmask >> lane) & 1);
             auto src = [&](int r) -> uint32_t { return live ? (uint32_t)W.tile[r][lane & (kTileIns - 1)] : kPad; };
             accumulate(A, R, src, s_lut);
-            wave_fence();
+            sfence();
+        } else if (regbig) {
+            // this tile's insertion-column flags, one load per lane
+            const uint64_t fm = __ballot(lane < ncol && insflag[c0 + lane] != 0);
+            ins_col = live && ((fm >> lane) & 1);
+#pragma unroll
+            for (int c = 0; c < kBigCh; ++c) {
+                if (c * kWave >= R) continue;
+                const int nr = min(kWave, R - c * kWave);
+                const bool mine = lane < nr;
+                const int is0 = bs[c].is;
+                sfence();
+                stage_window(mine, brd[c].seq_start, is0);
+                sfence();
+                if (mine) {
+                    const ReadRef rd = slim_ref(brd[c]);
+                    for (int tt = 0; tt < ncol; ++tt)
+                        W.tile[lane][tt] = (uint16_t)sim_step_e<DUPLEX>(
+                            bs[c], rd, minpos + c0 + tt, ((fm >> tt) & 1) != 0, idx_err,
+                            [&](int is) { return (uint32_t)W.stage[((is - is0) << 6) + lane]; });
+                }
+                sfence();
+                auto src = [&](int rr) -> uint32_t { return live ? (uint32_t)W.tile[rr][lane & (kTileIns - 1)] : kPad; };
+                accumulate(A, nr, src, s_lut);
+            }
+            sfence();
         } else {
             ins_col = live && insflag[t];
             for (int c = 0; c < R; c += kWave) {
@@ -1174,7 +1315,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
     if (idx_err) { write_status(DCR_ST_INDEX_ERROR); return; }
     if (bad) { write_status(DCR_ST_EXIT_BADCHAR); return; }
     if (qoverflow) { write_status(DCR_ST_OVERFLOW_ERROR); return; }
-    wave_fence();
+    sfence();
 
     // ---- phase 3: adjust_consensus_fields (:745-871) over [first, last]
     const int lo = first < 0 ? T : first;
@@ -1261,7 +1402,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
             oseq[i] = 'N';
             oqual[i] = 0;
         }
-    wave_fence();
+    sfence();
     for (int i0 = 0; i0 < nruns; i0 += kWave) {
         const int i = i0 + lane;
         uint32_t v = 0, nx = 0;
@@ -1269,14 +1410,14 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
             v = rstart_buf[i];
             nx = i + 1 < nruns ? (rstart_buf[i + 1] >> 4) : (uint32_t)nops;
         }
-        wave_fence();
+        sfence();
         if (i < nruns) ocig[i] = ((nx - (v >> 4)) << 4) | (v & 15);
     }
 
     // ---- E = round(mean(e/d), 3) with numpy's pairwise summation (:1015-1018)
     // pairwise_sum(a, n): n < 8 sequential; n <= 128 eight accumulators; else
     // split at n2 = n/2 rounded down to a multiple of 8 and add the halves.
-    wave_fence();
+    sfence();
     auto leaf = [&](int fo, int fn) -> double {
         double res;
         if (fn < 8) {
@@ -1630,10 +1771,6 @@ __device__ __forceinline__ double vmin_f64(double x, double y) {
     return r;
 }
 
-__device__ __forceinline__ void lds_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
 
 // inclusive prefix max over the wave (DPP row shifts, then row broadcasts)
 __device__ __forceinline__ int wave_scan_max(int v) {

@@ -13,7 +13,9 @@ from duplexumiconsensusreads_amd.params import ConsensusParams, build_dcr_params
 
 libs = sys.argv[2:]
 nfam = int(sys.argv[1])
-packed = synth.packed_fixed_size(nfam, seed=3)
+cfg = os.environ.get("ABL_CONFIG", "C2")
+packed = (synth.packed_fixed_size(nfam, seed=3) if cfg == "C2"
+          else synth.packed_config(synth.CONFIGS[cfg], nfam, seed=3, max_reads=1000))
 db = DeviceBatch(packed)
 P = build_dcr_params(ConsensusParams())
 handles = []
