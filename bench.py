@@ -4,8 +4,10 @@ Workload (BASELINE.json configs[1]): per GPU a synthetic
 duplex batch of 10 M reads = 312,500 MI families x 4 subfamilies x 8 reads,
 2x150 bp ``150M`` reads, no indels, qualities {Q37 .80, Q25 .12, Q12 .08}.
 One step = the whole hot path over that batch with inputs resident in HBM:
-per-read preprocessing (k_prep), 1.25 M single-strand consensus
-(k_consensus<false>) and 625 k duplex consensus (k_consensus<true>).
+1.25 M single-strand consensus records (k_recmeta<ss>, k_consensus_fast<ss>
+and its exact pass, k_decide + k_consensus_general<ss>) and 625 k duplex
+records (the same kernels <ds>), per-read preprocessing fused into them.
+--config C3 / C4 / C5 runs the other BASELINE.json shapes (per-GPU shards).
 
 value = duplex consensus bases emitted by all ranks per second (weak scaling:
 each rank owns its own families, no data-path collective; max time over

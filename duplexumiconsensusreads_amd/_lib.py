@@ -34,6 +34,8 @@ EXPORTS = {
     "dcr_last_kernel_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
 }
 
+# HIP-event slots of dcr_last_kernel_timing: k_recmeta<ss> includes k_prep_big,
+# k_consensus_general<..> includes the k_decide pass that precedes it
 KERNELS = ("k_prep", "k_recmeta<ss>", "k_consensus_fast<ss>", "k_consensus_exact<ss>", "k_consensus_general<ss>",
            "k_recmeta<ds>", "k_consensus_fast<ds>", "k_consensus_exact<ds>", "k_consensus_general<ds>")
 
