@@ -68,7 +68,7 @@ struct dcr_ctx {
     dcr_params host_params{};
     // fast-kernel constants (fast_constants)
     uint32_t fast_kq = 0, fast_kqlo = 0;
-    int fast_maxq = 0, fast_t16 = 0, fast_r_safe = 0;
+    int fast_maxq = 0, fast_t16 = 0, fast_r_safe = 0, fast_qlo = 0;
     uint16_t *d_llr16 = nullptr;   // device [128]
     uint32_t *d_wtab = nullptr;    // device [DCR_LUT_N] (general kernel's decision pass)
     int n_cu = 256;     // compute units (persistent grid size)
@@ -100,13 +100,14 @@ static int fast_allowed(const dcr_params *p) {
 // Returns 0 when the decision cannot be made for these parameters (then every
 // record takes the general kernel).
 static int fast_constants(const dcr_params &hp, uint16_t llr16[128], uint32_t &kq, uint32_t &kqlo, int &maxq,
-                          int &t16, int &r_safe) {
+                          int &t16, int &r_safe, int &qlo_out) {
     const int mb = std::min(std::max(hp.min_base_quality, 0), 255);
     kq = (uint32_t)(255 - mb) * 0x01010101u;
     maxq = hp.max_base_quality;
     int qlo = 123;
     while (qlo > 0 && hp.mismatch[qlo - 1] > 0.0 && hp.match[qlo - 1] >= hp.mismatch[qlo - 1]) --qlo;
     kqlo = (uint32_t)(0x80 - qlo) * 0x01010101u;
+    qlo_out = qlo;
     for (int q = 0; q < 128; ++q) {
         llr16[q] = 0;
         if (q >= qlo && q <= 122) {
@@ -160,7 +161,7 @@ static int upload_fast(dcr_ctx *c, const dcr_params *params) {
     uint16_t llr[128];
     uint32_t wtab[DCR_LUT_N];
     const int ok = fast_constants(*params, llr, c->fast_kq, c->fast_kqlo, c->fast_maxq, c->fast_t16,
-                                 c->fast_r_safe);
+                                 c->fast_r_safe, c->fast_qlo);
     c->fast_ok = fast_allowed(params) && ok;
     c->wide_ok = c->fast_ok && wide_table(*params, wtab);
     if (hipMemcpy(c->d_llr16, llr, sizeof(llr), hipMemcpyHostToDevice) != hipSuccess ||
@@ -354,6 +355,8 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         f.maxq = c->fast_maxq;
         f.t16 = c->fast_t16;
         f.r_safe = c->fast_r_safe;
+        f.minbq = duplex ? -1 : c->host_params.min_base_quality;
+        f.lo_check = duplex || c->host_params.min_base_quality < c->fast_qlo;
         f.llr16 = c->d_llr16;
         return f;
     };

@@ -80,6 +80,8 @@ struct FastArgs {
     int maxq;
     int t16;                        // decision margin in 1/16 nat (dcr_capi.hip: fast_constants)
     int r_safe;                     // most reads for which no decided column's L_b can underflow
+    int minbq;                      // single-strand: min_base_quality (masked rows in the table); duplex: -1
+    int lo_check;                   // some unmasked quality may lie below fast_qlo: check the bytes
     const uint16_t *llr16;          // [123] per-quality LLR term, 1/16 nat, rounded down
 };
 

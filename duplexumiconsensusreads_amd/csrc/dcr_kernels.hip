@@ -2064,18 +2064,24 @@ __device__ __forceinline__ void fast_load(const FastArgs &a, const RecMeta &m, c
 // kept base below fast_qlo.  Single-strand inputs mask qual < min_base_quality
 // to class N keeping the quality (:280): v_lerp_u8 computes (q + 256 - m) >> 1,
 // whose bit 7 is q >= m.  code = (k << 11) | 16 (q + k) per byte.
-template <bool DUPLEX>
+// The single-strand mask (qual < min_base_quality -> 'N' keeping the quality,
+// :280) is folded into the table: the rows of (base class, quality below the
+// mask) ARE 'N' rows.  An invalid letter is flagged even when its quality is
+// masked (the reference would read it as 'N'): its record takes the general
+// kernel, which reproduces that exactly.  LO: some unmasked quality lies below
+// fast_qlo, so the bytes are checked for it (not with the default flags).
+template <bool DUPLEX, bool LO>
 __device__ __forceinline__ uint2 make_codes4(uint32_t B, uint32_t Q, uint32_t kq, uint32_t kqlo, uint32_t &bad) {
     const uint32_t h = (B >> 1) & 0x07070707u;
-    uint32_t k = __builtin_amdgcn_perm(0u, 0x04020301u, h);                       // A1 C3 T2 G4 . . . N0
-    uint32_t x = B ^ __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, h);         // 0 for a valid letter
-    uint32_t lo = ~(Q + kqlo) & __builtin_amdgcn_perm(0u, 0xFFFFFFFFu, h);       // bit 7: a base with q < fast_qlo
-    if (!DUPLEX) {
-        const uint32_t L = __builtin_amdgcn_lerp(Q, kq, 0x01010101u);
-        const uint32_t keep = __builtin_amdgcn_perm(L << 8, L, 0x090B080Au);      // 0xff per kept byte
-        k &= keep;
-        x &= keep;                                                                // masked bytes are 'N'
-        lo &= keep;
+    const uint32_t k = __builtin_amdgcn_perm(0u, 0x04020301u, h);                 // A1 C3 T2 G4 . . . N0
+    const uint32_t x = B ^ __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, h);   // 0 for a valid letter
+    uint32_t lo = 0;
+    if (LO) {
+        lo = ~(Q + kqlo) & __builtin_amdgcn_perm(0u, 0xFFFFFFFFu, h);            // bit 7: a base with q < fast_qlo
+        if (!DUPLEX) {
+            const uint32_t L = __builtin_amdgcn_lerp(Q, kq, 0x01010101u);
+            lo &= __builtin_amdgcn_perm(L << 8, L, 0x090B080Au);                  // masked bytes are 'N' rows
+        }
     }
     bad |= x | ((((Q + 0x05050505u) | Q) | lo) & 0x80808080u);
     const uint32_t w = k + Q;                                                     // per byte, <= 126
@@ -2213,7 +2219,7 @@ struct Stamps {
 // phase 0: element codes of the prefetched bytes into the stage (dword d of
 // the record's bytes -> four codes at stage + 8 d); returns the lanes'
 // invalid-input flags
-template <bool DUPLEX>
+template <bool DUPLEX, bool LO>
 __device__ __forceinline__ uint32_t stage_codes(const FastArgs &a, const RecMeta &m, const FastStage &st, uint8_t *lds,
                                                 int stage_addr, int lane) {
     const int ndw = (int)(m.w >> 15);
@@ -2222,7 +2228,8 @@ __device__ __forceinline__ uint32_t stage_codes(const FastArgs &a, const RecMeta
     for (int u = 0; u < kStageDw; ++u) {
         if (u * kWave < ndw) {
             if (u * kWave + lane < ndw) {
-                const uint2 c = make_codes4<DUPLEX>(st.vb[u], st.vq[u], a.kq, a.kqlo, bad);
+                const uint2 c = LO ? make_codes4<DUPLEX, true>(st.vb[u], st.vq[u], a.kq, a.kqlo, bad)
+                                   : make_codes4<DUPLEX, false>(st.vb[u], st.vq[u], a.kq, a.kqlo, bad);
                 *(uint2 *)(lds + stage_addr + 8 * (u * kWave + lane)) = c;
             }
         }
@@ -2280,7 +2287,8 @@ __device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &
         while (__ballot(go)) {
             if (go) {
                 const uint32_t code = *(const uint16_t *)(lds + stage_addr + 2 * (y + tl - 1));
-                if (code < (uint32_t)fk::kNMax) --tl; else go = false;
+                // an 'N' row: sequenced 'N' or a masked quality (:280, folded into the table)
+                if (*(const uint32_t *)(lds + code + 8) & 63u) --tl; else go = false;
                 go = go && tl > 0;
             }
         }
@@ -2405,8 +2413,9 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
                 const int col = x & 255, len = (x >> 8) & 255;
                 const uint32_t ad = (uint32_t)(t - col) < (uint32_t)len ? (uint32_t)(cr + 2 * t) : (uint32_t)fk::kSent;
                 const uint32_t code = *(const uint16_t *)(lds + ad);
-                const uint32_t k = code >> 11;                       // N 0, A 1, T 2, C 3, G 4
-                const uint32_t q = ((code >> 4) & 127u) - k;         // raw quality (pad 'N': 2)
+                const uint32_t kc = code >> 11;                      // code bank: N 0, A 1, T 2, C 3, G 4
+                const uint32_t q = ((code >> 4) & 127u) - kc;        // raw quality (pad 'N': 2)
+                const uint32_t k = (*(const uint32_t *)(lds + code + 8) & 63u) ? 0u : kc;   // masked rows: 'N'
                 const double fm = P->match[q], fx = P->mismatch[q];
                 U = U * fx;
 #pragma unroll
@@ -2597,8 +2606,9 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
     __shared__ __attribute__((aligned(16))) uint8_t lds[fk::kLdsBytes];
     for (int i = threadIdx.x; i < 5 * (fk::kRowMax + 1); i += fk::kBlockThreads) {
         const int k = i / (fk::kRowMax + 1), q = i % (fk::kRowMax + 1);
-        const uint64_t inc = k == 0 ? 0ull : (uint64_t)a.llr16[q] << (16 * (k - 1));
-        *(uint4 *)(lds + 0x800 * k + 16 * (q + k)) = make_uint4((uint32_t)inc, (uint32_t)(inc >> 32), 1u << (6 * k), 0u);
+        const bool nrow = k == 0 || q < a.minbq;          // 'N', or masked below min_base_quality (:280)
+        const uint64_t inc = nrow ? 0ull : (uint64_t)a.llr16[q] << (16 * (k - 1));
+        *(uint4 *)(lds + 0x800 * k + 16 * (q + k)) = make_uint4((uint32_t)inc, (uint32_t)(inc >> 32), nrow ? 1u : 1u << (6 * k), 0u);
     }
     if (threadIdx.x < 64) ((double *)(lds + fk::kInvD))[threadIdx.x] = threadIdx.x == 0 ? 0.0 : 1.0 / (double)threadIdx.x;
     if (threadIdx.x == 0) *(uint16_t *)(lds + fk::kSent) = (uint16_t)fk::kPadCode;
@@ -2655,7 +2665,8 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
         sp.mark(0);
         if (DCR_STAMP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         sp.mark(1);                    // [0] wait for this record's prefetched bytes
-        const uint32_t bad = stage_codes<DUPLEX>(a, m0, st, lds, stage_addr, lane);
+        const uint32_t bad = a.lo_check ? stage_codes<DUPLEX, true>(a, m0, st, lds, stage_addr, lane)
+                                        : stage_codes<DUPLEX, false>(a, m0, st, lds, stage_addr, lane);
         // the read words go through LDS: a register copy of them would live
         // across the prefetch's refill of st and force a wait for it at the
         // loop's back edge
