@@ -2320,7 +2320,7 @@ __device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &
 template <bool DUPLEX, int NT, bool EXACT>
 __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &m, const Staged &sg, uint8_t *lds,
                                               const int stage_addr, const int ov_addr, const int rm_addr, const int lane,
-                                              Stamps &sp) {
+                                              Stamps &sp, const double2 *xt) {
     const dcr_out &O = a.O;
     const int64_t rec = m.rec;
     const int64_t off = m.off;
@@ -2416,7 +2416,8 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
                 const uint32_t kc = code >> 11;                      // code bank: N 0, A 1, T 2, C 3, G 4
                 const uint32_t q = ((code >> 4) & 127u) - kc;        // raw quality (pad 'N': 2)
                 const uint32_t k = (*(const uint32_t *)(lds + code + 8) & 63u) ? 0u : kc;   // masked rows: 'N'
-                const double fm = P->match[q], fx = P->mismatch[q];
+                const double2 f = xt[q];                             // (1 - p', p'/5), LDS copy of P's rows
+                const double fm = f.x, fx = f.y;
                 U = U * fx;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) L4[i] = L4[i] * (k == (uint32_t)(i + 1) ? fm : fx);
@@ -2604,6 +2605,11 @@ __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
 template <bool DUPLEX, bool EXACT>
 __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[fk::kLdsBytes];
+    // EXACT: the likelihood factors of quality rows 0..127 (the exact columns'
+    // per-read products read them once per row; the common kernel keeps none)
+    __shared__ double2 s_xt[EXACT ? 128 : 1];
+    if (EXACT)
+        for (int i = threadIdx.x; i < 128; i += fk::kBlockThreads) s_xt[i] = make_double2(a.P->match[i], a.P->mismatch[i]);
     for (int i = threadIdx.x; i < 5 * (fk::kRowMax + 1); i += fk::kBlockThreads) {
         const int k = i / (fk::kRowMax + 1), q = i % (fk::kRowMax + 1);
         const bool nrow = k == 0 || q < a.minbq;          // 'N', or masked below min_base_quality (:280)
@@ -2713,10 +2719,10 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
             send_to_general<DUPLEX>(a, m0, sg.rm, lds, lane);
         } else if (sg.state == 0) {
             bool done;
-            if (sg.T <= 64) done = finish_record<DUPLEX, 1, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
-            else if (sg.T <= 128) done = finish_record<DUPLEX, 2, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
-            else if (sg.T <= 192) done = finish_record<DUPLEX, 3, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
-            else done = finish_record<DUPLEX, 4, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp);
+            if (sg.T <= 64) done = finish_record<DUPLEX, 1, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt);
+            else if (sg.T <= 128) done = finish_record<DUPLEX, 2, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt);
+            else if (sg.T <= 192) done = finish_record<DUPLEX, 3, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt);
+            else done = finish_record<DUPLEX, 4, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt);
             if (!EXACT && !done) {
                 if (lane == npend) pend = i;
                 if (++npend == kWave) flush(lane);
