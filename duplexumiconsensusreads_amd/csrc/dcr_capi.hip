@@ -133,7 +133,7 @@ static int fast_constants(const dcr_params &hp, uint16_t llr16[128], uint32_t &k
 // row v (quality byte, '+' 256, '-' 257):
 //   bits 0-15   llr16 = floor(16 ln(match[v] / mismatch[v]) - 1e-6), a lower bound
 //   bits 16-30  z16   = ceil(16 (-ln mismatch[v]) + 1e-6), an upper bound
-//   bit 31      the row cannot be a call's row (quality above 122 or below fast_qlo, '+')
+//   bit 31      the row cannot be a call's row (quality above 122 or below fast_qlo; '+' / '-' with 1-p' < p'/5)
 // Returns 0 when some z16 does not fit (then the pass is not used).
 static int wide_table(const dcr_params &hp, uint32_t wtab[DCR_LUT_N]) {
     int qlo = 123;
@@ -144,7 +144,7 @@ static int wide_table(const dcr_params &hp, uint32_t wtab[DCR_LUT_N]) {
         const double z = std::ceil(-16.0 * std::log(mm) + 1e-6);
         if (!(z >= 0.0 && z <= 32767.0)) return 0;
         uint32_t w = (uint32_t)z << 16;
-        const bool call_row = v == DCR_LUT_DEL ? m >= mm : (v >= qlo && v <= 122);
+        const bool call_row = v >= DCR_LUT_PLUS ? m >= mm : (v >= qlo && v <= 122);   // '+', '-' rows
         if (call_row) {
             const double l = std::floor(16.0 * std::log(m / mm) - 1e-6);
             if (!(l <= 1040.0)) return 0;

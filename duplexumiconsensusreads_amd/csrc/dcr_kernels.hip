@@ -58,8 +58,7 @@ constexpr uint32_t kDel = (5u << 9) | DCR_LUT_DEL;
 struct WaveLds {
     uint16_t pad_code[4];                  // [0] = kPad: sentinel the fast layout loads outside a read (8 B keeps stage 8-aligned)
     uint16_t stage[kStageElems];           // element codes of the record's bytes (records that fit)
-    uint16_t tile[kWave][kTileIns + 2];    // insertion layout: 64 reads x 32 columns (rows padded to 17 dwords:
-                                           // a column write by 64 lanes hits distinct banks)
+    uint16_t tile[kWave][kTileIns];        // insertion layout: 64 reads x 32 columns
     int32_t cons[kColsLds];
     double et[kColsLds];
     // uniform stack of the pairwise-sum walk (phase 3)
@@ -826,6 +825,65 @@ __device__ bool decide_record(const Args &a, const int64_t rec, const int R, con
     return decide_tiles<DUPLEX, 4>(a, rec, R, T, minpos, cw, stage, s_wtab, lane);
 }
 
+// One column tile of the general kernel's layouts decided from integer LLR
+// bounds (as k_decide, with '+' rows as a sixth class): `src(r)` gives read r's
+// element code in the lane's column.  Returns true when every live column is
+// decided (call b, quality maxQ, unmasked) and fills `co` with the reference's
+// finalize outputs for it (:603-621, :1001-1012); false leaves the tile to the
+// double products.
+template <class Src>
+__device__ __forceinline__ bool decide_tile(const Args &a, int R, bool live, bool ins_col, const Src &src,
+                                            const uint32_t *s_wtab, ColOut &co) {
+    if (a.t16 < 0 || R > 4095) return false;
+    uint32_t S[6] = {0, 0, 0, 0, 0, 0}, N[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t nN = 0, Z = 0;
+    bool bad = false;
+    for (int r = 0; r < R; ++r) {
+        const uint32_t e = src(r);
+        const uint32_t cls = e >> 9;
+        const uint32_t w = s_wtab[e & 511u];
+        bad |= cls == 7 || (cls != 6 && (w >> 31) != 0);
+        const uint32_t l = w & 0xFFFFu;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            S[k] += cls == (uint32_t)k ? l : 0u;
+            N[k] += cls == (uint32_t)k;
+        }
+        nN += cls == 6;
+        Z += (w >> 16) & 0x7FFFu;
+    }
+    // the first largest in the reference's order A T C G + -
+    uint32_t Lb = S[0], kb = 0;
+#pragma unroll
+    for (int k = 1; k < 6; ++k) {
+        const bool g = S[k] > Lb;
+        Lb = g ? S[k] : Lb;
+        kb = g ? (uint32_t)k : kb;
+    }
+    uint32_t L2 = 0, nb = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        L2 = max(L2, kb != (uint32_t)k ? S[k] : 0u);
+        nb = kb == (uint32_t)k ? N[k] : nb;
+    }
+    const int nother = R - (int)nN - (int)nb;           // rows of the other classes (each adds <= 1/16 nat)
+    const bool ok = !bad && (int)(Lb - L2) - nother >= a.t16 && (int)Z - (int)Lb <= 16 * 700;
+    if (__ballot(live && !ok)) return false;
+    // finalize (:613-618, :1001-1012) for an unmasked call kb
+    const bool has_plus = N[4] > 0;
+    const bool lower = has_plus && kb < 4;
+    co.ch = (int)((0x2D2B47435441ull >> (8 * kb)) & 0xffu) + (lower ? 32 : 0);   // "ATCG+-"
+    co.q = a.P->max_base_quality;
+    co.d = R - (int)nN - (int)N[4];
+    int match;
+    if (kb == 4) match = (int)nb;
+    else if (kb == 5) match = ins_col ? 0 : (int)nb;
+    else match = (lower == ins_col) ? (int)nb : 0;
+    co.e = R - match;
+    co.overflow = false;
+    return true;
+}
+
 // --------------------------------------------------- per-read register view
 // lane r of these registers holds read r (R <= 64); read back with readlane
 struct LaneReads {
@@ -840,7 +898,8 @@ struct LaneReads {
 // and processed by the general kernel.
 template <bool DUPLEX, bool FAST>
 __device__ __forceinline__ void process_record(const Args &a, const int64_t rec, WaveLds &W, const double2 *s_lut,
-                                               const double *s_qthr, const bool dec, const int lane) {
+                                               const double *s_qthr, const uint32_t *s_wtab, const bool dec,
+                                               const int lane) {
     const dcr_params *P = a.P;
 
     const dcr_out &O = DUPLEX ? a.ds : a.ss;
@@ -956,6 +1015,8 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
     const bool staged = fits && !ins;
     if (DCR_ABL == 9 && ins && big) return;       // diagnostic: general kernel without the > 64-read insertion layout
     if (DCR_ABL == 10 && ins && !big) return;     // diagnostic: ... without the <= 64-read insertion layout
+    if (DCR_ABL == 11 && !ins) return;            // diagnostic: ... without the records free of insertions
+    if (DCR_ABL == 12 && ins) return;             // diagnostic: ... without any insertion layout
     if constexpr (FAST) {
         if (!staged || !cols_lds) {          // general kernel takes it
             if (lane == 0) {
@@ -1148,6 +1209,8 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
         Acc A;
         acc_init(A);
         bool ins_col = false;
+        bool tdec = false;                           // this tile decided by decide_tile
+        ColOut tco{};
         if (decided) {
             // the call, d and e of a decided column; quality maxQ (kb: A T C G + -)
         } else if (staged) {
@@ -1215,7 +1278,8 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
             sfence();
             ins_col = live && ((insmask >> lane) & 1);
             auto src = [&](int r) -> uint32_t { return live ? (uint32_t)W.tile[r][lane & (kTileIns - 1)] : kPad; };
-            accumulate(A, R, src, s_lut);
+            tdec = decide_tile(a, R, live, ins_col, src, s_wtab, tco);
+            if (!tdec) accumulate(A, R, src, s_lut);
             sfence();
         } else if (regbig) {
             // this tile's insertion-column flags, one load per lane
@@ -1264,7 +1328,9 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
             }
         }
         ColOut co;
-        if (decided) {
+        if (tdec) {
+            co = tco;
+        } else if (decided) {
             const uint32_t w = live ? (uint32_t)a.ws.cons[off + t] : 0u;
             co.ch = (int)((0x2D2B47435441ull >> (8 * (w & 7u))) & 0xffu);   // "ATCG+-"
             co.q = P->max_base_quality;
@@ -2743,8 +2809,11 @@ __global__ __launch_bounds__(kBlock, 2) void k_consensus_general(Args a) {
     __shared__ double2 s_lut[DCR_LUT_N];
     __shared__ double s_qthr[DCR_MAX_QTHRESH];
     __shared__ WaveLds s_wave[kWavesPerBlock];
+    __shared__ uint32_t s_wtab[DCR_LUT_N];
     const dcr_params *P = a.P;
     for (int i = threadIdx.x; i < DCR_LUT_N; i += kBlock) s_lut[i] = make_double2(P->match[i], P->mismatch[i]);
+    if (a.t16 >= 0)
+        for (int i = threadIdx.x; i < DCR_LUT_N; i += kBlock) s_wtab[i] = a.wtab[i];
     for (int i = threadIdx.x; i < DCR_MAX_QTHRESH; i += kBlock) s_qthr[i] = P->qthresh[i];
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2752,7 +2821,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_consensus_general(Args a) {
     const int nw = gridDim.x * kWavesPerBlock;
     for (int i = blockIdx.x * kWavesPerBlock + wave; i < n; i += nw) {
         const int v = a.ws.ovf[i];                  // bit 31: k_decide decided every column
-        process_record<DUPLEX, false>(a, v & 0x7fffffff, s_wave[wave], s_lut, s_qthr, v < 0, threadIdx.x & 63);
+        process_record<DUPLEX, false>(a, v & 0x7fffffff, s_wave[wave], s_lut, s_qthr, s_wtab, v < 0, threadIdx.x & 63);
     }
 }
 
