@@ -2805,7 +2805,10 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
 
 // persistent: drains the general list written by k_recmeta
 template <bool DUPLEX>
-__global__ __launch_bounds__(kBlock, 2) void k_consensus_general(Args a) {
+#ifndef DCR_GEN_OCC
+#define DCR_GEN_OCC 2
+#endif
+__global__ __launch_bounds__(kBlock, DCR_GEN_OCC) void k_consensus_general(Args a) {
     __shared__ double2 s_lut[DCR_LUT_N];
     __shared__ double s_qthr[DCR_MAX_QTHRESH];
     __shared__ WaveLds s_wave[kWavesPerBlock];
