@@ -156,31 +156,33 @@ def test_gpu_deep_insertion_columns_many_classes(ctx):
     assert_same(packed, got, want)
 
 
-@pytest.mark.parametrize("maxq", [60, 93])
-def test_gpu_underflow_columns(ctx, maxq):
+@pytest.mark.parametrize("maxq,nreads", [(60, 63), (93, 63), (60, 100), (93, 130)])
+def test_gpu_underflow_columns(ctx, maxq, nreads):
     """Deep high-quality columns where the reference's products underflow:
-    one 'G' row beside 62 sequenced 'N' rows at maxQ gives L = 0 for every
+    one 'G' row beside sequenced 'N' rows at maxQ gives L = 0 for every
     class, a NaN posterior and the call 'A' (:603-618) although the LLR bound
-    would decide 'G'; and a 4-way split of 60 rows (18/15/15/12) at Q93 whose
-    call likelihood underflows.  Records above r_safe take the exact path."""
+    would decide 'G'; and a 4-way split (18/15/15/12 + 'N') at maxQ whose call
+    likelihood underflows.  63 reads: the fast kernel (records above r_safe
+    take the exact path); 100 / 130 reads: k_decide (its Z - L_b bound sends
+    the record to the double products)."""
     L = 40
-    packed = synth.packed_fixed_size(4, sub_size=63, read_len=L, seed=3)
+    packed = synth.packed_fixed_size(4, sub_size=nreads, read_len=L, seed=3)
     packed.quals[:] = maxq
     n_sub = len(packed.sub_off) - 1
     for s in range(n_sub):
         g0 = int(packed.sub_off[s])
         b0 = int(packed.seq_off[g0])
         tmpl = packed.bases[b0:b0 + L].copy()
-        for r in range(63):
+        for r in range(nreads):
             o = int(packed.seq_off[g0 + r])
             packed.bases[o:o + L] = tmpl
         if s % 2 == 0:
             packed.bases[b0 + 10] = ord("G")
-            for r in range(1, 63):
+            for r in range(1, nreads):
                 packed.bases[int(packed.seq_off[g0 + r]) + 10] = ord("N")
         else:
-            col = b"G" * 18 + b"A" * 15 + b"T" * 15 + b"C" * 12 + b"N" * 3
-            for r in range(63):
+            col = b"G" * 18 + b"A" * 15 + b"T" * 15 + b"C" * 12 + b"N" * (nreads - 60)
+            for r in range(nreads):
                 packed.bases[int(packed.seq_off[g0 + r]) + 20] = col[r]
     params = ConsensusParams(max_base_quality=maxq, max_reads=1000)
     ctx.set_params(params)
