@@ -1905,7 +1905,7 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
     // record-level result); a read whose offset from the first read does not fit
     // 16 bits sends its record to the general kernel (flag 4)
     int carry = -1;
-    constexpr int kBatch = 4;                     // 64-read chunks with their loads in flight together
+    constexpr int kBatch = 6;                     // 64-read chunks with their loads in flight together
     for (int64_t cb = gbeg; cb < gend; cb += kBatch * kWave) {
     RdRaw raw[kBatch];
 #pragma unroll
