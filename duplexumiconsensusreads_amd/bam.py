@@ -5,11 +5,17 @@ The reference streams BAM through pysam/htslib (DuplexUMIConsensusReads.py:1476,
 the host carries its own codec for the SAM spec v1.6 BAM layout: BGZF blocks
 (RFC1952 members with the BC extra field), the binary header, and records with
 typed aux fields.  Throughput-critical ingest of very large files is a later
-native item; this codec is correct and streams.
+native item.  The BGZF layer runs natively when
+``libdcr_bgzf.so`` (csrc/dcr_bgzf.cpp, include/dcr_bgzf.h) is built: blocks are
+inflated / deflated on a pool of host threads, and the written files are
+byte-identical to the Python writer's.  The Python BGZF classes below stay as
+the portable codec (``DCR_BGZF=python`` forces them).
 """
 from __future__ import annotations
 
 import array
+import ctypes
+import os
 import struct
 import zlib
 
@@ -38,6 +44,100 @@ def reg2bin(beg: int, end: int) -> int:
     if beg >> 26 == end >> 26:
         return ((1 << 3) - 1) // 7 + (beg >> 26)
     return 0
+
+
+_NATIVE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdcr_bgzf.so")
+_native_lib = None
+
+
+def native_bgzf():
+    """The native codec library, or None when it is not built (or disabled)."""
+    global _native_lib
+    if _native_lib is None:
+        if os.environ.get("DCR_BGZF", "") == "python" or not os.path.exists(_NATIVE_PATH):
+            return None
+        lib = ctypes.CDLL(_NATIVE_PATH)
+        vp, i64 = ctypes.c_void_p, ctypes.c_int64
+        lib.dcr_bgzf_open_read.restype = vp
+        lib.dcr_bgzf_open_read.argtypes = [ctypes.c_char_p, ctypes.c_int]
+        lib.dcr_bgzf_read.restype = i64
+        lib.dcr_bgzf_read.argtypes = [vp, vp, i64]
+        lib.dcr_bgzf_close_read.restype = None
+        lib.dcr_bgzf_close_read.argtypes = [vp]
+        lib.dcr_bgzf_open_write.restype = vp
+        lib.dcr_bgzf_open_write.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+        lib.dcr_bgzf_write.restype = ctypes.c_int
+        lib.dcr_bgzf_write.argtypes = [vp, ctypes.c_char_p, i64]
+        lib.dcr_bgzf_close_write.restype = ctypes.c_int
+        lib.dcr_bgzf_close_write.argtypes = [vp]
+        lib.dcr_bgzf_last_error.restype = ctypes.c_char_p
+        lib.dcr_bgzf_last_error.argtypes = []
+        _native_lib = lib
+    return _native_lib
+
+
+def _native_error(lib, what):
+    return OSError(f"{what}: {lib.dcr_bgzf_last_error().decode()}")
+
+
+class NativeBGZFReader:
+    """BGZF decompressed stream from csrc/dcr_bgzf.cpp (threaded inflate)."""
+
+    def __init__(self, path, n_threads=0):
+        self._lib = native_bgzf()
+        self._h = self._lib.dcr_bgzf_open_read(os.fsencode(path), n_threads)
+        if not self._h:
+            raise _native_error(self._lib, "BGZF open")
+
+    def read(self, n):
+        buf = ctypes.create_string_buffer(n)
+        got = self._lib.dcr_bgzf_read(self._h, buf, n)
+        if got < 0:
+            raise ValueError(self._lib.dcr_bgzf_last_error().decode())
+        return buf.raw[:got]
+
+    def close(self):
+        if self._h:
+            self._lib.dcr_bgzf_close_read(self._h)
+            self._h = None
+
+
+class NativeBGZFWriter:
+    """BGZF writer from csrc/dcr_bgzf.cpp (threaded deflate, same bytes as BGZFWriter)."""
+
+    def __init__(self, path, level=6, n_threads=0):
+        self._lib = native_bgzf()
+        self._h = self._lib.dcr_bgzf_open_write(os.fsencode(path), level, n_threads)
+        if not self._h:
+            raise _native_error(self._lib, "BGZF open")
+        self._buf = bytearray()
+
+    def write(self, data):
+        self._buf += data
+        if len(self._buf) >= 1 << 20:
+            self._push()
+
+    def _push(self):
+        if self._buf:
+            if self._lib.dcr_bgzf_write(self._h, bytes(self._buf), len(self._buf)) != 0:
+                raise _native_error(self._lib, "BGZF write")
+            self._buf = bytearray()
+
+    def close(self):
+        if self._h:
+            self._push()
+            rc = self._lib.dcr_bgzf_close_write(self._h)
+            self._h = None
+            if rc != 0:
+                raise _native_error(self._lib, "BGZF close")
+
+
+def open_bgzf_reader(path):
+    return NativeBGZFReader(path) if native_bgzf() is not None else BGZFReader(path)
+
+
+def open_bgzf_writer(path, level=6):
+    return NativeBGZFWriter(path, level) if native_bgzf() is not None else BGZFWriter(path, level)
 
 
 class BGZFReader:
@@ -233,7 +333,7 @@ class AlignmentFile:
     def __init__(self, path, mode="rb", template=None, header=None):
         self.mode = mode
         if mode.startswith("r"):
-            self._r = BGZFReader(path)
+            self._r = open_bgzf_reader(path)
             magic = self._r.read(4)
             if magic != b"BAM\x01":
                 raise ValueError(f"{path}: not a BAM file")
@@ -253,16 +353,25 @@ class AlignmentFile:
                 self.header = header
             else:
                 self.header = BamHeader()
-            self._w = BGZFWriter(path)
+            self._w = open_bgzf_writer(path)
             self._w.write(self.header.encode())
 
     def __iter__(self):
+        # records are cut from 1 MiB reads of the decompressed stream
+        buf, pos = b"", 0
+        unpack = struct.unpack_from
         while True:
-            hb = self._r.read(4)
-            if len(hb) < 4:
-                return
-            n = struct.unpack("<i", hb)[0]
-            yield decode_record(self._r.read(n))
+            if len(buf) - pos < 4 or len(buf) - pos < 4 + unpack("<i", buf, pos)[0]:
+                more = self._r.read(1 << 20)
+                if not more:
+                    if len(buf) - pos >= 4:
+                        yield decode_record(buf[pos + 4:])      # truncated last record, as before
+                    return
+                buf, pos = buf[pos:] + more, 0
+                continue
+            n = unpack("<i", buf, pos)[0]
+            yield decode_record(buf[pos + 4:pos + 4 + n])
+            pos += 4 + n
 
     def fetch_all(self):
         return list(self)
