@@ -19,6 +19,8 @@ import os
 import struct
 import zlib
 
+import numpy as np
+
 from .records import AlignedSegment, array_subtype
 
 _SEQ_ALPHA = "=ACMGRSVTWYHKDBN"
@@ -28,6 +30,11 @@ _MAX_BLOCK = 0xff00
 
 # decode table: byte -> two bases
 _SEQ_PAIR = [(_SEQ_ALPHA[b >> 4] + _SEQ_ALPHA[b & 15]) for b in range(256)]
+_SEQ_PAIR_NP = np.array([p.encode() for p in _SEQ_PAIR], dtype="S2")
+# encode table: ASCII (either case) -> 4-bit code; '=' is 0, unknown letters 15
+_SEQ_CODE_NP = np.full(256, 15, np.uint8)
+for _c, _i in _SEQ_CODE.items():
+    _SEQ_CODE_NP[ord(_c)] = _SEQ_CODE_NP[ord(_c.lower())] = _i
 
 
 def reg2bin(beg: int, end: int) -> int:
@@ -266,7 +273,8 @@ def decode_record(buf: bytes) -> AlignedSegment:
     cig = struct.unpack_from(f"<{n_cig}I", buf, off); off += 4 * n_cig
     r._cigar = [(c & 15, c >> 4) for c in cig] or None
     nb = (l_seq + 1) // 2
-    seq = "".join(_SEQ_PAIR[b] for b in buf[off:off + nb])[:l_seq]; off += nb
+    seq = _SEQ_PAIR_NP[np.frombuffer(buf, np.uint8, nb, off)].tobytes()[:l_seq].decode() if nb else ""
+    off += nb
     qual = buf[off:off + l_seq]; off += l_seq
     r._seq = seq or None
     if l_seq and qual[0] != 0xff:
@@ -317,10 +325,13 @@ def encode_record(r: AlignedSegment) -> bytes:
                        bin_, len(cig), r.flag, l_seq, r.next_reference_id,
                        r.next_reference_start, r.template_length)
     cigb = struct.pack(f"<{len(cig)}I", *[(n << 4) | op for op, n in cig])
-    codes = [_SEQ_CODE.get(c, 15) for c in seq.upper()]
-    if l_seq & 1:
-        codes.append(0)
-    seqb = bytes((codes[i] << 4) | codes[i + 1] for i in range(0, len(codes), 2))
+    if l_seq:
+        codes = _SEQ_CODE_NP[np.frombuffer(seq.encode("latin-1"), np.uint8)]
+        if l_seq & 1:
+            codes = np.append(codes, np.uint8(0))
+        seqb = ((codes[0::2] << 4) | codes[1::2]).tobytes()
+    else:
+        seqb = b""
     qualb = bytes(r._qual) if r._qual is not None else b"\xff" * l_seq
     tagb = b"".join(_encode_tag(t, c, v) for t, c, v in r._tags)
     body = core + name + cigb + seqb + qualb + tagb

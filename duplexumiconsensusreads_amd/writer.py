@@ -17,9 +17,13 @@ from __future__ import annotations
 
 from .records import AlignedSegment
 
+_PHRED33 = bytes((i + 33) & 0xff for i in range(256))
+
 
 def int_list_str(vals) -> str:
-    return "[" + ", ".join(str(int(v)) for v in vals) + "]"
+    if hasattr(vals, "tolist"):
+        vals = vals.tolist()
+    return "[" + ", ".join(map(str, map(int, vals))) + "]"
 
 
 def family_code(read) -> str:
@@ -86,7 +90,11 @@ def duplex_record(core, ss_a: AlignedSegment, ss_b: AlignedSegment) -> AlignedSe
 
     def aq(rec):
         q = rec.query_qualities
-        return "".join(chr(x + 33) for x in q) if q is not None else ""
+        if q is None:
+            return ""
+        if q and max(q) > 222:                           # chr() beyond latin-1
+            return "".join(chr(x + 33) for x in q)
+        return bytes(q).translate(_PHRED33).decode("latin-1")
 
     r.set_tags((("MI", ss_a.get_tag("MI").split("/")[0]),
                 ("RX", ss_a.get_tag("RX")),
