@@ -74,3 +74,20 @@ def test_cli_matches_reference_main_gpu(tmp_path):
     finally:
         ctx.close()
     assert_matches_reference(res)
+
+
+def test_cli_output_files_identical_with_either_bgzf_codec(tmp_path, monkeypatch):
+    # the native BGZF codec (libdcr_bgzf.so) and the Python one write the same bytes
+    if bam.native_bgzf() is None:
+        pytest.skip("libdcr_bgzf.so not built")
+    files = {}
+    for codec in ("native", "python"):
+        if codec == "python":
+            monkeypatch.setenv("DCR_BGZF", "python")
+            monkeypatch.setattr(bam, "_native_lib", None)
+        d = tmp_path / codec
+        d.mkdir()
+        run_cli(d, dcr_oracle_c.run)
+        files[codec] = {p.name: p.read_bytes() for p in sorted(d.iterdir())}
+    assert len(files["native"]) == 3
+    assert files["native"] == files["python"]
