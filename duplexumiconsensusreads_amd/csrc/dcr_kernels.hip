@@ -2078,7 +2078,10 @@ constexpr int kRm = kPtrs + 16 * 8;                        // per wave: u64 [64]
 constexpr int kMv = kRm + kWaves * kWave * 8;              // per wave: u32 [8] a later record's descriptor
 constexpr int kOv = kMv + kWaves * 32;                     // per wave: u16 [256] column words d | e << 6 | call << 12
 constexpr int kDivR = kOv + kWaves * 512;                  // u32 [64] ceil(2^24 / R): msum / R = msum * [R] >> 24
-constexpr int kLdsBytes = kDivR + 64 * 4;
+#ifndef DCR_LDS_PAD
+#define DCR_LDS_PAD 0
+#endif
+constexpr int kLdsBytes = kDivR + 64 * 4 + DCR_LDS_PAD;       // PAD: diagnostic builds only
 static_assert(kStageElems * 2 == 0x1000, "one 4 KiB stage per wave");
 static_assert(16 * (kRowMax + 5) <= 0x800, "a class bank fits 2 KiB");
 static_assert(5 * kLdsBytes <= 160 * 1024, "five blocks (20 waves) per CU");
