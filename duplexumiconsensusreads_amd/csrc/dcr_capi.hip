@@ -363,7 +363,15 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     auto strand = [&](bool duplex) -> int {
         a.n_rec = (duplex ? 2LL : 4LL) * in->n_fam;
         const dcr::FastArgs fa = fast_args(duplex);
-        const unsigned nb = (unsigned)((a.n_rec + 255) / 256);    // k_recmeta: 64 records per wave
+        // k_recmeta: 64 records per wave, or fewer when the reads per record
+        // exceed 16 on average (about 1,024 reads per wave)
+        int rpw = 64;
+        if (!duplex && a.n_rec > 0) {
+            const int64_t avg = (int64_t)in->n_reads / a.n_rec;
+            while (rpw > 1 && (int64_t)rpw * avg > 1024) rpw >>= 1;
+        }
+        a.rpw = rpw;
+        const unsigned nb = (unsigned)((a.n_rec + 4LL * rpw - 1) / (4LL * rpw));
         hipEvent_t *ev = c->ev + (duplex ? 6 : 2);
         // the exact queue is filled by the common kernel; its length is only
         // known on the device, so the exact kernel gets the resident grid

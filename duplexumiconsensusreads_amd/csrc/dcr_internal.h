@@ -54,6 +54,7 @@ struct Args {
     dcr_out ds;
     int64_t n_rec;
     int fast_ok;            // fast_allowed() (dcr_capi.hip): the fast kernel may take records
+    int rpw;                // k_recmeta: records per wave (a power of two <= 64; fewer for deep records)
     int t16;                // decision margin in 1/16 nat (fast_constants)
     const uint32_t *wtab;   // [DCR_LUT_N] per LUT row: LLR term | -ln(p'/5) bound << 16 | not-a-call-row << 31
 };

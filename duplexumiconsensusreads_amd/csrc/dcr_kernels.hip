@@ -1702,7 +1702,8 @@ __device__ __forceinline__ double pairwise_et(const double *a, int n, int lane) 
 // records it writes the launch metadata the fast kernel fetches with one scalar
 // load per record plus one 8-byte load per read.
 //
-// One wave per 64 records.  Reads are visited lane = read (coalesced loads) and
+// One wave per a.rpw records (64, or fewer when records are deep, so that the
+// read pass of a C4-shape batch still spreads over thousands of waves).  Reads are visited lane = read (coalesced loads) and
 // folded into their record's LDS slot with LDS atomics; the record of a read
 // comes from a marker per record start and a DPP prefix-max scan.  List appends
 // are wave-aggregated (one global atomic per wave per list).
@@ -1878,11 +1879,11 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
     const int lane = threadIdx.x & 63;
     RecAgg *agg = s_agg[wave];
     int *mark = s_mark[wave];
-    const int64_t rb = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kWave;
+    const int64_t rb = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * a.rpw;
     if (rb >= a.n_rec) return;
     const int64_t rk = rb + lane;
-    const bool vk = rk < a.n_rec;
-    const int64_t rend = min(rb + kWave, a.n_rec);
+    const bool vk = lane < a.rpw && rk < a.n_rec;
+    const int64_t rend = min(rb + a.rpw, a.n_rec);
     int g0 = 0, R = 0;
     int64_t gbeg, gend;
     if (!DUPLEX) {
