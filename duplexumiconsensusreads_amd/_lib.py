@@ -41,6 +41,11 @@ KERNELS = ("k_prep", "k_recmeta<ss>", "k_consensus_fast<ss>", "k_consensus_exact
 
 _lib = None
 
+# numpy view of dcr_read_info (include/dcr.h), 24 bytes
+READ_INFO_DTYPE = np.dtype([("seq_start", "<i8"), ("len", "<i4"), ("n_cig", "<i4"), ("status", "<i4"),
+                            ("has_ins", "<i4")])
+assert READ_INFO_DTYPE.itemsize == ctypes.sizeof(DcrReadInfo)
+
 
 class DcrError(RuntimeError):
     pass
@@ -117,10 +122,9 @@ class Context:
         return ss, ds, info
 
     def read_info(self, n):
-        arr = (DcrReadInfo * max(n, 1))()
-        _check(load().dcr_read_info_host(self._ctx, ctypes.cast(arr, ctypes.c_void_p), n))
-        return {k: np.array([getattr(x, k) for x in arr[:n]])
-                for k in ("seq_start", "len", "n_cig", "status", "has_ins")}
+        arr = np.zeros(max(n, 1), dtype=READ_INFO_DTYPE)
+        _check(load().dcr_read_info_host(self._ctx, arr.ctypes.data, n))
+        return {k: arr[k][:n].copy() for k in READ_INFO_DTYPE.names}
 
     # -- device-pointer path (inputs resident in HBM) ----------------------
     def reserve(self, batch_struct: DcrBatch):

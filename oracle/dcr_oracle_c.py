@@ -33,8 +33,9 @@ def load():
     return _lib
 
 
-def info_to_dict(arr):
-    return {k: np.array([getattr(x, k) for x in arr]) for k in ("seq_start", "len", "n_cig", "status", "has_ins")}
+INFO_DTYPE = np.dtype([("seq_start", "<i8"), ("len", "<i4"), ("n_cig", "<i4"), ("status", "<i4"),
+                       ("has_ins", "<i4")])
+assert INFO_DTYPE.itemsize == ctypes.sizeof(DcrReadInfo)
 
 
 def run(packed, params, n_threads=1, want_info=True):
@@ -43,11 +44,12 @@ def run(packed, params, n_threads=1, want_info=True):
     P = build_dcr_params(params)
     ss = OutArrays(4 * packed.n_fam, packed.ss_cols)
     ds = OutArrays(2 * packed.n_fam, packed.ds_cols)
-    info = (DcrReadInfo * max(packed.n_reads, 1))()
+    info = np.zeros(max(packed.n_reads, 1), dtype=INFO_DTYPE)
     b = packed.as_struct()
     so, do = ss.as_struct(), ds.as_struct()
     rc = lib.dcr_oracle_run(ctypes.byref(P), ctypes.byref(b), ctypes.byref(so),
-                            ctypes.byref(do), ctypes.cast(info, ctypes.c_void_p), n_threads)
+                            ctypes.byref(do), ctypes.c_void_p(info.ctypes.data), n_threads)
     if rc != 0:
         raise RuntimeError(f"dcr_oracle_run failed: {rc}")
-    return ss, ds, (info_to_dict(info[:packed.n_reads]) if want_info else None)
+    n = packed.n_reads
+    return ss, ds, ({k: info[k][:n].copy() for k in INFO_DTYPE.names} if want_info else None)
