@@ -143,6 +143,19 @@ def open_bgzf_reader(path):
     return NativeBGZFReader(path) if native_bgzf() is not None else BGZFReader(path)
 
 
+def bgzf_stream(path):
+    """The whole decompressed byte stream of a BGZF file."""
+    r = open_bgzf_reader(path)
+    out = bytearray()
+    while True:
+        chunk = r.read(1 << 22)
+        if not chunk:
+            break
+        out += chunk
+    r.close()
+    return bytes(out)
+
+
 def open_bgzf_writer(path, level=6):
     return NativeBGZFWriter(path, level) if native_bgzf() is not None else BGZFWriter(path, level)
 
@@ -173,8 +186,13 @@ class BGZFReader:
         if bsize is None:
             raise ValueError("BGZF block without BC field")
         rest = self._f.read(bsize - xlen - 19 + 8)
+        if len(rest) != bsize - xlen - 19 + 8:
+            raise ValueError("truncated BGZF block")
         cdata = rest[:-8]
+        crc, isize = struct.unpack("<II", rest[-8:])
         data = zlib.decompress(cdata, -15)
+        if len(data) != isize or (zlib.crc32(data) & 0xffffffff) != crc:
+            raise ValueError("BGZF block CRC32 / ISIZE mismatch")
         self._buf = self._buf[self._pos:] + data
         self._pos = 0
         return True
@@ -375,8 +393,8 @@ class AlignmentFile:
             if len(buf) - pos < 4 or len(buf) - pos < 4 + unpack("<i", buf, pos)[0]:
                 more = self._r.read(1 << 20)
                 if not more:
-                    if len(buf) - pos >= 4:
-                        yield decode_record(buf[pos + 4:])      # truncated last record, as before
+                    if len(buf) > pos:
+                        raise ValueError("truncated BAM record at the end of the file")
                     return
                 buf, pos = buf[pos:] + more, 0
                 continue

@@ -1,31 +1,47 @@
 """Command line drop-in for the reference script's ``main``
 (DuplexUMIConsensusReads.py:1426-1650): same flags (``parse_args`` :10-91),
-same output files, same summary lines, same record order.
+same output files, same stdout, same record order.
 
-What changes is the middle of the loop.  The reference calls
-``make_consensus_read`` six times per family (:1560-1588); here complete
-families are collected into batches and each batch is ONE ``dcr_run_batch``
-call on the GPU (``pipeline.run_batch``), then drained in input order.  The
-host keeps the per-read filters (``pass_filters`` :1135-1181), MI grouping
-(``add_read_to_family`` :1185-1217), the family checks and the seeded
-downsampling (``pipeline.prepare_family``), so the RNG call sequence is the
-reference's.
+The per-record work runs natively (libdcr_io.so, include/dcr_io.h):
 
-Failure semantics follow the reference: records of every family before a
-failing one are written, then the reference's exception (or ``sys.exit(1)``
-with its message) is raised at that family.
+* the ingest reads the BAM (threaded BGZF inflate), applies ``pass_filters``
+  (:1135-1181), groups MI runs (:1185-1217), checks and splits families and
+  downsamples with CPython's MT19937 (:100-188), and packs whole batches of
+  families into pinned host memory;
+* the device runs the six ``make_consensus_read`` calls of every family of a
+  batch (:1560-1582) in one asynchronous submit (stream.DeviceStream);
+* the writer formats the duplex records (:1352-1419) and deflates BGZF
+  blocks on a worker pool; excluded reads and filtered families are copied
+  through as stored.
+
+Batches are pipelined: a thread ingests batch k+1 while the device runs batch
+k and the main thread writes batch k-1.
+
+Failure semantics follow the reference: everything the reference writes
+before it stops (consensus records of earlier families; side-file records up
+to the failing family, ``dcr_host_batch.tab_*_cut``) is written, then its
+exception, or its message and ``sys.exit(1)``, is raised at that family.
 """
 from __future__ import annotations
 
 import argparse
+import queue
 import random
 import sys
-from typing import List, Optional
+import threading
+from typing import Optional
 
-from . import bam, pipeline
+import numpy as np
+
+from . import native_io
 from .params import ConsensusParams
 
 SPLIT_NAMES = {0: "A1", 1: "B2", 2: "B1", 3: "A2"}      # split_dict (:1511)
+EQX_LINE = 'Symbols "x" and "=" were found in CIGAR strings and were changed to "M"'   # :375
+STAGE_LINES = ("\t\t * Reconstruct alignment in progress", "\t\t * Call consensus in progress",
+               "\t\t * Adjust consensus fields in progress")                            # :1318-1341
+BADCHAR_LINE = ("\n ERROR: input values to nucleotide/INDEL list in function call_consensus() and subfunction "
+                "most_likely_nucleotide() are different than the allowed ones. \n Please check documentation")
 
 
 def parse_args(argv):
@@ -45,107 +61,294 @@ def parse_args(argv):
     ap.add_argument("--error_rate_pre_labeling", required=False, default=0, type=int)
     ap.add_argument("--deletion_score", required=False, default=30, type=int)
     ap.add_argument("--no_insertion_score", required=False, default=30, type=int)
-    # not a reference flag: families per device call (does not change any output)
-    ap.add_argument("--batch_families", required=False, default=65536, type=int, help=argparse.SUPPRESS)
+    # not reference flags: batching and codec knobs (they do not change any record)
+    ap.add_argument("--batch_reads", required=False, default=1 << 20, type=int, help=argparse.SUPPRESS)
+    ap.add_argument("--threads", required=False, default=0, type=int, help=argparse.SUPPRESS)
+    ap.add_argument("--compression_level", required=False, default=6, type=int, help=argparse.SUPPRESS)
+    ap.add_argument("--device", required=False, default=0, type=int, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
-class ReadFormatExit(SystemExit):
-    """``pass_filters`` prints an error and calls sys.exit(1) (:1148-1165)."""
+class ReferenceExit(SystemExit):
+    """The reference prints an error and calls sys.exit(1)."""
 
 
-def pass_filters(read, map_q_threshold: int) -> bool:
-    """``pass_filters`` (:1135-1181): format checks (exit), then the flag /
-    MAPQ filters."""
-    if not read.has_tag("MI"):
-        print("ERROR: family code tag (MI) not found in file")
-        raise ReadFormatExit(1)
-    if not read.has_tag("RX"):
-        print("ERROR: family code tag (RX) not found in file")
-        raise ReadFormatExit(1)
-    cs = read.cigarstring
-    if cs is None:                        # `x in None` (:1158) on a read without CIGAR
-        raise TypeError("argument of type 'NoneType' is not iterable")
-    if any(x in cs for x in ("P", "N", "B", "*")):
-        print("ERROR: unexpected symbols (P, N, B, *) were found in CIGAR strings.")
-        raise ReadFormatExit(1)
-    if any(op == 4 for op, _ in read.cigartuples[1:-1]):
-        print("ERROR: softclips (S) found in the middle of the read.")
-        raise ReadFormatExit(1)
-    return (read.is_paired and read.is_proper_pair and not read.is_unmapped and not read.mate_is_unmapped
-            and not read.is_supplementary and not read.is_qcfail and read.mapping_quality >= map_q_threshold)
+def badchar_column(hb, f: int, k: int, min_base_quality: int):
+    """The column most_likely_nucleotide prints before exiting on an invalid
+    letter (:582-585), for single-strand consensus k of processed family f.
+
+    Error reporting only (the device already decided the outcome): the reads
+    are preprocessed as :191-325 do and laid out as reconstruct_alignment
+    (:458-545) does until the first column holding a letter outside
+    A T C G N a t c g n + -."""
+    a = hb.a
+    allowed = set("ATCGNatcgn+-")
+    pos, cig, seq = [], [], []
+    for r in range(int(a["sub_off"][4 * f + k]), int(a["sub_off"][4 * f + k + 1])):
+        o, n = int(a["seq_off"][r]), int(a["seq_len"][r])
+        s = a["bases"][o:o + n].tobytes().decode("latin-1")
+        q = a["quals"][o:o + n]
+        c0 = int(a["cig_off"][r])
+        ops, s5, s3, inseq = [], 0, 0, False
+        for w in a["cigar"][c0:c0 + int(a["cig_n"][r])]:
+            op, ln = int(w) & 15, int(w) >> 4
+            if op == 4:
+                if not inseq:
+                    s5 = ln
+                else:
+                    s3 = ln
+            elif op != 5:
+                inseq = True
+                ops.append((op, ln))
+        keep = slice(s5, -s3) if s3 else slice(s5, None)
+        s, q = s[keep], q[keep]
+        s = "".join("N" if qq < min_base_quality else ch for ch, qq in zip(s, q))
+        tn = len(s) - len(s.rstrip("N"))
+        s = s[:len(s) - tn]
+        exp = [0 if op in (7, 8) else op for op, ln in ops for _ in range(ln)]
+        pos.append(int(a["read_pos"][r]))
+        cig.append(exp[:len(exp) - tn])
+        seq.append(s)
+    lo, hi = min(pos), max(p + len(s) for p, s in zip(pos, seq))
+    ic, iz = [0] * len(pos), [0] * len(pos)
+    for p in range(lo, hi):
+        cur = [c[i] if i < len(c) else 99 for c, i in zip(cig, ic)]
+        col = []
+        if 1 in cur:
+            for r, op in enumerate(cur):
+                if op == 1:
+                    col.append(seq[r][iz[r]].lower())
+                    ic[r] += 1
+                    iz[r] += 1
+                else:
+                    col.append("+")
+        else:
+            for r in range(len(pos)):
+                if p < pos[r] or iz[r] >= len(seq[r]):
+                    col.append("N")
+                elif cig[r][ic[r]] == 2:
+                    col.append("-")
+                    ic[r] += 1
+                else:
+                    col.append(seq[r][iz[r]])
+                    ic[r] += 1
+                    iz[r] += 1
+        if any(ch not in allowed for ch in col):
+            return np.array(col)
+    return None
 
 
-def family_code_of(read) -> str:
-    return read.get_tag("MI").split("/")[0]       # :1204, :1209
-
-
-class _Run:
-    """One pass over the input: counters, the pending batch, the writers."""
-
-    def __init__(self, params: ConsensusParams, backend, batch_families: int, consensusbam, unprocessedbam,
-                 verbose: bool, rng):
-        self.params, self.backend, self.batch_families = params, backend, batch_families
-        self.consensusbam, self.unprocessedbam = consensusbam, unprocessedbam
-        self.verbose, self.rng = verbose, rng
-        self.pending: List[pipeline.FamilyResult] = []
-        self.processed = 0
-        self.excluded = 0
-
-    def family_done(self, family):
-        """preprocess_family (:1226-1287) for one completed family.  Filtered
-        families go to the side file at once, as the reference writes them
-        (:1536-1540); the rest wait for their batch."""
-        code = family_code_of(family[0])
-        try:
-            res = pipeline.prepare_family(family, self.params, self.rng)
-        except pipeline.FamilyExit as e:
-            self.drain()
-            print(str(e))
-            raise SystemExit(1)
-        except Exception:
-            self.drain()
-            raise
-        if res.subs is None:
-            self.excluded += 1
-            for r in family:
-                self.unprocessedbam.write(r)
-            return
-        res.code = code
-        self.processed += 1
-        self.pending.append(res)
-        if len(self.pending) >= self.batch_families:
-            self.drain()
-
-    def drain(self):
-        """Run the pending batch on the device and write its records in input
-        order; stop at the first family the reference would fail on."""
-        if not self.pending:
-            return
-        todo, self.pending = self.pending, []
-        pipeline.run_batch(todo, self.params, self.backend)
-        for fam in todo:
-            if fam.crash is not None:
-                exc = pipeline.reference_exception(fam.crash)
-                if isinstance(exc, pipeline.FamilyExit):
-                    print(str(exc))
-                    raise SystemExit(1)
-                raise exc
-            if self.verbose:
-                for idx in range(4):
-                    print("Single-strand consensus for subfamily", fam.code, SPLIT_NAMES[idx], "in progress")
-                print("Double-strand consensus for family", fam.code, "in progress")
-            for rec in fam.ds:
-                self.consensusbam.write(rec)
-            if self.verbose:
-                print("Consensus reads for family", fam.code, "have been sucessfully written \n")
-
-
-def default_backend(device: int = 0):
+def default_backend(params: ConsensusParams, device: int = 0):
     """The HIP library on ``device`` (fails loudly without it: no CPU fallback)."""
     from . import _lib
-    ctx = _lib.Context(ConsensusParams(), device=device)
-    return _lib.backend(ctx)
+    from .stream import DeviceStream
+    ctx = _lib.Context(params, device=device)
+    return DeviceStream(ctx)
+
+
+def _as_backend(backend, params):
+    if backend is None:
+        return default_backend(params)
+    if hasattr(backend, "submit"):
+        return backend
+    from .stream import CallBackend
+    return CallBackend(backend, params)
+
+
+def _raise_reference(kind: str, msg: str = ""):
+    if kind == "exit":
+        raise ReferenceExit(1)
+    exc = {"IndexError": IndexError, "TypeError": TypeError, "ValueError": ValueError,
+           "OverflowError": OverflowError, "AttributeError": AttributeError}.get(kind)
+    if kind == "UnicodeEncodeError":
+        raise UnicodeEncodeError("ascii", "", 0, 1, "ordinal not in range(128)")
+    raise (exc or RuntimeError)(msg or f"reference would raise {kind} here")
+
+
+class _Driver:
+    def __init__(self, args, params, backend, ing, cons, excl, unproc):
+        self.args, self.params, self.backend = args, params, backend
+        self.ing, self.cons, self.excl, self.unproc = ing, cons, excl, unproc
+        self.verbose = args.verbose
+
+    # -- stdout of one batch, in the reference's order --------------------------
+    def _prints(self, hb, fail_f, kind, which, last_batch):
+        a = hb.a
+        F = hb.n_fam
+        eqx = a["fam_eqx"][:4 * F]
+        if not self.verbose and fail_f >= F and not eqx.any():
+            return
+        if not self.verbose:
+            # only the =/X lines (:374-375), per processed family in order
+            nz = np.nonzero(eqx.reshape(F, 4).any(axis=1))[0] if F else []
+            for f in nz:
+                if f > fail_f:
+                    break
+                for k in range(4):
+                    if f == fail_f and not self._ss_started(k, kind, which):
+                        break
+                    for _ in range(int(eqx[4 * f + k])):
+                        print(EQX_LINE)
+            return
+        max_reads = self.params.max_reads
+        n_tab = hb.s.n_tab
+        for t in range(n_tab):
+            kind_t, p = int(a["tab_kind"][t]), int(a["tab_proc"][t])
+            code = hb.name(a["tab_code"][t])
+            sampled = int(a["tab_sampled"][t])
+            for k in range(4):                                              # :183-186
+                if sampled >> k & 1:
+                    print("Family", code, "subfamily", SPLIT_NAMES[k], "has been randomly downsampled to",
+                          max_reads, "reads to form consensus read")
+            if kind_t == native_io.FAM_FILTERED:
+                print("Not enough reads in family", code, "to form consensus reads \n")       # :180
+                continue
+            failing = p == fail_f
+            self._trim_prints(hb, p, kind if failing else None, which if failing else None)
+            if failing and which >= 8:
+                return
+            for k in range(4):
+                if failing and which == k and kind == "TypeError":
+                    print("Single-strand consensus for subfamily", code, SPLIT_NAMES[k], "in progress")
+                    return
+                print("Single-strand consensus for subfamily", code, SPLIT_NAMES[k], "in progress")   # :1566-1567
+                for _ in range(int(eqx[4 * p + k])):
+                    print(EQX_LINE)
+                if failing and which == k:
+                    self._stage_prints(kind)
+                    return
+                for line in STAGE_LINES:
+                    print(line)
+            print("Double-strand consensus for family", code, "in progress")                    # :1578-1579
+            for j in range(2):
+                if failing and which == 4 + j and kind != "UnicodeEncodeError":
+                    self._stage_prints(kind)
+                    return
+                for line in STAGE_LINES:
+                    print(line)
+                if failing and which == 4 + j:
+                    return
+            is_last = last_batch and t == n_tab - 1
+            print("Consensus reads for family", code,
+                  "have been sucessfully writen \n" if is_last else "have been sucessfully written \n")  # :1597, :1631
+
+    @staticmethod
+    def _ss_started(k, kind, which):
+        """Were subfamily k's =/X lines printed before the failure?"""
+        if which >= 8:
+            return False
+        if which >= 4 or k < which:
+            return True
+        return k == which and kind != "TypeError"
+
+    @staticmethod
+    def _stage_prints(kind):
+        """Stage lines printed before a consensus call fails (:1318-1341)."""
+        n = {"exit": 2, "TypeError": 0}.get(kind, 3)
+        for line in STAGE_LINES[:n]:
+            print(line)
+
+    def _trim_prints(self, hb, p, kind, which):
+        """Verbose '3-prime N trimming' lines (:306-310): one per trailing 'N'
+        after clip removal and masking, printing the masked sequence."""
+        a = hb.a
+        mb = self.params.min_base_quality
+        r0, r1 = int(a["sub_off"][4 * p]), int(a["sub_off"][4 * p + 4])
+        for r in range(r0, r1):
+            o, n = int(a["seq_off"][r]), int(a["seq_len"][r])
+            if n == 0:
+                return
+            cig = a["cigar"][int(a["cig_off"][r]):int(a["cig_off"][r]) + int(a["cig_n"][r])]
+            s5 = s3 = 0
+            inseq = False
+            for c in cig:
+                op, ln = int(c) & 15, int(c) >> 4
+                if op == 4:
+                    if not inseq:
+                        s5 = ln
+                    else:
+                        s3 = ln
+                elif op != 5:
+                    inseq = True
+            seq = a["bases"][o + s5:o + n - s3].copy()
+            q = a["quals"][o + s5:o + n - s3]
+            seq[q < mb] = ord("N")
+            text = seq.tobytes().decode("latin-1")
+            tn = len(text) - len(text.rstrip("N"))
+            for _ in range(tn):
+                print("3-prime N trimming has been performed on read", text)
+
+    # -- one batch --------------------------------------------------------------
+    def finish(self, hb, handle, last_batch):
+        ss, ds, rstat = self.backend.result(handle)
+        F = hb.n_fam
+        fail_f, kind, which = native_io.first_failure(hb, ss, ds, F, rstat)
+        self._prints(hb, fail_f, kind, which, last_batch)
+        self.cons.write_consensus(hb, ss, ds, fail_f)
+        if fail_f < F:
+            t = int(np.nonzero(hb.a["tab_proc"][:hb.s.n_tab] == fail_f)[0][0])
+            exc_cut, filt_cut = int(hb.a["tab_exc_cut"][t]), int(hb.a["tab_filt_cut"][t])
+        else:
+            exc_cut, filt_cut = hb.s.n_side_exc, hb.s.n_side_filt
+        self.excl.write(hb.a["side_exc"][:exc_cut])
+        self.unproc.write(hb.a["side_filt"][:filt_cut])
+        if fail_f < F:
+            if kind == "exit":
+                col = badchar_column(hb, fail_f, which, self.params.min_base_quality) if which < 4 else None
+                if col is not None:
+                    print("nucleotides = ", col)
+                print(BADCHAR_LINE)
+            _raise_reference(kind)
+        if hb.end_kind == native_io.END_ERROR:
+            ek, msg = hb.error()
+            if ek == "exit":
+                print(msg)
+            _raise_reference(ek, msg)
+
+    def run(self, batch_reads):
+        """Ingest thread -> device -> writer, in input order."""
+        n_buf = 3
+        free = queue.Queue()
+        for _ in range(n_buf):
+            free.put(self.backend.host_batch(batch_reads))
+        ready = queue.Queue()
+        stop = threading.Event()
+
+        def ingest():
+            try:
+                while not stop.is_set():
+                    hb = free.get()
+                    if hb is None:
+                        return
+                    self.ing.next(hb)
+                    ready.put(hb)
+                    if hb.end_kind != native_io.END_FULL:
+                        return
+            except BaseException as e:      # surfaced in the main thread
+                ready.put(e)
+
+        th = threading.Thread(target=ingest, name="dcr-ingest", daemon=True)
+        th.start()
+        pending = None
+        try:
+            while True:
+                hb = ready.get()
+                if isinstance(hb, BaseException):
+                    raise hb
+                handle = self.backend.submit(hb)
+                if pending is not None:
+                    self.finish(*pending, last_batch=False)
+                    free.put(pending[0])
+                pending = (hb, handle)
+                if hb.end_kind != native_io.END_FULL:
+                    break
+            self.finish(*pending, last_batch=True)
+            pending = None
+        finally:
+            stop.set()
+            free.put(None)
+            th.join()
+            self.backend.close()
 
 
 def main(argv: Optional[list] = None, backend=None, rng=random) -> int:
@@ -153,13 +356,14 @@ def main(argv: Optional[list] = None, backend=None, rng=random) -> int:
     args = parse_args(sys.argv[1:] if argv is None else argv)
     params = ConsensusParams.from_args(args)
     try:
-        inbam = bam.AlignmentFile(args.input_file, "rb")
+        ing = native_io.Ingest(args.input_file, params.min_map_quality, params.min_reads, params.max_reads,
+                               params.min_base_quality, args.threads)
         if args.verbose:
             print(args.input_file, "has been read.")
     except Exception:
         print("ERROR: input file not found. \n Please specify file name of a valid .bam file. "
               "Include the format in the file name.")
-        raise SystemExit(1)
+        raise ReferenceExit(1)
     if args.output_file is None:
         consensus_filename = "%s_cons.bam" % args.input_file[:-4]
     elif args.output_file.endswith(".bam"):
@@ -167,58 +371,34 @@ def main(argv: Optional[list] = None, backend=None, rng=random) -> int:
     else:
         print("ERROR: output file is not specified in the right format. \n Please specify the file name of a "
               "valid .bam file. Include the format in the file name.")
-        raise SystemExit(1)
-    if backend is None:
-        backend = default_backend()
-    consensusbam = bam.AlignmentFile(consensus_filename, "wb", template=inbam)
-    excludedbam = bam.AlignmentFile("%s_filteredreads.bam" % consensus_filename[:-4], "wb", template=inbam)
-    unprocessedbam = bam.AlignmentFile("%s_filteredfamilies.bam" % consensus_filename[:-4], "wb", template=inbam)
-
-    run = _Run(params, backend, max(1, args.batch_families), consensusbam, unprocessedbam, args.verbose, rng)
-    passed_reads = excluded_reads = 0
-    family: Optional[list] = None
-    code = None
+        raise ReferenceExit(1)
+    be = _as_backend(backend, params)
+    lvl, nt = args.compression_level, args.threads
+    cons = native_io.BgzfWriter(consensus_filename, ing.header, lvl, nt)
+    excl = native_io.BgzfWriter("%s_filteredreads.bam" % consensus_filename[:-4], ing.header, lvl, nt)
+    unproc = native_io.BgzfWriter("%s_filteredfamilies.bam" % consensus_filename[:-4], ing.header, lvl, nt)
+    ing.set_rng_state(rng.getstate())
     try:
-        for read in inbam:
-            try:
-                ok = pass_filters(read, params.min_map_quality)
-            except BaseException:
-                run.drain()
-                raise
-            if not ok:
-                excluded_reads += 1
-                excludedbam.write(read)
-                continue
-            passed_reads += 1
-            if family is None:                         # add_read_to_family (:1202-1217)
-                family, code = [read], family_code_of(read)
-            elif family_code_of(read) == code:
-                family.append(read)
-            else:
-                run.family_done(family)
-                family, code = [read], family_code_of(read)
-        if family is None:
-            # the reference calls preprocess_family(None, None) here (:1597) -> TypeError
-            run.drain()
-            raise TypeError("'NoneType' object is not iterable")
-        run.family_done(family)
-        run.drain()
+        _Driver(args, params, be, ing, cons, excl, unproc).run(max(args.batch_reads, 1))
+        c = ing.counters()
         if args.verbose:
             print("\n Input file has been completely read \n")
-        tot_r = passed_reads + excluded_reads
-        tot_f = run.processed + run.excluded
+        passed_reads, excluded_reads = c["passed"], c["excluded"]
+        processed, excluded = c["processed"], c["filtered"]
+        tot_r, tot_f = passed_reads + excluded_reads, processed + excluded
         print("\n A total of %d reads (%.2f %%) passed the initial quality filters." %
               (passed_reads, passed_reads / tot_r * 100))
         print("\n A total of %d reads (%.2f %%) were filtered out." % (excluded_reads, excluded_reads / tot_r * 100))
         print("\n A total of %d families (%.2f %%) were successfully processed to generate a consensus read." %
-              (run.processed, run.processed / tot_f * 100))
+              (processed, processed / tot_f * 100))
         print("\n A total of %d families (%.2f %%) were filtered out due to not enough reads to generate a "
-              "consensus read." % (run.excluded, run.excluded / tot_f * 100))
+              "consensus read." % (excluded, excluded / tot_f * 100))
     finally:
-        excludedbam.close()
-        unprocessedbam.close()
-        consensusbam.close()
-        inbam.close()
+        rng.setstate(ing.rng_state(rng.getstate()))
+        excl.close()
+        unproc.close()
+        cons.close()
+        ing.close()
     return 0
 
 

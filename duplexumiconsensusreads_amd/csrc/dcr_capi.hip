@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 #include <string>
 
@@ -60,6 +61,14 @@ struct dcr_ctx {
     dcr_params *d_params = nullptr;
     DevBuf ws;          // workspace
     DevBuf io;          // staging for the host-pointer entry point
+    // streaming (dcr_submit / dcr_wait): copy streams and per-slot device buffers
+    hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+    struct Slot {
+        DevBuf buf;
+        hipEvent_t ev_h2d = nullptr, ev_comp = nullptr, ev_d2h = nullptr;
+        int *h_err = nullptr;     // pinned copy of the batch's capacity flag
+        bool busy = false;
+    } slots[DCR_MAX_SLOTS];
     dcr::Workspace w{};
     int64_t last_reads = 0;
     bool timed = false;
@@ -235,6 +244,16 @@ void dcr_destroy(dcr_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->ws.release();
     c->io.release();
+    for (auto &S : c->slots) {
+        if (S.ev_d2h) (void)hipEventSynchronize(S.ev_d2h);
+        S.buf.release();
+        if (S.ev_h2d) (void)hipEventDestroy(S.ev_h2d);
+        if (S.ev_comp) (void)hipEventDestroy(S.ev_comp);
+        if (S.ev_d2h) (void)hipEventDestroy(S.ev_d2h);
+        if (S.h_err) (void)hipHostFree(S.h_err);
+    }
+    if (c->s_h2d) (void)hipStreamDestroy(c->s_h2d);
+    if (c->s_d2h) (void)hipStreamDestroy(c->s_d2h);
     if (c->d_params) (void)hipFree(c->d_params);
     if (c->d_llr16) (void)hipFree(c->d_llr16);
     if (c->d_wtab) (void)hipFree(c->d_wtab);
@@ -465,15 +484,13 @@ int dcr_read_info_host(dcr_ctx *c, dcr_read_info *out, int64_t n) {
     return DCR_OK;
 }
 
-// host-pointer entry point: one staging allocation, H2D, run, D2H
-int dcr_run_batch_host(dcr_ctx *c, const dcr_batch *h, dcr_out *hss, dcr_out *hds) {
-    if (!c || !h || !hss || !hds) return fail(DCR_EARG, "NULL argument");
-    HIP_TRY(hipSetDevice(c->device));
+// Device layout of one batch's inputs and outputs in a single buffer:
+// returns the bytes needed; with base != nullptr also fills the device
+// views db (inputs) and dout[0..1] (single-strand, duplex outputs).
+static size_t plan_io(const dcr_batch *h, char *base, dcr_batch *db, dcr_out dout[2]) {
     const int64_t F = h->n_fam, n = h->n_reads;
-    struct Piece { const void *src; void **dst_in; size_t bytes; };
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + std::max<size_t>(bytes, 1)); return o; };
-    // inputs
     const size_t o_sub = take(sizeof(int32_t) * (4 * F + 1));
     const size_t o_pos = take(sizeof(int32_t) * n);
     const size_t o_mq = take(n);
@@ -486,7 +503,6 @@ int dcr_run_batch_host(dcr_ctx *c, const dcr_batch *h, dcr_out *hss, dcr_out *hd
     const size_t o_q = take(h->n_bases);
     const size_t o_sc = take(sizeof(int64_t) * (4 * F + 1));
     const size_t o_dc = take(sizeof(int64_t) * (2 * F + 1));
-    // outputs
     size_t oo[2][14];
     const int64_t nrec[2] = {4 * F, 2 * F};
     const int64_t ncol[2] = {h->ss_cols, h->ds_cols};
@@ -500,41 +516,21 @@ int dcr_run_batch_host(dcr_ctx *c, const dcr_batch *h, dcr_out *hss, dcr_out *hd
         oo[k][12] = take(sizeof(uint16_t) * ncol[k]);
         oo[k][13] = take(sizeof(uint16_t) * ncol[k]);
     }
-    if (off > c->io.cap) {
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        HIP_TRY(c->io.ensure(off));
-    }
-    char *d = (char *)c->io.p;
-    dcr_batch db = *h;
-    auto up = [&](size_t o, const void *src, size_t bytes) -> hipError_t {
-        if (!bytes) return hipSuccess;
-        return hipMemcpyAsync(d + o, src, bytes, hipMemcpyHostToDevice, c->stream);
-    };
-    HIP_TRY(up(o_sub, h->sub_off, sizeof(int32_t) * (4 * F + 1)));
-    HIP_TRY(up(o_pos, h->read_pos, sizeof(int32_t) * n));
-    HIP_TRY(up(o_mq, h->read_mapq, n));
-    HIP_TRY(up(o_so, h->seq_off, sizeof(int64_t) * n));
-    HIP_TRY(up(o_sl, h->seq_len, sizeof(int32_t) * n));
-    HIP_TRY(up(o_co, h->cig_off, sizeof(int32_t) * n));
-    HIP_TRY(up(o_cn, h->cig_n, sizeof(int32_t) * n));
-    HIP_TRY(up(o_cg, h->cigar, sizeof(uint32_t) * h->n_cigar));
-    HIP_TRY(up(o_b, h->bases, h->n_bases));
-    HIP_TRY(up(o_q, h->quals, h->n_bases));
-    HIP_TRY(up(o_sc, h->ss_col_off, sizeof(int64_t) * (4 * F + 1)));
-    HIP_TRY(up(o_dc, h->ds_col_off, sizeof(int64_t) * (2 * F + 1)));
-    db.sub_off = (const int32_t *)(d + o_sub);
-    db.read_pos = (const int32_t *)(d + o_pos);
-    db.read_mapq = (const uint8_t *)(d + o_mq);
-    db.seq_off = (const int64_t *)(d + o_so);
-    db.seq_len = (const int32_t *)(d + o_sl);
-    db.cig_off = (const int32_t *)(d + o_co);
-    db.cig_n = (const int32_t *)(d + o_cn);
-    db.cigar = (const uint32_t *)(d + o_cg);
-    db.bases = (const uint8_t *)(d + o_b);
-    db.quals = (const uint8_t *)(d + o_q);
-    db.ss_col_off = (const int64_t *)(d + o_sc);
-    db.ds_col_off = (const int64_t *)(d + o_dc);
-    dcr_out dout[2];
+    if (!base) return off;
+    char *d = base;
+    *db = *h;
+    db->sub_off = (const int32_t *)(d + o_sub);
+    db->read_pos = (const int32_t *)(d + o_pos);
+    db->read_mapq = (const uint8_t *)(d + o_mq);
+    db->seq_off = (const int64_t *)(d + o_so);
+    db->seq_len = (const int32_t *)(d + o_sl);
+    db->cig_off = (const int32_t *)(d + o_co);
+    db->cig_n = (const int32_t *)(d + o_cn);
+    db->cigar = (const uint32_t *)(d + o_cg);
+    db->bases = (const uint8_t *)(d + o_b);
+    db->quals = (const uint8_t *)(d + o_q);
+    db->ss_col_off = (const int64_t *)(d + o_sc);
+    db->ds_col_off = (const int64_t *)(d + o_dc);
     for (int k = 0; k < 2; ++k) {
         dout[k].status = (uint8_t *)(d + oo[k][0]);
         dout[k].pos = (int32_t *)(d + oo[k][1]);
@@ -551,31 +547,138 @@ int dcr_run_batch_host(dcr_ctx *c, const dcr_batch *h, dcr_out *hss, dcr_out *hd
         dout[k].d = (uint16_t *)(d + oo[k][12]);
         dout[k].e = (uint16_t *)(d + oo[k][13]);
     }
+    return off;
+}
+
+// the host batch's inputs -> device views (async on stream s)
+static hipError_t upload_inputs(const dcr_batch *h, const dcr_batch &db, hipStream_t s) {
+    const int64_t F = h->n_fam, n = h->n_reads;
+    struct P { void *dst; const void *src; size_t bytes; } ps[12] = {
+        {(void *)db.sub_off, h->sub_off, sizeof(int32_t) * (4 * F + 1)},
+        {(void *)db.read_pos, h->read_pos, sizeof(int32_t) * n},
+        {(void *)db.read_mapq, h->read_mapq, (size_t)n},
+        {(void *)db.seq_off, h->seq_off, sizeof(int64_t) * n},
+        {(void *)db.seq_len, h->seq_len, sizeof(int32_t) * n},
+        {(void *)db.cig_off, h->cig_off, sizeof(int32_t) * n},
+        {(void *)db.cig_n, h->cig_n, sizeof(int32_t) * n},
+        {(void *)db.cigar, h->cigar, sizeof(uint32_t) * h->n_cigar},
+        {(void *)db.bases, h->bases, (size_t)h->n_bases},
+        {(void *)db.quals, h->quals, (size_t)h->n_bases},
+        {(void *)db.ss_col_off, h->ss_col_off, sizeof(int64_t) * (4 * F + 1)},
+        {(void *)db.ds_col_off, h->ds_col_off, sizeof(int64_t) * (2 * F + 1)}};
+    for (auto &p : ps)
+        if (p.bytes) {
+            hipError_t e = hipMemcpyAsync(p.dst, p.src, p.bytes, hipMemcpyHostToDevice, s);
+            if (e != hipSuccess) return e;
+        }
+    return hipSuccess;
+}
+
+// device outputs -> the host dcr_out arrays that are not NULL (async on stream s)
+static hipError_t download_outputs(const dcr_out *dev, dcr_out *host, int64_t R, int64_t C, hipStream_t s) {
+    struct P { void *dst; const void *src; size_t bytes; } ps[14] = {
+        {host->status, dev->status, (size_t)R}, {host->pos, dev->pos, 4 * (size_t)R},
+        {host->mapq, dev->mapq, 4 * (size_t)R}, {host->len, dev->len, 4 * (size_t)R},
+        {host->n_cig, dev->n_cig, 4 * (size_t)R}, {host->n_de, dev->n_de, 4 * (size_t)R},
+        {host->D, dev->D, 4 * (size_t)R}, {host->M, dev->M, 4 * (size_t)R}, {host->E, dev->E, 8 * (size_t)R},
+        {host->seq, dev->seq, (size_t)C}, {host->qual, dev->qual, (size_t)C},
+        {host->cigar, dev->cigar, 4 * (size_t)C}, {host->d, dev->d, 2 * (size_t)C}, {host->e, dev->e, 2 * (size_t)C}};
+    for (auto &p : ps)
+        if (p.dst && p.bytes) {
+            hipError_t e = hipMemcpyAsync(p.dst, p.src, p.bytes, hipMemcpyDeviceToHost, s);
+            if (e != hipSuccess) return e;
+        }
+    return hipSuccess;
+}
+
+// host-pointer entry point: one staging allocation, H2D, run, D2H
+int dcr_run_batch_host(dcr_ctx *c, const dcr_batch *h, dcr_out *hss, dcr_out *hds) {
+    if (!c || !h || !hss || !hds) return fail(DCR_EARG, "NULL argument");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t need = plan_io(h, nullptr, nullptr, nullptr);
+    if (need > c->io.cap) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(c->io.ensure(need));
+    }
+    dcr_batch db;
+    dcr_out dout[2];
+    plan_io(h, (char *)c->io.p, &db, dout);
+    HIP_TRY(upload_inputs(h, db, c->stream));
     int rc = dcr_run_batch(c, &db, &dout[0], &dout[1]);
     if (rc) return rc;
-    dcr_out *hh[2] = {hss, hds};
-    for (int k = 0; k < 2; ++k) {
-        auto dn = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
-            if (!bytes || !dst) return hipSuccess;
-            return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream);
-        };
-        const size_t R = nrec[k], C = ncol[k];
-        HIP_TRY(dn(hh[k]->status, dout[k].status, R));
-        HIP_TRY(dn(hh[k]->pos, dout[k].pos, 4 * R));
-        HIP_TRY(dn(hh[k]->mapq, dout[k].mapq, 4 * R));
-        HIP_TRY(dn(hh[k]->len, dout[k].len, 4 * R));
-        HIP_TRY(dn(hh[k]->n_cig, dout[k].n_cig, 4 * R));
-        HIP_TRY(dn(hh[k]->n_de, dout[k].n_de, 4 * R));
-        HIP_TRY(dn(hh[k]->D, dout[k].D, 4 * R));
-        HIP_TRY(dn(hh[k]->M, dout[k].M, 4 * R));
-        HIP_TRY(dn(hh[k]->E, dout[k].E, 8 * R));
-        HIP_TRY(dn(hh[k]->seq, dout[k].seq, C));
-        HIP_TRY(dn(hh[k]->qual, dout[k].qual, C));
-        HIP_TRY(dn(hh[k]->cigar, dout[k].cigar, 4 * C));
-        HIP_TRY(dn(hh[k]->d, dout[k].d, 2 * C));
-        HIP_TRY(dn(hh[k]->e, dout[k].e, 2 * C));
-    }
+    HIP_TRY(download_outputs(&dout[0], hss, 4 * (int64_t)h->n_fam, h->ss_cols, c->stream));
+    HIP_TRY(download_outputs(&dout[1], hds, 2 * (int64_t)h->n_fam, h->ds_cols, c->stream));
     return dcr_sync(c);
+}
+
+// ---- streaming (pinned host batches, per-slot device buffers, copy streams) ----
+
+void *dcr_host_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocDefault) != hipSuccess) {
+        g_err = "hipHostMalloc failed";
+        return nullptr;
+    }
+    return p;
+}
+
+void dcr_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
+int dcr_submit(dcr_ctx *c, int slot, const dcr_batch *h, dcr_out *hss, dcr_out *hds, int32_t *read_status) {
+    if (!c || !h || !hss || !hds) return fail(DCR_EARG, "NULL argument");
+    if (slot < 0 || slot >= DCR_MAX_SLOTS) return fail(DCR_EARG, "slot out of range");
+    HIP_TRY(hipSetDevice(c->device));
+    if (!c->s_h2d) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->s_h2d, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&c->s_d2h, hipStreamNonBlocking));
+    }
+    dcr_ctx::Slot &S = c->slots[slot];
+    if (!S.ev_h2d) {
+        HIP_TRY(hipEventCreateWithFlags(&S.ev_h2d, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&S.ev_comp, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&S.ev_d2h, hipEventDisableTiming));
+        HIP_TRY(hipHostMalloc((void **)&S.h_err, sizeof(int), hipHostMallocDefault));
+        *S.h_err = 0;
+    }
+    if (S.busy) return fail(DCR_EARG, "slot still in flight (dcr_wait it first)");
+    const size_t need = plan_io(h, nullptr, nullptr, nullptr);
+    if (need > S.buf.cap) HIP_TRY(S.buf.ensure(need + need / 8));   // idle slot: nothing in flight uses it
+    dcr_batch db;
+    dcr_out dout[2];
+    plan_io(h, (char *)S.buf.p, &db, dout);
+    // H2D on the copy stream
+    HIP_TRY(upload_inputs(h, db, c->s_h2d));
+    HIP_TRY(hipEventRecord(S.ev_h2d, c->s_h2d));
+    // kernels on the compute stream
+    HIP_TRY(hipStreamWaitEvent(c->stream, S.ev_h2d, 0));
+    int rc = dcr_run_batch(c, &db, &dout[0], &dout[1]);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(S.h_err, c->w.err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    if (read_status && h->n_reads > 0)
+        HIP_TRY(hipMemcpy2DAsync(read_status, sizeof(int32_t), (const char *)c->w.info + offsetof(dcr_read_info, status),
+                                 sizeof(dcr_read_info), sizeof(int32_t), (size_t)h->n_reads, hipMemcpyDeviceToHost,
+                                 c->stream));
+    HIP_TRY(hipEventRecord(S.ev_comp, c->stream));
+    // D2H of the outputs on the second copy stream
+    HIP_TRY(hipStreamWaitEvent(c->s_d2h, S.ev_comp, 0));
+    HIP_TRY(download_outputs(&dout[0], hss, 4 * (int64_t)h->n_fam, h->ss_cols, c->s_d2h));
+    HIP_TRY(download_outputs(&dout[1], hds, 2 * (int64_t)h->n_fam, h->ds_cols, c->s_d2h));
+    HIP_TRY(hipEventRecord(S.ev_d2h, c->s_d2h));
+    S.busy = true;
+    return DCR_OK;
+}
+
+int dcr_wait(dcr_ctx *c, int slot) {
+    if (!c || slot < 0 || slot >= DCR_MAX_SLOTS) return fail(DCR_EARG, "bad argument");
+    dcr_ctx::Slot &S = c->slots[slot];
+    if (!S.busy) return DCR_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipEventSynchronize(S.ev_d2h));
+    S.busy = false;
+    if (*S.h_err) return fail(DCR_ECAPACITY, "a consensus needed more columns than its output region");
+    return DCR_OK;
 }
 
 }  // extern "C"

@@ -1,0 +1,412 @@
+// dcr_format.cpp — native writer side (include/dcr_io.h): the duplex
+// consensus records of a batch, built from kernel outputs with the
+// reference's exact field and tag layout, and a BGZF writer that deflates
+// blocks on a worker pool (libdeflate).
+//
+// Reference (/root/reference/DuplexUMIConsensusReads.py):
+//   record fields        make_consensus_read :1352-1384
+//   name / flag          get_consensus_id :892-933, get_consensus_flag :936-968
+//   duplex tags          add_tags(method="double_strand") :1076-1120
+//   mate fields          fix_paired_end_fields :1390-1419
+//   pysam typing         smallest integer type, 'f' float32, 'Z' text, 'B' arrays;
+//                        sd/se text is str() of a list of numpy-1.x ints: "[1, 2]"
+#include <cctype>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/dcr.h"
+#include "../../include/dcr_io.h"
+#include "dcr_host.h"
+
+using namespace dcrh;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &m) {
+    g_err = m;
+    return code;
+}
+
+constexpr size_t kBlockData = 0xff00;
+const uint8_t kEof[28] = {0x1f, 0x8b, 0x08, 0x04, 0x00, 0x00, 0x00, 0x00, 0x00, 0xff, 0x06, 0x00, 0x42, 0x43,
+                          0x02, 0x00, 0x1b, 0x00, 0x03, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00};
+
+struct TLComp {
+    libdeflate_compressor *c[13] = {};
+    ~TLComp() {
+        for (auto *p : c)
+            if (p) libdeflate_free_compressor(p);
+    }
+    libdeflate_compressor *get(int level) {
+        if (!c[level]) c[level] = libdeflate_alloc_compressor(level);
+        return c[level];
+    }
+};
+thread_local TLComp tl_comp;
+
+// ASCII -> 4-bit BAM code ("=ACMGRSVTWYHKDBN", either case; unknown 15)
+struct NtTable {
+    uint8_t code[256];
+    NtTable() {
+        std::memset(code, 15, sizeof code);
+        const char *a = "=ACMGRSVTWYHKDBN";
+        for (int i = 0; i < 16; ++i) {
+            code[(uint8_t)a[i]] = (uint8_t)i;
+            code[(uint8_t)std::tolower(a[i])] = (uint8_t)i;
+        }
+    }
+};
+const NtTable kNt;
+
+// SAM spec §5.3 bin of [beg, end)
+int reg2bin(int64_t beg, int64_t end) {
+    --end;
+    if (beg >> 14 == end >> 14) return (int)(((1 << 15) - 1) / 7 + (beg >> 14));
+    if (beg >> 17 == end >> 17) return (int)(((1 << 12) - 1) / 7 + (beg >> 17));
+    if (beg >> 20 == end >> 20) return (int)(((1 << 9) - 1) / 7 + (beg >> 20));
+    if (beg >> 23 == end >> 23) return (int)(((1 << 6) - 1) / 7 + (beg >> 23));
+    if (beg >> 26 == end >> 26) return (int)(((1 << 3) - 1) / 7 + (beg >> 26));
+    return 0;
+}
+
+// growable byte buffer with unchecked appends after reserve()
+struct Buf {
+    std::vector<uint8_t> v;
+    size_t n = 0;
+    void reserve(size_t more) {
+        if (n + more > v.size()) v.resize(std::max(v.size() * 2, n + more + (1 << 20)));
+    }
+    uint8_t *p() { return v.data() + n; }
+    void b(uint8_t x) { v[n++] = x; }
+    void raw(const void *s, size_t k) { std::memcpy(v.data() + n, s, k); n += k; }
+    void u16(uint32_t x) { wr16(p(), x); n += 2; }
+    void u32(uint32_t x) { wr32(p(), x); n += 4; }
+    void str(const char *s) { raw(s, std::strlen(s)); }
+    void uint(uint32_t x) {
+        char t[12];
+        int k = 0;
+        do { t[k++] = (char)('0' + x % 10); x /= 10; } while (x);
+        while (k) v[n++] = (uint8_t)t[--k];
+    }
+    void sint(int64_t x) {
+        if (x < 0) { v[n++] = '-'; x = -x; }
+        char t[24];
+        int k = 0;
+        do { t[k++] = (char)('0' + x % 10); x /= 10; } while (x);
+        while (k) v[n++] = (uint8_t)t[--k];
+    }
+};
+
+// pysam's type code for an untyped int tag value (>= 0 here)
+void int_tag(Buf &o, const char *tag, int64_t v) {
+    o.raw(tag, 2);
+    if (v < 0) {
+        if (v >= -128) { o.b('c'); o.b((uint8_t)(int8_t)v); }
+        else if (v >= -32768) { o.b('s'); o.u16((uint32_t)(uint16_t)(int16_t)v); }
+        else { o.b('i'); o.u32((uint32_t)(int32_t)v); }
+    } else if (v <= 255) { o.b('C'); o.b((uint8_t)v); }
+    else if (v <= 65535) { o.b('S'); o.u16((uint32_t)v); }
+    else { o.b('I'); o.u32((uint32_t)v); }
+}
+
+void float_tag(Buf &o, const char *tag, double v) {
+    o.raw(tag, 2);
+    o.b('f');
+    const float f = (float)v;
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    o.u32(u);
+}
+
+void z_begin(Buf &o, const char *tag) { o.raw(tag, 2); o.b('Z'); }
+
+// "[1, 2, 3]" (str() of a list of numpy-1.x ints)
+void list_text(Buf &o, const char *tag, const uint16_t *v, int32_t n) {
+    z_begin(o, tag);
+    o.b('[');
+    for (int32_t i = 0; i < n; ++i) {
+        if (i) { o.b(','); o.b(' '); }
+        o.uint(v[i]);
+    }
+    o.b(']');
+    o.b(0);
+}
+
+// B:C array of uint8 values (pysam infers 'C' for ints in 0..255)
+void u8_array(Buf &o, const char *tag, const uint8_t *v, int32_t n) {
+    o.raw(tag, 2);
+    o.b('B');
+    o.b('C');
+    o.u32((uint32_t)n);
+    o.raw(v, (size_t)n);
+}
+
+
+struct Ctx {
+    const dcr_host_batch *hb;
+    const dcr_fmt_out *ss, *ds;
+};
+
+}  // namespace
+
+struct dcr_bgzw {
+    FILE *f = nullptr;
+    int level = 6;
+    std::unique_ptr<Pool> pool;
+    std::vector<uint8_t> in;     // pending uncompressed bytes
+    size_t n_in = 0;
+    std::vector<std::vector<uint8_t>> out;
+    std::vector<size_t> out_len;
+    int64_t bytes_in = 0, bytes_out = 0;
+    bool bad = false;
+
+    // deflate in[0, n) as blocks of 0xff00 bytes on the pool, write in order
+    bool flush(size_t n) {
+        const size_t nb = (n + kBlockData - 1) / kBlockData;
+        if (out.size() < nb) { out.resize(nb); out_len.resize(nb); }
+        const int lvl = level;
+        const bool ok = pool->run(nb, [&](size_t i) {
+            const size_t off = i * kBlockData, len = std::min(kBlockData, n - off);
+            std::vector<uint8_t> &o = out[i];
+            if (o.size() < 0x10000) o.resize(0x10000);
+            size_t clen = libdeflate_deflate_compress(tl_comp.get(lvl), in.data() + off, len, o.data() + 18,
+                                                      0x10000 - 26);
+            if (clen == 0) clen = libdeflate_deflate_compress(tl_comp.get(0), in.data() + off, len, o.data() + 18,
+                                                              0x10000 - 26);
+            if (clen == 0) return false;
+            uint8_t *h = o.data();
+            h[0] = 0x1f; h[1] = 0x8b; h[2] = 8; h[3] = 4;
+            wr32(h + 4, 0); h[8] = 0; h[9] = 0xff;
+            wr16(h + 10, 6); h[12] = 66; h[13] = 67; wr16(h + 14, 2);
+            wr16(h + 16, (uint32_t)(clen + 25));
+            wr32(o.data() + 18 + clen, libdeflate_crc32(0, in.data() + off, len));
+            wr32(o.data() + 22 + clen, (uint32_t)len);
+            out_len[i] = clen + 26;
+            return true;
+        });
+        if (!ok) { g_err = "BGZF block failed to deflate"; return false; }
+        for (size_t i = 0; i < nb; ++i) {
+            if (std::fwrite(out[i].data(), 1, out_len[i], f) != out_len[i]) { g_err = "write failed"; return false; }
+            bytes_out += (int64_t)out_len[i];
+        }
+        bytes_in += (int64_t)n;
+        return true;
+    }
+    bool write(const uint8_t *s, size_t n) {
+        while (n > 0) {
+            const size_t k = std::min(in.size() - n_in, n);
+            std::memcpy(in.data() + n_in, s, k);
+            n_in += k; s += k; n -= k;
+            if (n_in == in.size()) {
+                if (!flush(n_in)) return false;
+                n_in = 0;
+            }
+        }
+        return true;
+    }
+};
+
+namespace {
+
+// one duplex record (pe j of processed family f)
+void format_record(const Ctx &c, int32_t f, int j, const char *code, size_t l_code, Buf &o) {
+    const dcr_host_batch *hb = c.hb;
+    const dcr_fmt_out *ss = c.ss, *ds = c.ds;
+    const int32_t k = 2 * f + j, a = 4 * f + 2 * j, b = a + 1;
+    const int32_t pos = ds->pos[k], opos = ds->pos[2 * f + 1 - j];
+    const int32_t len = ds->len[k];
+    const int32_t tlen = ds->pos[2 * f + 1] + ds->len[2 * f + 1] - ds->pos[2 * f];
+    const int32_t tid = hb->fam_tid[f];
+    const int64_t ro = hb->ds_col_off[k], ao = hb->ss_col_off[a], bo = hb->ss_col_off[b];
+    const size_t rec0 = o.n;
+    o.u32(0);                                        // block_size
+    o.u32((uint32_t)tid);                            // reference_id = read0's (:1363)
+    o.u32((uint32_t)pos);                            // reference_start (:790)
+    const char *pe = j == 0 ? "_paired-end1" : "_paired-end2";
+    const size_t l_rn = 16 + l_code + 12 + 1;        // "consensus_family" code pe NUL
+    o.b((uint8_t)l_rn);
+    o.b((uint8_t)(ds->mapq[k] & 0xff));
+    int64_t rl = 0;
+    const uint32_t *cg = ds->cigar + ro;
+    const int32_t nc = ds->n_cig[k];
+    for (int32_t i = 0; i < nc; ++i) {
+        const uint32_t op = cg[i] & 15;
+        if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += cg[i] >> 4;
+    }
+    o.u16(pos >= 0 ? (uint32_t)reg2bin(pos, pos + (rl > 0 ? rl : 1)) : 4680u);
+    o.u16((uint32_t)nc);
+    o.u16(j == 0 ? 99u : 147u);                      // get_consensus_flag (:959-963)
+    o.u32((uint32_t)len);
+    o.u32((uint32_t)tid);                            // fix_paired_end_fields (:1406-1416)
+    o.u32((uint32_t)opos);
+    o.u32((uint32_t)(j == 0 ? tlen : -tlen));
+    o.str("consensus_family");                       // get_consensus_id (:925-933)
+    o.raw(code, l_code);
+    o.str(pe);
+    o.b(0);
+    for (int32_t i = 0; i < nc; ++i) o.u32(cg[i]);
+    const uint8_t *sq = ds->seq + ro;
+    for (int32_t i = 0; i + 1 < len; i += 2) o.b((uint8_t)((kNt.code[sq[i]] << 4) | kNt.code[sq[i + 1]]));
+    if (len & 1) o.b((uint8_t)(kNt.code[sq[len - 1]] << 4));
+    o.raw(ds->qual + ro, (size_t)len);
+    // tags, in add_tags' order (:1117-1120)
+    z_begin(o, "MI");
+    o.raw(code, l_code);
+    o.b(0);
+    z_begin(o, "RX");
+    o.str(hb->names + hb->fam_rx[2 * f + j]);
+    o.b(0);
+    const int32_t a0 = hb->sub_off[a], a1 = hb->sub_off[a + 1], b0 = hb->sub_off[b], b1 = hb->sub_off[b + 1];
+    u8_array(o, "aQ", hb->read_mapq + a0, a1 - a0);
+    u8_array(o, "bQ", hb->read_mapq + b0, b1 - b0);
+    // cQ: the two single-strand MAPQs (ints <= 255 -> 'C')
+    o.raw("cQ", 2); o.b('B'); o.b('C'); o.u32(2);
+    o.b((uint8_t)ss->mapq[a]); o.b((uint8_t)ss->mapq[b]);
+    list_text(o, "ad", ss->d + ao, ss->n_de[a]);
+    list_text(o, "bd", ss->d + bo, ss->n_de[b]);
+    list_text(o, "cd", ds->d + ro, ds->n_de[k]);
+    int_tag(o, "aD", ss->D[a]); int_tag(o, "bD", ss->D[b]); int_tag(o, "cD", ds->D[k]);
+    int_tag(o, "aM", ss->M[a]); int_tag(o, "bM", ss->M[b]); int_tag(o, "cM", ds->M[k]);
+    list_text(o, "ae", ss->e + ao, ss->n_de[a]);
+    list_text(o, "be", ss->e + bo, ss->n_de[b]);
+    list_text(o, "ce", ds->e + ro, ds->n_de[k]);
+    float_tag(o, "aE", ss->E[a]); float_tag(o, "bE", ss->E[b]); float_tag(o, "cE", ds->E[k]);
+    z_begin(o, "ac"); o.raw(ss->seq + ao, (size_t)ss->len[a]); o.b(0);
+    z_begin(o, "bc"); o.raw(ss->seq + bo, (size_t)ss->len[b]); o.b(0);
+    z_begin(o, "aq");
+    for (int32_t i = 0; i < ss->len[a]; ++i) o.b((uint8_t)(ss->qual[ao + i] + 33));
+    o.b(0);
+    z_begin(o, "bq");
+    for (int32_t i = 0; i < ss->len[b]; ++i) o.b((uint8_t)(ss->qual[bo + i] + 33));
+    o.b(0);
+    wr32(o.v.data() + rec0, (uint32_t)(o.n - rec0 - 4));
+}
+
+size_t record_bound(const Ctx &c, int32_t f, int j, size_t l_code) {
+    const int32_t k = 2 * f + j, a = 4 * f + 2 * j, b = a + 1;
+    size_t n = 36 + 16 + l_code + 13 + 4 * (size_t)c.ds->n_cig[k] + (size_t)c.ds->len[k] * 2;
+    n += 8 + l_code + 4 + std::strlen(c.hb->names + c.hb->fam_rx[2 * f + j]);
+    n += 24 + (size_t)(c.hb->sub_off[a + 1] - c.hb->sub_off[a]) + (size_t)(c.hb->sub_off[b + 1] - c.hb->sub_off[b]);
+    n += 16 + 7 * (2 * (size_t)c.ss->n_de[a] + 2 * (size_t)c.ss->n_de[b] + 2 * (size_t)c.ds->n_de[k]) + 64;
+    n += 9 * 8 + 3 * 8 + 2 * ((size_t)c.ss->len[a] + c.ss->len[b]) + 32;
+    return n;
+}
+
+}  // namespace
+
+extern "C" {
+
+dcr_bgzw *dcr_bgzw_open(const char *path, int level, int n_threads) {
+    if (!path || level < 0 || level > 12) { g_err = "bad arguments"; return nullptr; }
+    FILE *f = std::fopen(path, "wb");
+    if (!f) { g_err = std::string("cannot open ") + path; return nullptr; }
+    auto *w = new dcr_bgzw;
+    w->f = f;
+    w->level = level;
+    w->pool.reset(new Pool(pick_threads(n_threads)));
+    w->in.resize(kBlockData * (size_t)std::max(64, 8 * w->pool->size()));
+    return w;
+}
+
+int dcr_bgzw_write(dcr_bgzw *w, const void *bytes, int64_t n) {
+    if (!w || n < 0 || (n > 0 && !bytes)) return fail(DCR_IO_EARG, "bad arguments");
+    if (w->bad) return fail(DCR_IO_EFILE, "writer failed earlier");
+    if (!w->write((const uint8_t *)bytes, (size_t)n)) { w->bad = true; return DCR_IO_EFILE; }
+    return DCR_IO_OK;
+}
+
+int dcr_bgzw_close(dcr_bgzw *w) {
+    if (!w) return fail(DCR_IO_EARG, "NULL writer");
+    int rc = DCR_IO_OK;
+    if (!w->bad && w->n_in && !w->flush(w->n_in)) rc = DCR_IO_EFILE;
+    if (std::fwrite(kEof, 1, sizeof kEof, w->f) != sizeof kEof) rc = fail(DCR_IO_EFILE, "write failed");
+    if (std::fclose(w->f) != 0) rc = fail(DCR_IO_EFILE, "close failed");
+    delete w;
+    return rc;
+}
+
+int dcr_bgzw_sizes(dcr_bgzw *w, int64_t *out2) {
+    if (!w || !out2) return fail(DCR_IO_EARG, "NULL argument");
+    out2[0] = w->bytes_out;
+    out2[1] = w->bytes_in + (int64_t)w->n_in;
+    return DCR_IO_OK;
+}
+
+int32_t dcr_fmt_scan(const dcr_host_batch *hb, const dcr_fmt_out *ss, const dcr_fmt_out *ds,
+                     const int32_t *read_status, int32_t n_fam, int32_t *kind, int32_t *which) {
+    *kind = DCR_FAIL_NONE;
+    *which = -1;
+    auto st_fail = [](int st) { return st != 0 && st != DCR_ST_UPSTREAM && !(st & 0x10); };
+    auto unicode = [&](int32_t s) {
+        const int64_t o = hb->ss_col_off[s];
+        for (int32_t i = 0; i < ss->len[s]; ++i)
+            if (ss->qual[o + i] >= 95) return true;   // chr(q + 33) outside ASCII
+        return false;
+    };
+    for (int32_t f = 0; f < n_fam; ++f) {
+        // preprocess_family's read loop (:1272-1283): the first failing read
+        if (read_status) {
+            for (int32_t r = hb->sub_off[4 * f]; r < hb->sub_off[4 * f + 4]; ++r)
+                if (read_status[r]) {
+                    *kind = read_status[r];
+                    int k = 0;
+                    while (r >= hb->sub_off[4 * f + k + 1]) ++k;
+                    *which = 8 + k;
+                    return f;
+                }
+        } else {
+            for (int k = 0; k < 4; ++k)
+                if (ss->status[4 * f + k] & 0x10) { *kind = ss->status[4 * f + k] & 0x0f; *which = 8 + k; return f; }
+        }
+        for (int k = 0; k < 4; ++k)                   // make_consensus_read x4 (:1564-1569)
+            if (st_fail(ss->status[4 * f + k])) { *kind = ss->status[4 * f + k]; *which = k; return f; }
+        for (int j = 0; j < 2; ++j) {                 // x2 duplex (:1581-1582), then its set_tags (:1384)
+            if (st_fail(ds->status[2 * f + j])) { *kind = ds->status[2 * f + j]; *which = 4 + j; return f; }
+            if (unicode(4 * f + 2 * j) || unicode(4 * f + 2 * j + 1)) { *kind = DCR_FAIL_UNICODE; *which = 4 + j; return f; }
+        }
+    }
+    return n_fam;
+}
+
+int dcr_fmt_write(dcr_bgzw *w, const dcr_host_batch *hb, const dcr_fmt_out *ss, const dcr_fmt_out *ds,
+                  int32_t n_fam) {
+    if (!w || !hb || !ss || !ds || n_fam < 0 || n_fam > hb->n_fam) return fail(DCR_IO_EARG, "bad arguments");
+    if (w->bad) return fail(DCR_IO_EFILE, "writer failed earlier");
+    // family code per processed family (from the family table)
+    std::vector<int64_t> code_of((size_t)n_fam, -1);
+    for (int32_t t = 0; t < hb->n_tab; ++t)
+        if (hb->tab_kind[t] == DCR_FAM_PROCESSED && hb->tab_proc[t] < n_fam) code_of[(size_t)hb->tab_proc[t]] = hb->tab_code[t];
+    const Ctx c{hb, ss, ds};
+    const int32_t chunk = 512;
+    const int32_t nch = (n_fam + chunk - 1) / chunk;
+    // format chunks of families in parallel, append them in order
+    const int32_t group = std::max(1, 4 * w->pool->size());
+    std::vector<Buf> bufs((size_t)std::min(nch, group));
+    for (int32_t g0 = 0; g0 < nch; g0 += group) {
+        const int32_t g1 = std::min(nch, g0 + group);
+        w->pool->run((size_t)(g1 - g0), [&](size_t gi) {
+            Buf &o = bufs[gi];
+            o.n = 0;
+            const int32_t f0 = (g0 + (int32_t)gi) * chunk, f1 = std::min(n_fam, f0 + chunk);
+            for (int32_t f = f0; f < f1; ++f) {
+                const char *code = hb->names + code_of[(size_t)f];
+                const size_t lc = std::strlen(code);
+                for (int j = 0; j < 2; ++j) {
+                    o.reserve(record_bound(c, f, j, lc));
+                    format_record(c, f, j, code, lc, o);
+                }
+            }
+            return true;
+        });
+        for (int32_t gi = 0; gi < g1 - g0; ++gi)
+            if (!w->write(bufs[(size_t)gi].v.data(), bufs[(size_t)gi].n)) { w->bad = true; return DCR_IO_EFILE; }
+    }
+    return DCR_IO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,814 @@
+// dcr_ingest.cpp — native BAM ingest (include/dcr_io.h): BGZF inflate on a
+// worker pool, record walk, the reference's read filters, MI grouping,
+// family checks, the four-way split and check_number_reads' random.sample
+// (CPython's MT19937, bit for bit), and packing of processed families into
+// the dcr_batch layout the GPU consumes.
+//
+// Per batch the work splits into a serial walk (record boundaries, filters,
+// grouping, RNG; a few loads per record) and parallel parts (inflate of the
+// next window of BGZF blocks; per-read copies of sequence / qualities /
+// CIGAR into the caller's pinned arrays, queued by the walk as jobs).
+//
+// Reference: /root/reference/DuplexUMIConsensusReads.py (":line" below).
+#include <zlib.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/dcr_io.h"
+#include "dcr_host.h"
+
+using namespace dcrh;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &m) {
+    g_err = m;
+    return code;
+}
+
+struct TLDecomp {
+    libdeflate_decompressor *d = nullptr;
+    ~TLDecomp() {
+        if (d) libdeflate_free_decompressor(d);
+    }
+    libdeflate_decompressor *get() {
+        if (!d) d = libdeflate_alloc_decompressor();
+        return d;
+    }
+};
+thread_local TLDecomp tl_dec;
+
+// ---------------------------------------------------------------------------
+// CPython's random.Random (Modules/_randommodule.c genrand_uint32, getrandbits
+// for k <= 32; Lib/random.py 3.10 _randbelow_with_getrandbits and sample)
+struct PyRandom {
+    uint32_t mt[624];
+    int index = 625;
+    bool seeded = false;
+
+    uint32_t genrand() {
+        static const uint32_t mag01[2] = {0x0u, 0x9908b0dfu};
+        const int N = 624, M = 397;
+        uint32_t y;
+        if (index >= N) {
+            int kk;
+            for (kk = 0; kk < N - M; kk++) {
+                y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+                mt[kk] = mt[kk + M] ^ (y >> 1) ^ mag01[y & 1u];
+            }
+            for (; kk < N - 1; kk++) {
+                y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+                mt[kk] = mt[kk + (M - N)] ^ (y >> 1) ^ mag01[y & 1u];
+            }
+            y = (mt[N - 1] & 0x80000000u) | (mt[0] & 0x7fffffffu);
+            mt[N - 1] = mt[M - 1] ^ (y >> 1) ^ mag01[y & 1u];
+            index = 0;
+        }
+        y = mt[index++];
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= (y >> 18);
+        return y;
+    }
+    static int bit_length(uint32_t n) {
+        int k = 0;
+        while (n) { ++k; n >>= 1; }
+        return k;
+    }
+    uint32_t randbelow(uint32_t n) {
+        if (!n) return 0;
+        const int k = bit_length(n);   // n < 2^31 here, so k <= 31
+        uint32_t r = genrand() >> (32 - k);
+        while (r >= n) r = genrand() >> (32 - k);
+        return r;
+    }
+    // random.sample(range(n), k) -> indices in selection order
+    void sample(int n, int k, std::vector<int> &out) {
+        out.assign((size_t)k, 0);
+        long setsize = 21;
+        if (k > 5) setsize += (long)std::pow(4.0, std::ceil(std::log((double)k * 3) / std::log(4.0)));
+        if (n <= setsize) {
+            std::vector<int> pool((size_t)n);
+            for (int i = 0; i < n; ++i) pool[(size_t)i] = i;
+            for (int i = 0; i < k; ++i) {
+                const int j = (int)randbelow((uint32_t)(n - i));
+                out[(size_t)i] = pool[(size_t)j];
+                pool[(size_t)j] = pool[(size_t)(n - i - 1)];
+            }
+        } else {
+            std::vector<char> sel((size_t)n, 0);
+            for (int i = 0; i < k; ++i) {
+                int j = (int)randbelow((uint32_t)n);
+                while (sel[(size_t)j]) j = (int)randbelow((uint32_t)n);
+                sel[(size_t)j] = 1;
+                out[(size_t)i] = j;
+            }
+        }
+    }
+};
+
+// 4-bit BAM sequence code pairs -> two ASCII bases ("=ACMGRSVTWYHKDBN")
+struct SeqTable {
+    uint16_t pair[256];
+    SeqTable() {
+        const char *a = "=ACMGRSVTWYHKDBN";
+        for (int b = 0; b < 256; ++b) pair[b] = (uint16_t)((uint8_t)a[b >> 4] | ((uint8_t)a[b & 15] << 8));
+    }
+};
+const SeqTable kSeq;
+
+// One parsed record (offsets relative to the window start)
+struct Rec {
+    size_t off;         // offset of block_size
+    uint32_t len;       // 4 + block_size
+    int32_t tid, pos;
+    uint16_t flag, n_cig;
+    uint8_t mapq;
+    int32_t l_seq;
+    uint32_t o_cig, o_seq, o_qual;   // offsets of the fields from off
+    uint32_t o_mi, o_rx;             // offsets of the MI / RX string values (0: absent)
+    uint16_t l_mi, l_rx;             // string lengths
+    uint8_t mi_type, rx_type;        // tag type codes ('Z' expected)
+    uint16_t l_code;                 // MI prefix before the first '/'
+};
+
+struct Job {
+    size_t rec;         // window offset of the record
+    int64_t dst_base;
+    int64_t dst_cig;
+};
+
+}  // namespace
+
+struct dcr_ingest {
+    FILE *f = nullptr;
+    dcr_ingest_cfg cfg{};
+    std::unique_ptr<Pool> pool;
+    // compressed input
+    std::vector<uint8_t> cbuf;
+    size_t cbeg = 0, cend = 0;
+    bool file_eof = false;
+    // decompressed window
+    std::vector<uint8_t> win;
+    size_t wpos = 0, wend = 0;
+    bool data_eof = false;
+    std::vector<uint8_t> header;
+    // the open family (passing reads, input order)
+    std::vector<Rec> fam;
+    bool started = false;     // any passing read seen
+    bool finished = false;    // EOF processed
+    bool errored = false;
+    // counters :1508
+    int64_t passed = 0, excluded = 0, processed = 0, filtered = 0, records = 0;
+    PyRandom rng;
+    // pack jobs of the current batch
+    std::vector<Job> jobs;
+    std::vector<int> idx_tmp;
+
+    // -- BGZF ----------------------------------------------------------------
+    // Inflate the next run of whole BGZF blocks, appending to the window
+    // after moving [keep, wend) to its front.  Returns false on error.
+    bool refill(size_t keep) {
+        const size_t left = wend - keep;
+        if (keep > 0) {
+            std::memmove(win.data(), win.data() + keep, left);
+            for (auto &r : fam) r.off -= keep;
+            wpos -= keep;
+            wend = left;
+        }
+        const size_t want = (size_t)32 << 20;
+        if (win.size() < wend + want + 0x10000) win.resize(wend + want + 0x10000);
+        struct Blk { size_t coff, clen, doff; uint32_t isize, crc; };
+        std::vector<Blk> blks;
+        size_t total = 0;
+        for (;;) {
+            while (cend - cbeg >= 18 && total + 0x10000 <= want) {
+                const uint8_t *h = cbuf.data() + cbeg;
+                if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) {
+                    g_err = "not a BGZF file";
+                    return false;
+                }
+                const size_t xlen = rd16(h + 10);
+                if (cend - cbeg < 12 + xlen) break;
+                long bsize = -1;
+                for (size_t i = 0; i + 4 <= xlen;) {
+                    const uint8_t *s = h + 12 + i;
+                    const size_t slen = rd16(s + 2);
+                    if (s[0] == 66 && s[1] == 67 && slen == 2) bsize = rd16(s + 4);
+                    i += 4 + slen;
+                }
+                if (bsize < 0) { g_err = "BGZF block without BC field"; return false; }
+                const size_t blen = (size_t)bsize + 1;
+                if (blen < 12 + xlen + 8) { g_err = "BGZF block size too small"; return false; }
+                if (cend - cbeg < blen) break;
+                Blk b;
+                b.coff = cbeg + 12 + xlen;
+                b.clen = blen - 12 - xlen - 8;
+                b.crc = rd32(h + blen - 8);
+                b.isize = rd32(h + blen - 4);
+                if (b.isize > 0x10000) { g_err = "BGZF ISIZE above 64 KiB"; return false; }
+                b.doff = wend + total;
+                total += b.isize;
+                blks.push_back(b);
+                cbeg += blen;
+            }
+            if (total + 0x10000 > want) break;          // enough for this window
+            if (file_eof) {
+                if (cend > cbeg) { g_err = "truncated BGZF block at the end of the file"; return false; }
+                break;
+            }
+            // more compressed bytes
+            std::memmove(cbuf.data(), cbuf.data() + cbeg, cend - cbeg);
+            cend -= cbeg;
+            cbeg = 0;
+            const size_t got = std::fread(cbuf.data() + cend, 1, cbuf.size() - cend, f);
+            cend += got;
+            if (got == 0) file_eof = true;
+        }
+        const std::vector<Blk> *bp = &blks;
+        const bool ok = pool->run(blks.size(), [&](size_t i) {
+            const Blk &b = (*bp)[i];
+            if (b.isize == 0) return b.clen <= 2;      // empty block (the EOF marker)
+            size_t got = 0;
+            if (libdeflate_deflate_decompress(tl_dec.get(), cbuf.data() + b.coff, b.clen, win.data() + b.doff,
+                                              b.isize, &got) != 0 || got != b.isize)
+                return false;
+            return libdeflate_crc32(0, win.data() + b.doff, b.isize) == b.crc;
+        });
+        if (!ok) { g_err = "BGZF block failed to inflate or CRC mismatch"; return false; }
+        wend += total;
+        if (blks.empty() && file_eof && cend == cbeg) data_eof = true;
+        return true;
+    }
+
+    // make at least n bytes available at wpos (keeping the open family);
+    // 1: ok, 0: clean end of data with fewer bytes, -1: error
+    int need(size_t n) {
+        while (wend - wpos < n) {
+            if (data_eof) return 0;
+            flush_jobs();
+            const size_t keep = fam.empty() ? wpos : std::min(wpos, fam.front().off);
+            if (!refill(keep)) return -1;
+        }
+        return 1;
+    }
+
+    // -- pack jobs -------------------------------------------------------------
+    dcr_host_batch *hb = nullptr;
+    void flush_jobs() {
+        if (jobs.empty()) return;
+        const size_t chunk = 2048;
+        const size_t nchunks = (jobs.size() + chunk - 1) / chunk;
+        const uint8_t *w = win.data();
+        dcr_host_batch *b = hb;
+        pool->run(nchunks, [&](size_t c) {
+            const size_t j1 = std::min(jobs.size(), (c + 1) * chunk);
+            for (size_t j = c * chunk; j < j1; ++j) {
+                const Job &jb = jobs[j];
+                const uint8_t *r = w + jb.rec + 4;
+                const uint32_t l_rn = r[8];
+                const uint32_t n_cig = rd16(r + 12);
+                const int32_t l_seq = rdi32(r + 16);
+                const uint8_t *cig = r + 32 + l_rn;
+                std::memcpy(b->cigar + jb.dst_cig, cig, 4u * n_cig);
+                const uint8_t *s = cig + 4u * n_cig;
+                uint8_t *d = b->bases + jb.dst_base;
+                const int32_t half = l_seq >> 1;
+                for (int32_t i = 0; i < half; ++i) std::memcpy(d + 2 * i, &kSeq.pair[s[i]], 2);
+                if (l_seq & 1) d[l_seq - 1] = (uint8_t)(kSeq.pair[s[half]] & 0xff);
+                std::memcpy(b->quals + jb.dst_base, s + ((l_seq + 1) >> 1), (size_t)l_seq);
+            }
+            return true;
+        });
+        jobs.clear();
+    }
+
+    // -- record parse ------------------------------------------------------------
+    // 1 ok, 0 end of data, -1 error (g_err)
+    int parse(Rec &rc) {
+        int st = need(4);
+        if (st <= 0) {
+            if (st == 0 && wend > wpos) { g_err = "truncated BAM record at the end of the file"; return -1; }
+            return st;
+        }
+        const int32_t bs = rdi32(win.data() + wpos);
+        if (bs < 32) { g_err = "malformed BAM record (block_size < 32)"; return -1; }
+        st = need(4 + (size_t)bs);
+        if (st <= 0) {
+            if (st == 0) g_err = "truncated BAM record at the end of the file";
+            return -1;
+        }
+        const uint8_t *base = win.data() + wpos;
+        const uint8_t *r = base + 4;
+        rc.off = wpos;
+        rc.len = 4u + (uint32_t)bs;
+        rc.tid = rdi32(r);
+        rc.pos = rdi32(r + 4);
+        const uint32_t l_rn = r[8];
+        rc.mapq = r[9];
+        rc.n_cig = rd16(r + 12);
+        rc.flag = rd16(r + 14);
+        rc.l_seq = rdi32(r + 16);
+        if (rc.l_seq < 0) { g_err = "malformed BAM record (l_seq < 0)"; return -1; }
+        rc.o_cig = 4 + 32 + l_rn;
+        rc.o_seq = rc.o_cig + 4u * rc.n_cig;
+        rc.o_qual = rc.o_seq + (uint32_t)((rc.l_seq + 1) >> 1);
+        size_t p = rc.o_qual + (size_t)rc.l_seq;
+        if (p > rc.len) { g_err = "malformed BAM record (fields past block_size)"; return -1; }
+        rc.o_mi = rc.o_rx = 0;
+        rc.l_mi = rc.l_rx = 0;
+        rc.mi_type = rc.rx_type = 0;
+        // aux fields
+        while (p + 3 <= rc.len) {
+            const uint8_t t0 = base[p], t1 = base[p + 1], ty = base[p + 2];
+            size_t v = p + 3, e;
+            switch (ty) {
+                case 'A': case 'c': case 'C': e = v + 1; break;
+                case 's': case 'S': e = v + 2; break;
+                case 'i': case 'I': case 'f': e = v + 4; break;
+                case 'd': e = v + 8; break;
+                case 'Z': case 'H': {
+                    const void *z = std::memchr(base + v, 0, rc.len - v);
+                    if (!z) { g_err = "malformed BAM aux field (unterminated string)"; return -1; }
+                    e = (size_t)((const uint8_t *)z - base) + 1;
+                    break;
+                }
+                case 'B': {
+                    if (v + 5 > rc.len) { g_err = "malformed BAM aux array"; return -1; }
+                    const uint8_t sub = base[v];
+                    const uint32_t n = rd32(base + v + 1);
+                    size_t es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
+                    e = v + 5 + es * (size_t)n;
+                    break;
+                }
+                default: g_err = "malformed BAM aux field type"; return -1;
+            }
+            if (e > rc.len) { g_err = "malformed BAM aux field (past block_size)"; return -1; }
+            // the first occurrence, as pysam's get_tag (bam_aux_get)
+            if (t0 == 'M' && t1 == 'I' && !rc.mi_type) {
+                rc.mi_type = ty;
+                rc.o_mi = (uint32_t)v;
+                rc.l_mi = (uint16_t)(ty == 'Z' ? e - v - 1 : 0);
+            } else if (t0 == 'R' && t1 == 'X' && !rc.rx_type) {
+                rc.rx_type = ty;
+                rc.o_rx = (uint32_t)v;
+                rc.l_rx = (uint16_t)(ty == 'Z' ? e - v - 1 : 0);
+            }
+            p = e;
+        }
+        rc.l_code = rc.l_mi;
+        if (rc.mi_type == 'Z') {
+            const void *sl = std::memchr(base + rc.o_mi, '/', rc.l_mi);
+            if (sl) rc.l_code = (uint16_t)((const uint8_t *)sl - (base + rc.o_mi));
+        }
+        return 1;
+    }
+
+    const uint8_t *at(const Rec &r, uint32_t o) const { return win.data() + r.off + o; }
+
+    // pass_filters (:1135-1181): 1 pass, 0 excluded, -1 the reference stops (err set)
+    int filters(const Rec &r, int &err_kind, std::string &msg) const {
+        if (!r.mi_type) { err_kind = DCR_ERR_EXIT; msg = "ERROR: family code tag (MI) not found in file"; return -1; }
+        if (!r.rx_type) { err_kind = DCR_ERR_EXIT; msg = "ERROR: family code tag (RX) not found in file"; return -1; }
+        if (r.n_cig == 0) { err_kind = DCR_ERR_TYPE; msg = "argument of type 'NoneType' is not iterable"; return -1; }
+        const uint8_t *c = at(r, r.o_cig);
+        for (uint32_t i = 0; i < r.n_cig; ++i) {
+            const uint32_t op = rd32(c + 4 * i) & 15;
+            if (op == 3 || op == 6 || op >= 9) {
+                err_kind = DCR_ERR_EXIT;
+                msg = "ERROR: unexpected symbols (P, N, B, *) were found in CIGAR strings.";
+                return -1;
+            }
+        }
+        for (uint32_t i = 1; i + 1 < r.n_cig; ++i)
+            if ((rd32(c + 4 * i) & 15) == 4) {
+                err_kind = DCR_ERR_EXIT;
+                msg = "ERROR: softclips (S) found in the middle of the read.";
+                return -1;
+            }
+        const uint16_t fl = r.flag;
+        return (fl & 1) && (fl & 2) && !(fl & 4) && !(fl & 8) && !(fl & 2048) && !(fl & 512) &&
+               (int)r.mapq >= cfg.min_map_quality;
+    }
+
+    bool same_code(const Rec &a, const Rec &b) const {
+        return a.l_code == b.l_code && std::memcmp(at(a, a.o_mi), at(b, b.o_mi), a.l_code) == 0;
+    }
+
+    // -- the family -------------------------------------------------------------
+    // end soft clips of a read (batch.py _end_soft_clips; remove_clipping :214-226)
+    int32_t clip_total(const Rec &r) const {
+        const uint8_t *c = at(r, r.o_cig);
+        const int n = r.n_cig;
+        if (n == 0) return 0;
+        auto op = [&](int i) { return (int)(rd32(c + 4 * i) & 15); };
+        auto ln = [&](int i) { return (int32_t)(rd32(c + 4 * i) >> 4); };
+        const int first = 0, last = n - 1;
+        int32_t c5 = 0;
+        if (op(first) == 4) c5 = ln(first);
+        else if (op(first) == 5 && n > 1 && op(first + 1) == 4) c5 = ln(first + 1);
+        const int i5 = op(first) == 4 ? first : first + 1;
+        int c3i = -1;
+        if (op(last) == 4) c3i = last;
+        else if (op(last) == 5 && n > 1) c3i = last - 1;
+        int32_t c3 = 0;
+        if (c3i >= first && op(c3i) == 4 && !(c5 > 0 && c3i == i5)) c3 = ln(c3i);
+        return c5 + c3;
+    }
+
+    // does the read's CIGAR, after remove_clipping and trim_3prime_N, still
+    // hold a '=' / 'X' op (change_match_mismatch_operations prints, :374-375)?
+    bool eqx_after_trim(const Rec &r) const {
+        const uint8_t *c = at(r, r.o_cig);
+        bool any = false;
+        for (uint32_t i = 0; i < r.n_cig; ++i) {
+            const uint32_t op = rd32(c + 4 * i) & 15;
+            any |= (op == 7 || op == 8);
+        }
+        if (!any || r.l_seq == 0) return false;
+        // remove_clipping: S bases leave the sequence (:214-251)
+        int32_t s5 = 0, s3 = 0;
+        bool inseq = false, modified = false;
+        int64_t expanded = 0;
+        for (uint32_t i = 0; i < r.n_cig; ++i) {
+            const uint32_t w = rd32(c + 4 * i), op = w & 15, ln = w >> 4;
+            if (op == 5) modified = true;
+            else if (op == 4) {
+                modified = true;
+                if (!inseq) s5 = (int32_t)ln; else s3 = (int32_t)ln;
+            } else {
+                inseq = true;
+                expanded += ln;
+            }
+        }
+        (void)modified;
+        int32_t b = s5, e = r.l_seq - s3;       // seq[s5 : -s3] (s3 > 0) or seq[s5:]
+        if (s3 == 0) e = r.l_seq;
+        if (e < b) e = b;
+        // mask (:279-283) then count the trailing 'N' (:306-312)
+        const uint8_t *sq = at(r, r.o_seq), *ql = at(r, r.o_qual);
+        int32_t tn = 0;
+        for (int32_t i = e - 1; i >= b; --i) {
+            const int code = (sq[i >> 1] >> ((i & 1) ? 0 : 4)) & 15;
+            if (code == 15 || (int)ql[i] < cfg.min_base_quality) ++tn;
+            else break;
+        }
+        // original_cigar[:len - tn] with Python slice semantics (:320-322)
+        int64_t keep = expanded - tn;
+        if (keep < 0) keep = std::max<int64_t>(0, expanded + keep);
+        int64_t pos = 0;
+        for (uint32_t i = 0; i < r.n_cig && pos < keep; ++i) {
+            const uint32_t w = rd32(c + 4 * i), op = w & 15, ln = w >> 4;
+            if (op == 4 || op == 5) continue;
+            if (op == 7 || op == 8) return true;
+            pos += ln;
+        }
+        return false;
+    }
+
+    std::vector<Rec> sub[4];
+
+    // preprocess_family up to the read loop (:1248-1264), then pack or file
+    // the family.  Returns 1 done, 0 no room in this batch (nothing changed),
+    // -1 the reference stops at this family (batch error set).
+    int complete_family() {
+        dcr_host_batch *b = hb;
+        const Rec &r0 = fam.front();
+        const std::string code((const char *)at(r0, r0.o_mi), r0.l_code);
+        // capacity check first, with the unsampled family as the bound
+        int64_t nb = 0, nc = 0;
+        for (const Rec &r : fam) { nb += r.l_seq; nc += r.n_cig; }
+        const int64_t nfam_reads = (int64_t)fam.size();
+        const int64_t names_need = (int64_t)code.size() + 1 + 2 * (int64_t)(r0.l_rx + 1) + 64 * 2;
+        int64_t filt_bytes = 0;
+        for (const Rec &r : fam) filt_bytes += r.len;
+        const bool fits = b->n_tab < b->cap_tab && b->n_fam < b->cap_fam &&
+                          b->n_reads + nfam_reads <= b->cap_reads && b->n_bases + nb <= b->cap_bases &&
+                          b->n_cigar + nc <= b->cap_cigar && b->n_names + names_need <= b->cap_names &&
+                          b->n_side_filt + filt_bytes <= b->cap_side;
+        if (!fits) {
+            if (b->n_tab == 0 && b->n_side_exc == 0)
+                return fail_capacity("one family exceeds the batch capacities");
+            return 0;
+        }
+        // check_family_UMIs (:100-113)
+        if (r0.rx_type != 'Z') return stop(DCR_ERR_ATTRIBUTE, "'int' object has no attribute 'split'");
+        const char *rx0 = (const char *)at(r0, r0.o_rx);
+        const std::string umi1(rx0, r0.l_rx);
+        const size_t d1 = umi1.find('-');
+        if (d1 == std::string::npos) return stop(DCR_ERR_INDEX, "list index out of range");
+        const size_t d2 = umi1.find('-', d1 + 1);
+        const std::string umi2 = umi1.substr(d1 + 1, d2 == std::string::npos ? std::string::npos : d2 - d1 - 1) +
+                                 "-" + umi1.substr(0, d1);
+        for (const Rec &r : fam) {
+            if (r.rx_type != 'Z') return stop(DCR_ERR_ATTRIBUTE, "RX tag is not a string");
+            const char *x = (const char *)at(r, r.o_rx);
+            const bool eq1 = r.l_rx == umi1.size() && std::memcmp(x, umi1.data(), r.l_rx) == 0;
+            const bool eq2 = r.l_rx == umi2.size() && std::memcmp(x, umi2.data(), r.l_rx) == 0;
+            if (!eq1 && !eq2)
+                return stop(DCR_ERR_EXIT, "ERROR: family " + code +
+                                              " has different UMI tags. \n Please check output file of previous "
+                                              "step of the pipeline (fgbio GroupReadsByUmi)");
+        }
+        // check_family_rnames (:116-128)
+        for (size_t i = 1; i < fam.size(); ++i)
+            if (fam[i].tid != r0.tid)
+                return stop(DCR_ERR_EXIT, "ERROR: family " + code +
+                                              " has difference rnames (e.g. chromosome numbers). \n Please check "
+                                              "output file of previous step of the pipeline (fgbio "
+                                              "GroupReadsByUmi)");
+        // split_family (:132-154)
+        for (auto &s : sub) s.clear();
+        for (const Rec &r : fam) {
+            const bool rev = r.flag & 16, r1 = r.flag & 64, r2 = r.flag & 128;
+            if (!rev && r1) sub[0].push_back(r);
+            else if (!rev && r2) sub[1].push_back(r);
+            else if (rev && r1) sub[2].push_back(r);
+            else if (rev && r2) sub[3].push_back(r);
+        }
+        // check_number_reads (:157-188)
+        int sampled = 0;
+        bool enough = true;
+        for (int k = 0; k < 4; ++k) {
+            const int n = (int)sub[k].size();
+            if (n < cfg.min_reads) { enough = false; break; }
+            if (n > cfg.max_reads) {
+                if (cfg.max_reads < 0) return stop(DCR_ERR_VALUE, "Sample larger than population or is negative");
+                rng.sample(n, cfg.max_reads, idx_tmp);
+                std::vector<Rec> pick;
+                pick.reserve(idx_tmp.size());
+                for (int j : idx_tmp) pick.push_back(sub[k][(size_t)j]);
+                sub[k].swap(pick);
+                sampled |= 1 << k;
+            }
+        }
+        const int32_t t = b->n_tab++;
+        b->tab_sampled[t] = sampled;
+        b->tab_exc_cut[t] = b->n_side_exc;
+        b->tab_filt_cut[t] = b->n_side_filt;
+        b->tab_code[t] = put_name(code.data(), code.size());
+        if (!enough) {
+            // filtered family: its reads to _filteredfamilies.bam in input order (:1550-1551)
+            b->tab_kind[t] = DCR_FAM_FILTERED;
+            b->tab_proc[t] = -1;
+            for (const Rec &r : fam) {
+                std::memcpy(b->side_filt + b->n_side_filt, at(r, 0), r.len);
+                b->n_side_filt += r.len;
+            }
+            ++filtered;
+            return 1;
+        }
+        // pack
+        const int32_t f = b->n_fam++;
+        b->tab_kind[t] = DCR_FAM_PROCESSED;
+        b->tab_proc[t] = f;
+        b->fam_tid[f] = r0.tid;
+        int64_t mn[4], mx[4];
+        for (int k = 0; k < 4; ++k) {
+            int16_t eqx = 0;
+            mn[k] = mx[k] = 0;
+            bool first = true;
+            for (const Rec &r : sub[k]) {
+                const int32_t i = b->n_reads++;
+                b->read_pos[i] = r.pos;
+                b->read_mapq[i] = r.mapq;
+                b->seq_len[i] = r.l_seq;
+                b->seq_off[i] = b->n_bases;
+                b->cig_off[i] = (int32_t)b->n_cigar;
+                b->cig_n[i] = r.n_cig;
+                jobs.push_back(Job{r.off, b->n_bases, b->n_cigar});
+                b->n_bases += r.l_seq;
+                b->n_cigar += r.n_cig;
+                const int64_t end = (int64_t)r.pos + r.l_seq - clip_total(r);
+                if (first || r.pos < mn[k]) mn[k] = r.pos;
+                if (first || end > mx[k]) mx[k] = end;
+                first = false;
+                if (eqx < 0x7fff && eqx_after_trim(r)) ++eqx;
+            }
+            b->fam_eqx[4 * f + k] = (uint16_t)eqx;
+            b->sub_off[4 * f + k + 1] = b->n_reads;
+            const int64_t tt = (std::max<int64_t>(mx[k] - mn[k], 1) + 15) & ~(int64_t)15;
+            b->ss_col_off[4 * f + k + 1] = b->ss_col_off[4 * f + k] + tt;
+        }
+        for (int j = 0; j < 2; ++j) {
+            const int a = 2 * j, c = 2 * j + 1;
+            int64_t tt = std::max(mx[a], mx[c]) - std::min(mn[a], mn[c]);
+            tt = (std::max<int64_t>(tt, 1) + 15) & ~(int64_t)15;
+            b->ds_col_off[2 * f + j + 1] = b->ds_col_off[2 * f + j] + tt;
+        }
+        b->ss_cols = b->ss_col_off[4 * f + 4];
+        b->ds_cols = b->ds_col_off[2 * f + 2];
+        // writer metadata: RX of the read0 of A1 and of B1 (:1367 via add_tags)
+        for (int j = 0; j < 2; ++j) {
+            const std::vector<Rec> &s = sub[2 * j];
+            if (s.empty()) b->fam_rx[2 * f + j] = put_name("", 0);
+            else b->fam_rx[2 * f + j] = put_name((const char *)at(s[0], s[0].o_rx), s[0].l_rx);
+        }
+        ++processed;
+        return 1;
+    }
+
+    int64_t put_name(const char *s, size_t n) {
+        const int64_t o = hb->n_names;
+        std::memcpy(hb->names + o, s, n);
+        hb->names[o + (int64_t)n] = 0;
+        hb->n_names += (int64_t)n + 1;
+        return o;
+    }
+
+    int stop(int kind, const std::string &msg) {
+        hb->end_kind = DCR_END_ERROR;
+        hb->err_kind = kind;
+        std::snprintf(hb->err_msg, sizeof hb->err_msg, "%s", msg.c_str());
+        errored = true;
+        return -1;
+    }
+    int cap_err = 0;
+    int fail_capacity(const std::string &m) {
+        g_err = m;
+        cap_err = 1;
+        return -1;
+    }
+
+    // -- one batch ----------------------------------------------------------------
+    int next(dcr_host_batch *b) {
+        hb = b;
+        b->n_fam = b->n_reads = 0;
+        b->n_cigar = b->n_bases = b->ss_cols = b->ds_cols = 0;
+        b->n_tab = 0;
+        b->end_kind = DCR_END_FULL;
+        b->n_names = b->n_side_exc = b->n_side_filt = 0;
+        b->err_kind = DCR_ERR_NONE;
+        b->err_msg[0] = 0;
+        b->sub_off[0] = 0;
+        b->ss_col_off[0] = 0;
+        b->ds_col_off[0] = 0;
+        cap_err = 0;
+        if (errored || finished) {
+            b->end_kind = errored ? DCR_END_ERROR : DCR_END_EOF;
+            return fail(DCR_IO_EARG, "the input has already ended");
+        }
+        int rc = walk();
+        flush_jobs();
+        hb = nullptr;
+        if (rc < 0) {
+            if (cap_err) return DCR_IO_ECAPACITY;
+            if (!errored) return DCR_IO_EFORMAT;
+        }
+        return DCR_IO_OK;
+    }
+
+    int walk() {
+        dcr_host_batch *b = hb;
+        for (;;) {
+            Rec r;
+            const int st = parse(r);
+            if (st < 0) return -1;
+            if (st == 0) {
+                // end of input: the last family (:1610-1631)
+                if (!started) return stop(DCR_ERR_TYPE, "'NoneType' object is not subscriptable");
+                if (!fam.empty()) {
+                    const int c = complete_family();
+                    if (c <= 0) return c;
+                    fam.clear();
+                }
+                finished = true;
+                b->end_kind = DCR_END_EOF;
+                return 1;
+            }
+            int ek = 0;
+            std::string msg;
+            const int pf = filters(r, ek, msg);
+            if (pf < 0) return stop(ek, msg);
+            if (pf == 0) {
+                // excluded read -> _filteredreads.bam (:1523-1528)
+                if (b->n_side_exc + r.len > b->cap_side) {
+                    if (b->n_tab == 0 && b->n_side_exc == 0) return fail_capacity("a record exceeds cap_side");
+                    return 1;
+                }
+                std::memcpy(b->side_exc + b->n_side_exc, at(r, 0), r.len);
+                b->n_side_exc += r.len;
+                ++excluded;
+                ++records;
+                wpos += r.len;
+                continue;
+            }
+            if (r.mi_type != 'Z') return stop(DCR_ERR_ATTRIBUTE, "'int' object has no attribute 'split'");
+            if (!fam.empty() && !same_code(r, fam.front())) {
+                const int c = complete_family();
+                if (c <= 0) return c;      // 0: batch full, the read stays unconsumed
+                fam.clear();
+            }
+            ++passed;
+            ++records;
+            started = true;
+            fam.push_back(r);
+            wpos += r.len;
+        }
+    }
+};
+
+extern "C" {
+
+int dcr_io_abi_version(void) { return DCR_IO_ABI_VERSION; }
+const char *dcr_io_last_error(void) { return g_err.c_str(); }
+
+dcr_ingest *dcr_ingest_open(const char *path, const dcr_ingest_cfg *cfg) {
+    if (!path || !cfg) { g_err = "NULL argument"; return nullptr; }
+    FILE *f = std::fopen(path, "rb");
+    if (!f) { g_err = std::string("cannot open ") + path; return nullptr; }
+    std::unique_ptr<dcr_ingest> ing(new dcr_ingest);
+    ing->f = f;
+    ing->cfg = *cfg;
+    ing->pool.reset(new Pool(pick_threads(cfg->n_threads)));
+    ing->cbuf.resize((size_t)48 << 20);
+    // seed like an unseeded random.Random is not reproducible; callers pass
+    // their state with dcr_ingest_set_rng.  Default: random.seed(0).
+    for (int i = 0; i < 624; ++i) ing->rng.mt[i] = 0;
+    ing->rng.index = 624;
+    // header: magic, l_text, text, n_ref, refs
+    int st = ing->need(12);
+    if (st <= 0) { std::fclose(f); ing->f = nullptr; if (st == 0) g_err = "empty BAM"; return nullptr; }
+    const uint8_t *h = ing->win.data() + ing->wpos;
+    if (std::memcmp(h, "BAM\1", 4) != 0) { g_err = "not a BAM file"; std::fclose(f); ing->f = nullptr; return nullptr; }
+    const int32_t l_text = rdi32(h + 4);
+    if (l_text < 0 || ing->need(12 + (size_t)l_text) <= 0) { g_err = "truncated BAM header"; std::fclose(f); ing->f = nullptr; return nullptr; }
+    size_t p = 8 + (size_t)l_text;
+    const int32_t n_ref = rdi32(ing->win.data() + ing->wpos + p);
+    p += 4;
+    for (int32_t i = 0; i < n_ref; ++i) {
+        if (ing->need(p + 4) <= 0) { g_err = "truncated BAM header"; std::fclose(f); ing->f = nullptr; return nullptr; }
+        const int32_t ln = rdi32(ing->win.data() + ing->wpos + p);
+        if (ln < 0 || ing->need(p + 8 + (size_t)ln) <= 0) { g_err = "truncated BAM header"; std::fclose(f); ing->f = nullptr; return nullptr; }
+        p += 8 + (size_t)ln;
+    }
+    ing->header.assign(ing->win.data() + ing->wpos, ing->win.data() + ing->wpos + p);
+    ing->wpos += p;
+    return ing.release();
+}
+
+void dcr_ingest_close(dcr_ingest *ing) {
+    if (!ing) return;
+    if (ing->f) std::fclose(ing->f);
+    delete ing;
+}
+
+int64_t dcr_ingest_header(dcr_ingest *ing, const uint8_t **bytes) {
+    if (!ing || !bytes) return -1;
+    *bytes = ing->header.data();
+    return (int64_t)ing->header.size();
+}
+
+int dcr_ingest_set_rng(dcr_ingest *ing, const uint32_t *mt, int32_t index) {
+    if (!ing || !mt || index < 0 || index > 624) return fail(DCR_IO_EARG, "bad RNG state");
+    std::memcpy(ing->rng.mt, mt, sizeof ing->rng.mt);
+    ing->rng.index = index;
+    return DCR_IO_OK;
+}
+
+int dcr_ingest_get_rng(dcr_ingest *ing, uint32_t *mt, int32_t *index) {
+    if (!ing || !mt || !index) return fail(DCR_IO_EARG, "NULL argument");
+    std::memcpy(mt, ing->rng.mt, sizeof ing->rng.mt);
+    *index = ing->rng.index;
+    return DCR_IO_OK;
+}
+
+int dcr_ingest_next(dcr_ingest *ing, dcr_host_batch *hb) {
+    if (!ing || !hb) return fail(DCR_IO_EARG, "NULL argument");
+    if (hb->cap_fam < 1 || hb->cap_tab < 1 || hb->cap_reads < 1 || !hb->sub_off || !hb->names)
+        return fail(DCR_IO_EARG, "batch capacities not set");
+    return ing->next(hb);
+}
+
+int dcr_ingest_counters(dcr_ingest *ing, int64_t *out) {
+    if (!ing || !out) return fail(DCR_IO_EARG, "NULL argument");
+    out[0] = ing->passed;
+    out[1] = ing->excluded;
+    out[2] = ing->processed;
+    out[3] = ing->filtered;
+    out[4] = ing->records;
+    return DCR_IO_OK;
+}
+
+int dcr_py_sample(uint32_t *mt, int32_t *index, int32_t n, int32_t k, int32_t *out) {
+    if (!mt || !index || !out || n < 0 || k < 0 || k > n) return fail(DCR_IO_EARG, "bad sample arguments");
+    PyRandom r;
+    std::memcpy(r.mt, mt, sizeof r.mt);
+    r.index = *index;
+    std::vector<int> v;
+    r.sample(n, k, v);
+    for (int i = 0; i < k; ++i) out[i] = v[(size_t)i];
+    std::memcpy(mt, r.mt, sizeof r.mt);
+    *index = r.index;
+    return DCR_IO_OK;
+}
+
+}  // extern "C"

@@ -167,6 +167,22 @@ int dcr_last_timing(dcr_ctx *ctx, float *ms4);
 #define DCR_N_KERNEL_TIMES 9
 int dcr_last_kernel_timing(dcr_ctx *ctx, float *ms9);
 
+/* Streaming: a context has DCR_MAX_SLOTS slots of device buffers.
+ * dcr_submit copies a host batch (pinned memory, dcr_host_alloc) into the
+ * slot on a copy stream, runs it on the compute stream and copies the
+ * outputs back into the host dcr_out arrays on a second copy stream (NULL
+ * fields are not copied); it returns at once.  read_status (optional,
+ * n_reads int32) receives dcr_read_info.status of every read.  dcr_wait
+ * blocks until the slot's outputs are on the host.  Batches run on the
+ * device in submission order; H2D of one batch and D2H of another overlap
+ * the kernels of a third. */
+#define DCR_MAX_SLOTS 4
+void *dcr_host_alloc(size_t bytes);
+void dcr_host_free(void *p);
+int dcr_submit(dcr_ctx *ctx, int slot, const dcr_batch *host_in, dcr_out *host_ss, dcr_out *host_ds,
+               int32_t *read_status);
+int dcr_wait(dcr_ctx *ctx, int slot);
+
 /* CPU restatement with the same contract (oracle/, test infrastructure):
    host pointers, single thread (or n_threads > 1) */
 int dcr_oracle_run(const dcr_params *params, const dcr_batch *in, dcr_out *ss, dcr_out *ds,

@@ -1,0 +1,79 @@
+"""End-to-end cases of the CLI drop-in against the reference's own ``main()``
+run on the same inputs (tests/golden/e2e_cases.json.gz, made by
+tests/golden/make_golden_e2e_cases.py): a failing family in the middle of
+the input with filtered families and excluded reads after it (the side
+files hold exactly what the reference wrote before it stopped), the
+invalid-letter exit and its printed column, the UMI-mismatch exit, '=' / 'X'
+CIGAR lines, every verbose print, downsampling through main(), and an input
+where no read passes.
+
+The CPU cases run the batch backend on the C oracle (test infrastructure);
+the GPU case runs the HIP library.  Small batches (``--batch_reads``) put
+the failing family in a later batch than the first one."""
+import contextlib
+import gzip
+import io
+import json
+import os
+import random
+
+import pytest
+
+from duplexumiconsensusreads_amd import bam, cli
+from oracle import dcr_oracle_c
+from tests.golden_io import GOLDEN
+
+with gzip.open(os.path.join(GOLDEN, "e2e_cases.json.gz"), "rt") as _f:
+    CASES = json.load(_f)
+
+
+def run_case(tmp_path, name, backend, batch_reads):
+    case = CASES[name]
+    out = str(tmp_path / "cons.bam")
+    buf = io.StringIO()
+    exc = None
+    argv = ["-i", os.path.join(GOLDEN, f"e2e_case_{name}.bam"), "-o", out, *case["args"],
+            "--batch_reads", str(batch_reads)]
+    try:
+        with contextlib.redirect_stdout(buf):
+            cli.main(argv, backend=backend, rng=random.Random(case["random_seed"]))
+    except SystemExit as e:
+        exc = f"SystemExit({e.code})"
+    except Exception as e:  # noqa: BLE001 - compared with the reference's outcome
+        exc = type(e).__name__
+    stdout = buf.getvalue()
+    # the input path is part of the verbose first line
+    stdout = stdout.replace(os.path.join(GOLDEN, f"e2e_case_{name}.bam"),
+                            f"/root/repo/tests/golden/e2e_case_{name}.bam")
+    res = {"stdout": stdout, "exception": exc}
+    for key, path in (("consensus", out), ("filteredreads", out[:-4] + "_filteredreads.bam"),
+                      ("filteredfamilies", out[:-4] + "_filteredfamilies.bam")):
+        with bam.AlignmentFile(path, "rb") as f:
+            res[key] = [r.to_dict() for r in f]
+    return res
+
+
+def assert_case(res, name):
+    want = CASES[name]
+    assert res["exception"] == want["exception"]
+    assert res["stdout"] == want["stdout"]
+    for key in ("consensus", "filteredreads", "filteredfamilies"):
+        got, exp = res[key], want[key]
+        assert len(got) == len(exp), (key, len(got), len(exp))
+        for i, (g, w) in enumerate(zip(got, exp)):
+            assert g == w, (key, i, {k: (g.get(k), w.get(k)) for k in w if g.get(k) != w.get(k)})
+
+
+@pytest.mark.parametrize("batch_reads", [1 << 20, 200])
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_cli_case_matches_reference_main(tmp_path, name, batch_reads):
+    assert_case(run_case(tmp_path, name, dcr_oracle_c.run, batch_reads), name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_cli_case_matches_reference_main_gpu(tmp_path, name):
+    from duplexumiconsensusreads_amd.params import ConsensusParams
+    args = cli.parse_args(["-i", "x.bam", *CASES[name]["args"]])
+    be = cli.default_backend(ConsensusParams.from_args(args))
+    assert_case(run_case(tmp_path, name, be, 300), name)

@@ -44,10 +44,10 @@ def assert_matches_reference(res):
             assert g == w, (key, i, {k: (g.get(k), w.get(k)) for k in w if g.get(k) != w.get(k)})
 
 
-@pytest.mark.parametrize("batch", ["65536", "7"])
+@pytest.mark.parametrize("batch", ["1048576", "100"])
 def test_cli_matches_reference_main_oracle_backend(tmp_path, batch):
-    # batch size must not change any output (7: several device calls per file)
-    res = run_cli(tmp_path, dcr_oracle_c.run, ("--batch_families", batch))
+    # batch size must not change any output (100 reads: many batches per file)
+    res = run_cli(tmp_path, dcr_oracle_c.run, ("--batch_reads", batch))
     assert_matches_reference(res)
 
 
@@ -65,29 +65,31 @@ def test_cli_rejects_non_bam_output(tmp_path, capsys):
 
 
 @pytest.mark.gpu
-def test_cli_matches_reference_main_gpu(tmp_path):
-    from duplexumiconsensusreads_amd import _lib
+@pytest.mark.parametrize("batch", ["1048576", "300"])
+def test_cli_matches_reference_main_gpu(tmp_path, batch):
     from duplexumiconsensusreads_amd.params import ConsensusParams
-    ctx = _lib.Context(ConsensusParams(), device=0)
-    try:
-        res = run_cli(tmp_path, _lib.backend(ctx))
-    finally:
-        ctx.close()
+    be = cli.default_backend(ConsensusParams())     # pinned batches, asynchronous submits
+    res = run_cli(tmp_path, be, ("--batch_reads", batch))
     assert_matches_reference(res)
 
 
-def test_cli_output_files_identical_with_either_bgzf_codec(tmp_path, monkeypatch):
-    # the native BGZF codec (libdcr_bgzf.so) and the Python one write the same bytes
-    if bam.native_bgzf() is None:
-        pytest.skip("libdcr_bgzf.so not built")
-    files = {}
-    for codec in ("native", "python"):
-        if codec == "python":
-            monkeypatch.setenv("DCR_BGZF", "python")
-            monkeypatch.setattr(bam, "_native_lib", None)
-        d = tmp_path / codec
-        d.mkdir()
-        run_cli(d, dcr_oracle_c.run)
-        files[codec] = {p.name: p.read_bytes() for p in sorted(d.iterdir())}
-    assert len(files["native"]) == 3
-    assert files["native"] == files["python"]
+@pytest.mark.parametrize("level,threads", [("1", "1"), ("9", "4")])
+def test_cli_records_do_not_depend_on_codec_settings(tmp_path, level, threads):
+    # compression level and thread count change bytes on disk, never records
+    res = run_cli(tmp_path, dcr_oracle_c.run, ("--compression_level", level, "--threads", threads))
+    assert_matches_reference(res)
+
+
+def test_cli_consensus_stream_identical_to_python_record_writer(tmp_path):
+    """The native record formatter (csrc/dcr_format.cpp) writes the same
+    uncompressed BAM stream as the Python record path (writer.py through
+    bam.encode_record) for the same records."""
+    from duplexumiconsensusreads_amd.bam import bgzf_stream
+    res = run_cli(tmp_path, dcr_oracle_c.run)
+    native = bgzf_stream(str(tmp_path / "cons.bam"))
+    with bam.AlignmentFile(str(tmp_path / "cons.bam"), "rb") as f:
+        recs = list(f)
+        hdr = f.header.encode()
+    python = hdr + b"".join(bam.encode_record(r) for r in recs)
+    assert len(recs) == len(res["consensus"])
+    assert native == python

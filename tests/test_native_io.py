@@ -1,0 +1,177 @@
+"""The native host side (libdcr_io.so, include/dcr_io.h) on CPU:
+
+* the library exports every function the header declares and the ctypes
+  mirror of ``dcr_host_batch`` has the header's layout;
+* CPython's ``random.sample`` restated natively (MT19937 state in / out),
+  both of its branches (pool and set), against the interpreter;
+* the ingest (filters, MI grouping, family checks, split, downsampling,
+  packing, side records) against the host's Python restatement of the same
+  steps (cli.pass_filters / pipeline.prepare_family / batch.pack_families),
+  array for array and byte for byte, across batch sizes;
+* truncated and malformed input fail loudly.
+"""
+import ctypes
+import os
+import random
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from duplexumiconsensusreads_amd import bam, native_io, pipeline, synth
+from duplexumiconsensusreads_amd.batch import BATCH_FIELDS, pack_families
+from duplexumiconsensusreads_amd.params import ConsensusParams
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dcr_io.h")
+GOLDEN_BAM = os.path.join(ROOT, "tests", "golden", "e2e_c1_small.bam")
+
+
+def test_library_exports_every_header_function():
+    lib = native_io.load()
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    names = sorted(set(re.findall(r"^[A-Za-z_][\w\s\*]*?\b(dcr_\w+)\s*\(", txt, flags=re.M)))
+    assert "dcr_ingest_next" in names and "dcr_fmt_write" in names
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+def test_host_batch_layout_matches_header():
+    src = (f'#include "{HEADER}"\n#include <stdio.h>\n#include <stddef.h>\n'
+           'int main(void){printf("%zu %zu %zu %zu\\n", sizeof(dcr_host_batch), offsetof(dcr_host_batch, n_fam),'
+           ' offsetof(dcr_host_batch, err_msg), sizeof(dcr_ingest_cfg));return 0;}\n')
+    exe = "/tmp/_dcr_io_sizeof"
+    subprocess.run(["gcc", "-x", "c", "-", "-o", exe], input=src, text=True, check=True)
+    got = [int(x) for x in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()]
+    S = native_io.HostBatchStruct
+    assert got == [ctypes.sizeof(S), S.n_fam.offset, S.err_msg.offset, ctypes.sizeof(native_io.IngestCfg)]
+
+
+@pytest.mark.parametrize("n,k", [(5, 3), (30, 10), (150, 100), (1000, 100), (26, 6), (27, 6), (1000, 999),
+                                 (50, 1), (400, 60), (2, 1)])
+def test_native_sample_is_cpython_sample(n, k):
+    r = random.Random(n * 1000 + k)
+    for _ in range(5):
+        st = r.getstate()
+        got, st2 = native_io.py_sample(st, n, k)
+        assert got == r.sample(range(n), k)
+        assert st2 == r.getstate()
+
+
+def python_ingest(path, P, seed):
+    """The same steps through the Python host restatement (per record)."""
+    rng = random.Random(seed)
+    proc, exc, filt = [], [], []
+    fam, code = None, None
+
+    def done(f):
+        res = pipeline.prepare_family(f, P, rng)
+        if res.subs is None:
+            filt.extend(f)
+        else:
+            proc.append(res.subs)
+
+    with bam.AlignmentFile(path, "rb") as inb:
+        for r in inb:
+            if not legacy_pass_filters(r, P.min_map_quality):
+                exc.append(r)
+                continue
+            c = r.get_tag("MI").split("/")[0]
+            if fam is None:
+                fam, code = [r], c
+            elif c == code:
+                fam.append(r)
+            else:
+                done(fam)
+                fam, code = [r], c
+    done(fam)
+    return pack_families(proc), exc, filt, rng
+
+
+def legacy_pass_filters(read, q):
+    """pass_filters (:1135-1181) on a decoded record (no format errors in these inputs)."""
+    return (read.is_paired and read.is_proper_pair and not read.is_unmapped and not read.mate_is_unmapped
+            and not read.is_supplementary and not read.is_qcfail and read.mapping_quality >= q)
+
+
+def native_ingest(path, P, seed, reads):
+    rng = random.Random(seed)
+    ing = native_io.Ingest(path, P.min_map_quality, P.min_reads, P.max_reads, P.min_base_quality, 4)
+    ing.set_rng_state(rng.getstate())
+    out = []
+    while True:
+        hb = native_io.HostBatch(reads=reads, side_bytes=1 << 22)
+        ing.next(hb)
+        pk = hb.packed()
+        out.append((hb.s.n_reads, hb.s.n_bases, hb.s.n_cigar, hb.s.ss_cols, hb.s.ds_cols,
+                    {k: getattr(pk, k).copy() for k in BATCH_FIELDS}, hb.side("exc").tobytes(),
+                    hb.side("filt").tobytes()))
+        if hb.end_kind != native_io.END_FULL:
+            assert hb.end_kind == native_io.END_EOF
+            break
+    rng.setstate(ing.rng_state(rng.getstate()))
+    counters = ing.counters()
+    ing.close()
+    return out, rng, counters
+
+
+def concat(out):
+    cat = {k: [] for k in BATCH_FIELDS}
+    ro = bo = co = so = do = 0
+    for n_reads, n_bases, n_cig, ss_cols, ds_cols, a, _, _ in out:
+        for k, base in (("sub_off", ro), ("ss_col_off", so), ("ds_col_off", do)):
+            cat[k].append(a[k][1:] + base if cat[k] else a[k] + base)
+        for k in ("read_pos", "read_mapq", "seq_len", "cig_n", "cigar", "bases", "quals"):
+            cat[k].append(a[k])
+        cat["seq_off"].append(a["seq_off"] + bo)
+        cat["cig_off"].append(a["cig_off"] + co)
+        ro, bo, co, so, do = ro + n_reads, bo + n_bases, co + n_cig, so + ss_cols, do + ds_cols
+    return {k: np.concatenate(v) for k, v in cat.items()}
+
+
+@pytest.fixture(scope="module")
+def c1_bam(tmp_path_factory):
+    path = str(tmp_path_factory.mktemp("ing") / "c1.bam")
+    cfg = synth.SynthConfig("t", 600, sub_size="poisson5", indel_frac=0.1, softclip_frac=0.1, seed=5)
+    synth.write_config_bam(path, cfg)
+    return path
+
+
+@pytest.mark.parametrize("which,seed,max_reads,min_reads,reads", [
+    ("golden", 1, 100, 1, 1 << 16), ("golden", 7, 3, 1, 300), ("golden", 3, 6, 4, 200),
+    ("c1", 11, 7, 3, 5000), ("c1", 12, 4, 2, 1 << 20)])
+def test_ingest_matches_python_host_path(c1_bam, which, seed, max_reads, min_reads, reads):
+    path = GOLDEN_BAM if which == "golden" else c1_bam
+    P = ConsensusParams(max_reads=max_reads, min_reads=min_reads)
+    pk, exc, filt, rng1 = python_ingest(path, P, seed)
+    out, rng2, counters = native_ingest(path, P, seed, reads)
+    assert rng1.getstate() == rng2.getstate()
+    got = concat(out)
+    for k in BATCH_FIELDS:
+        assert np.array_equal(got[k], getattr(pk, k)), k
+    assert b"".join(o[6] for o in out) == b"".join(bam.encode_record(r) for r in exc)
+    assert b"".join(o[7] for o in out) == b"".join(bam.encode_record(r) for r in filt)
+    assert counters["excluded"] == len(exc) and counters["processed"] == pk.n_fam
+
+
+def test_ingest_rejects_truncated_input(tmp_path):
+    data = bam.bgzf_stream(GOLDEN_BAM)
+    bad = str(tmp_path / "trunc.bam")
+    w = bam.BGZFWriter(bad)
+    w.write(data[:len(data) - 100])          # ends inside a record
+    w.close()
+    ing = native_io.Ingest(bad)
+    hb = native_io.HostBatch(reads=1 << 16, side_bytes=1 << 22)
+    with pytest.raises(native_io.IOError_, match="truncated"):
+        ing.next(hb)
+    with pytest.raises(ValueError, match="truncated"):
+        with bam.AlignmentFile(bad, "rb") as f:
+            list(f)
+
+
+def test_ingest_rejects_non_bam(tmp_path):
+    p = tmp_path / "x.bam"
+    p.write_bytes(b"not a bam at all" * 10)
+    with pytest.raises(native_io.IOError_):
+        native_io.Ingest(str(p))
