@@ -1,30 +1,39 @@
-"""Benchmark: consensus bases/s of the duplex-consensus hot path on MI355X.
+"""Benchmark: consensus bases/s of the duplex-consensus drop-in on MI355X,
+whole node, plus the SSCS kernel's HBM roofline.
 
 Workload (BASELINE.json configs[1]): per GPU a synthetic
-duplex batch of 10 M reads = 312,500 MI families x 4 subfamilies x 8 reads,
+duplex BAM of 10 M reads = 312,500 MI families x 4 subfamilies x 8 reads,
 2x150 bp ``150M`` reads, no indels, qualities {Q37 .80, Q25 .12, Q12 .08}.
-One step = the whole hot path over that batch with inputs resident in HBM:
-1.25 M single-strand consensus records (k_recmeta<ss>, k_consensus_fast<ss>
-and its exact pass, k_decide + k_consensus_general<ss>) and 625 k duplex
-records (the same kernels <ds>), per-read preprocessing fused into them.
+
+value: one step = one run of the CLI drop-in (cli.main, the reference's
+``main`` DuplexUMIConsensusReads.py:1426-1650) over that BAM, from opening
+the input to closing the three outputs: native ingest (BGZF inflate,
+filters, grouping, downsampling, packing into pinned memory), asynchronous
+device batches (H2D, kernels, D2H on side streams), native record writer and
+BGZF deflate.  value = duplex consensus bases written by all ranks / the
+slowest rank's time (SURVEY.md §8d metric (1)).  The per-stage busy times are
+in config.stages.
+
+roofline: the single-strand kernel k_consensus_fast<ss> on the same batch
+with its inputs resident in HBM (K device-only passes, HIP events on the
+context stream): SURVEY.md §8d algorithmic bytes / average launch / 8 TB/s.
+config.device_resident holds that loop's consensus bases/s (kernels only).
+
+cpu_baseline: the C restatement (oracle/, kind "port") on the same batch.
+
 --config C3 / C4 / C5 runs the other BASELINE.json shapes (per-GPU shards).
-
-value = duplex consensus bases emitted by all ranks per second (weak scaling:
-each rank owns its own families, no data-path collective; max time over
-ranks).  roofline = the single-strand kernel's algorithmic bytes
- / its HIP-event-timed average launch / 8 TB/s.
-cpu_baseline = the C restatement (oracle/, kind "port") on a bounded sample
-of the same workload on this host.
-
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--families F]
-(N > 1 is launched by torch.distributed.run, one process per GPU.)
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
+(N > 1 is launched by torch.distributed.run, one process per GPU; every rank
+owns its own shard of families: weak scaling, no data-path collective.)
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shutil
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -35,7 +44,6 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 METRIC = "consensus bases/sec (whole node) + SSCS kernel HBM GB/s vs peak, 1/2/4/8 GPUs"
 
-
 # families per GPU for each workload shape (weak scaling: every rank its own shard)
 CONFIG_FAMILIES = {
     "C2": 312_500,     # 10 M reads: 4 subfamilies x 8 reads
@@ -44,7 +52,7 @@ CONFIG_FAMILIES = {
     "C5": 200_000,     # one 4 M-read streaming chunk of the 1 B-read run: Poisson(4)+1
 }
 WORKLOAD = {
-    "C2": "C2 (BASELINE.json configs[1]): 10M-read synthetic duplex batch per GPU, 312,500 MI families x "
+    "C2": "C2 (BASELINE.json configs[1]): 10M-read synthetic duplex BAM per GPU, 312,500 MI families x "
           "4 subfamilies x 8 reads, 2x150bp, no indels",
     "C3": "C3 shape (BASELINE.json configs[2]) per GPU: skewed subfamilies Zipf(1.5) on 1..100, 5% of reads with "
           "a 1-3 bp indel, 3% soft-clipped, 2x150bp",
@@ -67,8 +75,7 @@ def log(*a):
 
 def sscs_algorithmic_bytes(packed):
     """sum_r(2 len_r + 4 n_cig_r + 4 + 1) + T*(2 + 4) + 16 per
-    subfamily, with T the subfamily's alignment width (here T_ub == T: no
-    clipping, no indels)."""
+    subfamily, with T the subfamily's output region (T_ub rounded to 16)."""
     per_read = 2 * packed.seq_len.astype(np.int64) + 4 * packed.cig_n.astype(np.int64) + 5
     reads_b = int(per_read.sum())
     cols = int(packed.ss_col_off[-1])
@@ -80,7 +87,7 @@ def cpu_baseline(packed, reps):
     """The C restatement (oracle/dcr_oracle.c, test infrastructure used here
     only as the timed CPU leg) over the bench batch itself, multi-threaded
     over families.  The C2 batch takes ~1-2 s per pass on 16 threads, so the
-    sample is the whole batch, repeated ``reps`` times (≈10-30 thread-s)."""
+    sample is the whole batch, repeated ``reps`` times (~10-30 thread-s)."""
     from duplexumiconsensusreads_amd.params import ConsensusParams
     from oracle import dcr_oracle_c
     threads = min(16, os.cpu_count() or 1)   # the GPU box's CPU share is 16
@@ -94,8 +101,8 @@ def cpu_baseline(packed, reps):
     dt = min(dts)
     return {"value": bases / dt, "unit": "consensus bases/s", "cores": threads, "kind": "port",
             "sample": f"the whole bench batch ({packed.n_fam} families, {packed.n_reads} reads), "
-                      f"C restatement oracle/dcr_oracle.c on {threads} threads, best of {reps}: "
-                      f"{dt:.2f} s per pass"}
+                      f"C restatement oracle/dcr_oracle.c on {threads} threads, kernels only (no BAM I/O), "
+                      f"best of {reps}: {dt:.2f} s per pass"}
 
 
 def load_traffic(kernel, n_fam):
@@ -113,11 +120,64 @@ def load_traffic(kernel, n_fam):
         return None, None
 
 
+def device_resident(packed, params, local, steps, warmup):
+    """K device-only passes over the batch resident in HBM (kernel timing)."""
+    import torch
+    from duplexumiconsensusreads_amd import _lib
+    from duplexumiconsensusreads_amd.device import DeviceBatch
+    db = DeviceBatch(packed, device=f"cuda:{local}")
+    ctx = _lib.Context(params, device=local)
+    ctx.reserve(db.batch_struct)
+    torch.cuda.synchronize()
+    for _ in range(warmup):
+        ctx.run_device(db.batch_struct, db.ss_struct, db.ds_struct)
+    ctx.sync()
+    st_ss = db.out["ss"]["status"][:4 * packed.n_fam]
+    st_ds = db.out["ds"]["status"][:2 * packed.n_fam]
+    n_bad = int((st_ss != 0).sum().item() + (st_ds != 0).sum().item())
+    bases = int(db.out["ds"]["len"].view(torch.int32)[:2 * packed.n_fam].sum().item())
+    kms = {k: 0.0 for k in _lib.KERNELS}
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.run_device(db.batch_struct, db.ss_struct, db.ds_struct)
+        tm = ctx.last_kernel_timing()   # waits on this step's events only
+        for k in kms:
+            kms[k] += tm[k]
+    ctx.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ctx.close()
+    del db
+    torch.cuda.empty_cache()
+    return {k: v / steps for k, v in kms.items()}, bases, n_bad, dt / steps
+
+
+def e2e_passes(path, params_args, device, steps, warmup, workdir):
+    """W untimed + K timed CLI runs over the BAM at ``path``; returns
+    (seconds of the K runs, stats of the last run)."""
+    from duplexumiconsensusreads_amd import cli
+    out = os.path.join(workdir, "cons.bam")
+    argv = ["-i", path, "-o", out, "--device", str(device), *params_args]
+    import contextlib
+    import io
+    for _ in range(warmup):
+        with contextlib.redirect_stdout(io.StringIO()):
+            cli.main(argv)
+    stats = {}
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        stats = {}
+        with contextlib.redirect_stdout(io.StringIO()):
+            cli.main(argv, stats=stats)
+    return time.perf_counter() - t0, stats
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIG_FAMILIES),
                     help="workload shape (SURVEY.md §8d); C2 is the headline line, the others are "
                          "per-GPU shards of C3 / C4 / C5 reported for coverage")
@@ -125,6 +185,8 @@ def main():
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--cpu-reps", type=int, default=2, help="passes of the CPU baseline over the batch")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--kernel-only", action="store_true", help="skip the whole-node CLI runs")
+    ap.add_argument("--kernel-steps", type=int, default=10, help="device-resident passes for the roofline")
     args = ap.parse_args()
 
     import torch
@@ -132,84 +194,88 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    dev = f"cuda:{local}"
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    from duplexumiconsensusreads_amd import _lib
-    from duplexumiconsensusreads_amd.device import DeviceBatch
+        tdist.init_process_group("nccl", device_id=torch.device(dev))
+    from duplexumiconsensusreads_amd import _lib, shard, synth
     from duplexumiconsensusreads_amd.params import ConsensusParams
 
     t0 = time.perf_counter()
     families = args.families or CONFIG_FAMILIES[args.config]
     packed = make_batch(args.config, families, args.seed + 1000 * rank)
     log(f"[rank {rank}] generated {packed.n_reads} reads in {time.perf_counter() - t0:.1f} s")
-    dev = f"cuda:{local}"
-    db = DeviceBatch(packed, device=dev)
     # C4 runs with --max_reads 1000; the batch is already downsampled
     params = ConsensusParams(max_reads=1000) if args.config == "C4" else ConsensusParams()
-    ctx = _lib.Context(params, device=local)
-    ctx.reserve(db.batch_struct)
-    torch.cuda.synchronize()
+    params_args = ["--max_reads", "1000"] if args.config == "C4" else []
 
-    for _ in range(args.warmup):
-        ctx.run_device(db.batch_struct, db.ss_struct, db.ds_struct)
-    ctx.sync()
-    # correctness guard on the bench batch itself: every record must be OK
-    st_ss = db.out["ss"]["status"][:4 * packed.n_fam]
-    st_ds = db.out["ds"]["status"][:2 * packed.n_fam]
-    n_bad = int((st_ss != 0).sum().item() + (st_ds != 0).sum().item())
-    bases = int(db.out["ds"]["len"].view(torch.int32)[:2 * packed.n_fam].sum().item())
+    # -- SSCS kernel roofline: device-resident passes ------------------------------
+    kavg, dev_bases, n_bad, dev_step = device_resident(packed, params, local, args.kernel_steps, 2)
+    log(f"[rank {rank}] device-resident step {dev_step * 1e3:.2f} ms")
 
+    # -- whole node: the CLI over a BAM of the same families -------------------------
+    workdir = tempfile.mkdtemp(prefix=f"dcr_bench_r{rank}_", dir=os.environ.get("DCR_BENCH_DIR"))
+    stats, e2e_s = {}, None
+    try:
+        if not args.kernel_only:
+            bam_path = os.path.join(workdir, "in.bam")
+            t0 = time.perf_counter()
+            synth.write_packed_bam(bam_path, packed, seed=args.seed + 1000 * rank, level=1)
+            log(f"[rank {rank}] wrote {os.path.getsize(bam_path) / 1e6:.0f} MB BAM in {time.perf_counter() - t0:.1f} s")
+            if dist:
+                tdist.barrier()
+            torch.cuda.synchronize()
+            e2e_s, stats = e2e_passes(bam_path, params_args, local, args.steps, args.warmup, workdir)
+            torch.cuda.synchronize()
+            if dist:
+                tdist.barrier()
+            log(f"[rank {rank}] {args.steps} CLI passes in {e2e_s:.2f} s: {stats}")
+    finally:
+        shutil.rmtree(workdir, ignore_errors=True)
+
+    e2e_bases = stats.get("consensus_bases", 0) * args.steps
+    in_bases = int(packed.seq_len.astype(np.int64).sum()) * args.steps
     if dist:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    kms = {k: 0.0 for k in _lib.KERNELS}
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ctx.run_device(db.batch_struct, db.ss_struct, db.ds_struct)
-        tm = ctx.last_kernel_timing()   # waits on this step's events only
-        for k in kms:
-            kms[k] += tm[k]
-    ctx.sync()
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        from duplexumiconsensusreads_amd import shard
-        elapsed = shard.max_over_ranks(elapsed, device=dev)
-        total_bases, n_bad = shard.sum_over_ranks([bases, n_bad], device=dev)
+        slowest = shard.max_over_ranks(e2e_s or 0.0, device=dev)
+        dev_slowest = shard.max_over_ranks(dev_step, device=dev)
+        e2e_bases, in_bases, dev_bases, n_bad = shard.sum_over_ranks([e2e_bases, in_bases, dev_bases, n_bad], device=dev)
     else:
-        total_bases = bases
+        slowest, dev_slowest = e2e_s or 0.0, dev_step
 
     if rank == 0:
-        ms_step = elapsed * 1000.0 / args.steps
-        value = total_bases * args.steps / elapsed
-        kavg = {k: v / args.steps for k, v in kms.items()}
         alg = sscs_algorithmic_bytes(packed)
         if args.config == "C2":
             dom, dom_label = "k_consensus_fast<ss>", "k_consensus_fast<false, false> (single-strand consensus)"
             dom_ms = kavg[dom]
             traffic, tsrc = load_traffic("k_consensus_fast<false, false>", packed.n_fam)
         else:
-            # records split between the fast and general kernels: the whole single-strand stage
             dom_label = "single-strand stage (k_recmeta<ss> + k_consensus_fast<ss> + k_consensus_exact<ss> + k_consensus_general<ss>)"
             dom_ms = sum(kavg[k] for k in _lib.KERNELS[1:5])
             traffic, tsrc = None, None
         achieved = alg / (dom_ms / 1000.0) / 1e9
+        if args.kernel_only:
+            value, ms_step = dev_bases / dev_slowest, dev_slowest * 1e3
+            value_kind = "device-resident kernels only (--kernel-only)"
+        else:
+            value, ms_step = e2e_bases / slowest, slowest * 1e3 / args.steps
+            value_kind = "whole node: CLI from BAM open to output close"
+        stage = {k: round(v, 4) for k, v in stats.items() if k.endswith("_s")}
         res = {
             "metric": METRIC, "value": value, "unit": "consensus bases/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": WORKLOAD[args.config],
+            "config": {"workload": WORKLOAD[args.config], "value_is": value_kind,
                        "families_per_gpu": packed.n_fam, "reads_per_gpu": packed.n_reads,
-                       "input_bytes_per_gpu": packed.nbytes(),
-                       "kernel_ms": kavg,
+                       "input_bases_per_s": (in_bases / slowest) if slowest else None,
+                       "consensus_records_per_pass": stats.get("consensus_records"),
+                       "stages_s_last_pass": stage,
+                       "device_resident": {"consensus_bases_per_s": dev_bases / dev_slowest,
+                                           "ms_per_step": dev_slowest * 1e3, "kernel_ms": kavg,
+                                           "records_not_ok": n_bad},
                        "single_strand_stage_GBps": alg / (sum(kavg[k] for k in _lib.KERNELS[1:5]) / 1e3) / 1e9,
-                       "records_not_ok": n_bad,
-                       "parallelism": f"family-sharded x{world}, no data-path collective"},
+                       "parallelism": f"family-sharded x{world}, one process per GPU, no data-path collective"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": dom_label,
@@ -217,12 +283,10 @@ def main():
                          "traffic_source": (f"profiles/traffic.json ({tsrc.get('source', '')})" if tsrc else None)},
         }
         if not args.no_cpu and world == 1:
-            del db
             res["cpu_baseline"] = cpu_baseline(packed, args.cpu_reps)
         else:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)
-    ctx.close()
     if dist:
         tdist.destroy_process_group()
 

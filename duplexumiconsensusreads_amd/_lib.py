@@ -32,6 +32,11 @@ EXPORTS = {
     "dcr_read_info_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "dcr_last_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "dcr_last_kernel_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "dcr_host_alloc": (ctypes.c_void_p, [ctypes.c_size_t]),
+    "dcr_host_free": (None, [ctypes.c_void_p]),
+    "dcr_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_void_p]),
+    "dcr_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
 }
 
 # HIP-event slots of dcr_last_kernel_timing: k_recmeta<ss> includes k_prep_big,

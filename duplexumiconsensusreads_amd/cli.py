@@ -25,10 +25,12 @@ exception, or its message and ``sys.exit(1)``, is raised at that family.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import queue
 import random
 import sys
 import threading
+import time
 from typing import Optional
 
 import numpy as np
@@ -62,7 +64,7 @@ def parse_args(argv):
     ap.add_argument("--deletion_score", required=False, default=30, type=int)
     ap.add_argument("--no_insertion_score", required=False, default=30, type=int)
     # not reference flags: batching and codec knobs (they do not change any record)
-    ap.add_argument("--batch_reads", required=False, default=1 << 20, type=int, help=argparse.SUPPRESS)
+    ap.add_argument("--batch_reads", required=False, default=1 << 19, type=int, help=argparse.SUPPRESS)
     ap.add_argument("--threads", required=False, default=0, type=int, help=argparse.SUPPRESS)
     ap.add_argument("--compression_level", required=False, default=6, type=int, help=argparse.SUPPRESS)
     ap.add_argument("--device", required=False, default=0, type=int, help=argparse.SUPPRESS)
@@ -143,12 +145,12 @@ def default_backend(params: ConsensusParams, device: int = 0):
     from . import _lib
     from .stream import DeviceStream
     ctx = _lib.Context(params, device=device)
-    return DeviceStream(ctx)
+    return DeviceStream(ctx, owns_ctx=True)
 
 
-def _as_backend(backend, params):
+def _as_backend(backend, params, device=0):
     if backend is None:
-        return default_backend(params)
+        return default_backend(params, device)
     if hasattr(backend, "submit"):
         return backend
     from .stream import CallBackend
@@ -170,6 +172,9 @@ class _Driver:
         self.args, self.params, self.backend = args, params, backend
         self.ing, self.cons, self.excl, self.unproc = ing, cons, excl, unproc
         self.verbose = args.verbose
+        # per-stage busy seconds and totals (bench.py --e2e reports them)
+        self.stats = {"batches": 0, "consensus_records": 0, "consensus_bases": 0, "ingest_s": 0.0,
+                      "submit_s": 0.0, "wait_s": 0.0, "write_s": 0.0}
 
     # -- stdout of one batch, in the reference's order --------------------------
     def _prints(self, hb, fail_f, kind, which, last_batch):
@@ -280,11 +285,20 @@ class _Driver:
 
     # -- one batch --------------------------------------------------------------
     def finish(self, hb, handle, last_batch):
+        t0 = time.perf_counter()
         ss, ds, rstat = self.backend.result(handle)
+        t1 = time.perf_counter()
         F = hb.n_fam
         fail_f, kind, which = native_io.first_failure(hb, ss, ds, F, rstat)
         self._prints(hb, fail_f, kind, which, last_batch)
         self.cons.write_consensus(hb, ss, ds, fail_f)
+        st = self.stats
+        st["batches"] += 1
+        st["consensus_records"] += 2 * fail_f
+        if fail_f:
+            st["consensus_bases"] += int(np.ctypeslib.as_array(ctypes.cast(ds.len, ctypes.POINTER(ctypes.c_int32)),
+                                                              (2 * fail_f,)).sum())
+        st["wait_s"] += t1 - t0
         if fail_f < F:
             t = int(np.nonzero(hb.a["tab_proc"][:hb.s.n_tab] == fail_f)[0][0])
             exc_cut, filt_cut = int(hb.a["tab_exc_cut"][t]), int(hb.a["tab_filt_cut"][t])
@@ -292,6 +306,7 @@ class _Driver:
             exc_cut, filt_cut = hb.s.n_side_exc, hb.s.n_side_filt
         self.excl.write(hb.a["side_exc"][:exc_cut])
         self.unproc.write(hb.a["side_filt"][:filt_cut])
+        st["write_s"] += time.perf_counter() - t1
         if fail_f < F:
             if kind == "exit":
                 col = badchar_column(hb, fail_f, which, self.params.min_base_quality) if which < 4 else None
@@ -320,7 +335,9 @@ class _Driver:
                     hb = free.get()
                     if hb is None:
                         return
+                    t0 = time.perf_counter()
                     self.ing.next(hb)
+                    self.stats["ingest_s"] += time.perf_counter() - t0
                     ready.put(hb)
                     if hb.end_kind != native_io.END_FULL:
                         return
@@ -335,7 +352,9 @@ class _Driver:
                 hb = ready.get()
                 if isinstance(hb, BaseException):
                     raise hb
+                t0 = time.perf_counter()
                 handle = self.backend.submit(hb)
+                self.stats["submit_s"] += time.perf_counter() - t0
                 if pending is not None:
                     self.finish(*pending, last_batch=False)
                     free.put(pending[0])
@@ -351,8 +370,9 @@ class _Driver:
             self.backend.close()
 
 
-def main(argv: Optional[list] = None, backend=None, rng=random) -> int:
-    """``main`` (:1426-1650).  ``backend`` defaults to the HIP library."""
+def main(argv: Optional[list] = None, backend=None, rng=random, stats: Optional[dict] = None) -> int:
+    """``main`` (:1426-1650).  ``backend`` defaults to the HIP library;
+    ``stats`` (optional) receives per-stage times and output totals."""
     args = parse_args(sys.argv[1:] if argv is None else argv)
     params = ConsensusParams.from_args(args)
     try:
@@ -372,15 +392,22 @@ def main(argv: Optional[list] = None, backend=None, rng=random) -> int:
         print("ERROR: output file is not specified in the right format. \n Please specify the file name of a "
               "valid .bam file. Include the format in the file name.")
         raise ReferenceExit(1)
-    be = _as_backend(backend, params)
+    be = _as_backend(backend, params, args.device)
     lvl, nt = args.compression_level, args.threads
     cons = native_io.BgzfWriter(consensus_filename, ing.header, lvl, nt)
     excl = native_io.BgzfWriter("%s_filteredreads.bam" % consensus_filename[:-4], ing.header, lvl, nt)
     unproc = native_io.BgzfWriter("%s_filteredfamilies.bam" % consensus_filename[:-4], ing.header, lvl, nt)
     ing.set_rng_state(rng.getstate())
     try:
-        _Driver(args, params, be, ing, cons, excl, unproc).run(max(args.batch_reads, 1))
+        drv = _Driver(args, params, be, ing, cons, excl, unproc)
+        try:
+            drv.run(max(args.batch_reads, 1))
+        finally:
+            if stats is not None:
+                stats.update(drv.stats)
         c = ing.counters()
+        if stats is not None:
+            stats.update(c)
         if args.verbose:
             print("\n Input file has been completely read \n")
         passed_reads, excluded_reads = c["passed"], c["excluded"]

@@ -125,15 +125,51 @@ void float_tag(Buf &o, const char *tag, double v) {
 
 void z_begin(Buf &o, const char *tag) { o.raw(tag, 2); o.b('Z'); }
 
-// "[1, 2, 3]" (str() of a list of numpy-1.x ints)
+// ", <v>" for v < 1000 as 8 bytes (length in the last byte)
+struct ListTab {
+    uint8_t t[1000][8];
+    ListTab() {
+        for (int v = 0; v < 1000; ++v) {
+            char s[8] = {',', ' '};
+            int n = std::snprintf(s + 2, 6, "%d", v);
+            std::memcpy(t[v], s, 7);
+            t[v][7] = (uint8_t)(2 + n);
+        }
+    }
+};
+const ListTab kList;
+
+// "[1, 2, 3]" (str() of a list of numpy-1.x ints); the caller reserved
+// 7 bytes per value plus slack, so the 8-byte copies may run past the text
 void list_text(Buf &o, const char *tag, const uint16_t *v, int32_t n) {
     z_begin(o, tag);
     o.b('[');
+    uint8_t *p = o.p();
     for (int32_t i = 0; i < n; ++i) {
-        if (i) { o.b(','); o.b(' '); }
-        o.uint(v[i]);
+        const uint32_t x = v[i];
+        if (x < 1000) {
+            std::memcpy(p, kList.t[x], 8);
+            p += kList.t[x][7];
+        } else {
+            p[0] = ','; p[1] = ' ';
+            p += 2 + std::snprintf((char *)p + 2, 8, "%u", x);
+        }
     }
+    if (n) {                                   // drop the first ", "
+        const size_t len = (size_t)(p - o.p());
+        std::memmove(o.p(), o.p() + 2, len - 2);
+        p -= 2;
+    }
+    o.n = (size_t)(p - o.v.data());
     o.b(']');
+    o.b(0);
+}
+
+void phred_text(Buf &o, const char *tag, const uint8_t *q, int32_t n) {
+    z_begin(o, tag);
+    uint8_t *p = o.p();
+    for (int32_t i = 0; i < n; ++i) p[i] = (uint8_t)(q[i] + 33);
+    o.n += (size_t)n;
     o.b(0);
 }
 
@@ -151,6 +187,20 @@ struct Ctx {
     const dcr_host_batch *hb;
     const dcr_fmt_out *ss, *ds;
 };
+
+// one BGZF block of in[0, len) (len <= 0xff00) at out (>= 64 KiB); returns its size
+size_t bgzf_block(const uint8_t *in, size_t len, int level, uint8_t *out) {
+    size_t clen = libdeflate_deflate_compress(tl_comp.get(level), in, len, out + 18, 0x10000 - 26);
+    if (clen == 0) clen = libdeflate_deflate_compress(tl_comp.get(0), in, len, out + 18, 0x10000 - 26);
+    if (clen == 0) return 0;
+    out[0] = 0x1f; out[1] = 0x8b; out[2] = 8; out[3] = 4;
+    wr32(out + 4, 0); out[8] = 0; out[9] = 0xff;
+    wr16(out + 10, 6); out[12] = 66; out[13] = 67; wr16(out + 14, 2);
+    wr16(out + 16, (uint32_t)(clen + 25));
+    wr32(out + 18 + clen, libdeflate_crc32(0, in, len));
+    wr32(out + 22 + clen, (uint32_t)len);
+    return clen + 26;
+}
 
 }  // namespace
 
@@ -174,20 +224,8 @@ struct dcr_bgzw {
             const size_t off = i * kBlockData, len = std::min(kBlockData, n - off);
             std::vector<uint8_t> &o = out[i];
             if (o.size() < 0x10000) o.resize(0x10000);
-            size_t clen = libdeflate_deflate_compress(tl_comp.get(lvl), in.data() + off, len, o.data() + 18,
-                                                      0x10000 - 26);
-            if (clen == 0) clen = libdeflate_deflate_compress(tl_comp.get(0), in.data() + off, len, o.data() + 18,
-                                                              0x10000 - 26);
-            if (clen == 0) return false;
-            uint8_t *h = o.data();
-            h[0] = 0x1f; h[1] = 0x8b; h[2] = 8; h[3] = 4;
-            wr32(h + 4, 0); h[8] = 0; h[9] = 0xff;
-            wr16(h + 10, 6); h[12] = 66; h[13] = 67; wr16(h + 14, 2);
-            wr16(h + 16, (uint32_t)(clen + 25));
-            wr32(o.data() + 18 + clen, libdeflate_crc32(0, in.data() + off, len));
-            wr32(o.data() + 22 + clen, (uint32_t)len);
-            out_len[i] = clen + 26;
-            return true;
+            out_len[i] = bgzf_block(in.data() + off, len, lvl, o.data());
+            return out_len[i] != 0;
         });
         if (!ok) { g_err = "BGZF block failed to deflate"; return false; }
         for (size_t i = 0; i < nb; ++i) {
@@ -195,6 +233,12 @@ struct dcr_bgzw {
             bytes_out += (int64_t)out_len[i];
         }
         bytes_in += (int64_t)n;
+        return true;
+    }
+    bool put_compressed(const uint8_t *s, size_t n, size_t raw) {
+        if (std::fwrite(s, 1, n, f) != n) { g_err = "write failed"; return false; }
+        bytes_out += (int64_t)n;
+        bytes_in += (int64_t)raw;
         return true;
     }
     bool write(const uint8_t *s, size_t n) {
@@ -278,12 +322,8 @@ void format_record(const Ctx &c, int32_t f, int j, const char *code, size_t l_co
     float_tag(o, "aE", ss->E[a]); float_tag(o, "bE", ss->E[b]); float_tag(o, "cE", ds->E[k]);
     z_begin(o, "ac"); o.raw(ss->seq + ao, (size_t)ss->len[a]); o.b(0);
     z_begin(o, "bc"); o.raw(ss->seq + bo, (size_t)ss->len[b]); o.b(0);
-    z_begin(o, "aq");
-    for (int32_t i = 0; i < ss->len[a]; ++i) o.b((uint8_t)(ss->qual[ao + i] + 33));
-    o.b(0);
-    z_begin(o, "bq");
-    for (int32_t i = 0; i < ss->len[b]; ++i) o.b((uint8_t)(ss->qual[bo + i] + 33));
-    o.b(0);
+    phred_text(o, "aq", ss->qual + ao, ss->len[a]);
+    phred_text(o, "bq", ss->qual + bo, ss->len[b]);
     wr32(o.v.data() + rec0, (uint32_t)(o.n - rec0 - 4));
 }
 
@@ -292,7 +332,7 @@ size_t record_bound(const Ctx &c, int32_t f, int j, size_t l_code) {
     size_t n = 36 + 16 + l_code + 13 + 4 * (size_t)c.ds->n_cig[k] + (size_t)c.ds->len[k] * 2;
     n += 8 + l_code + 4 + std::strlen(c.hb->names + c.hb->fam_rx[2 * f + j]);
     n += 24 + (size_t)(c.hb->sub_off[a + 1] - c.hb->sub_off[a]) + (size_t)(c.hb->sub_off[b + 1] - c.hb->sub_off[b]);
-    n += 16 + 7 * (2 * (size_t)c.ss->n_de[a] + 2 * (size_t)c.ss->n_de[b] + 2 * (size_t)c.ds->n_de[k]) + 64;
+    n += 16 + 8 * (2 * (size_t)c.ss->n_de[a] + 2 * (size_t)c.ss->n_de[b] + 2 * (size_t)c.ds->n_de[k]) + 64;
     n += 9 * 8 + 3 * 8 + 2 * ((size_t)c.ss->len[a] + c.ss->len[b]) + 32;
     return n;
 }
@@ -382,15 +422,24 @@ int dcr_fmt_write(dcr_bgzw *w, const dcr_host_batch *hb, const dcr_fmt_out *ss, 
     for (int32_t t = 0; t < hb->n_tab; ++t)
         if (hb->tab_kind[t] == DCR_FAM_PROCESSED && hb->tab_proc[t] < n_fam) code_of[(size_t)hb->tab_proc[t]] = hb->tab_code[t];
     const Ctx c{hb, ss, ds};
-    const int32_t chunk = 512;
+    // pending bytes first (blocks stay in order)
+    if (w->n_in) {
+        if (!w->flush(w->n_in)) { w->bad = true; return DCR_IO_EFILE; }
+        w->n_in = 0;
+    }
+    // chunks of families, each formatted and deflated by one task into its
+    // own run of BGZF blocks (a record may span blocks), written in order
+    const int32_t chunk = 128;
     const int32_t nch = (n_fam + chunk - 1) / chunk;
-    // format chunks of families in parallel, append them in order
     const int32_t group = std::max(1, 4 * w->pool->size());
-    std::vector<Buf> bufs((size_t)std::min(nch, group));
+    struct Task { Buf raw; std::vector<uint8_t> comp; size_t n_comp = 0; };
+    std::vector<Task> tasks((size_t)std::min(nch, group));
+    const int lvl = w->level;
     for (int32_t g0 = 0; g0 < nch; g0 += group) {
         const int32_t g1 = std::min(nch, g0 + group);
-        w->pool->run((size_t)(g1 - g0), [&](size_t gi) {
-            Buf &o = bufs[gi];
+        const bool ok = w->pool->run((size_t)(g1 - g0), [&](size_t gi) {
+            Task &t = tasks[gi];
+            Buf &o = t.raw;
             o.n = 0;
             const int32_t f0 = (g0 + (int32_t)gi) * chunk, f1 = std::min(n_fam, f0 + chunk);
             for (int32_t f = f0; f < f1; ++f) {
@@ -401,10 +450,23 @@ int dcr_fmt_write(dcr_bgzw *w, const dcr_host_batch *hb, const dcr_fmt_out *ss, 
                     format_record(c, f, j, code, lc, o);
                 }
             }
+            const size_t nb = (o.n + kBlockData - 1) / kBlockData;
+            if (t.comp.size() < nb * 0x10000) t.comp.resize(nb * 0x10000);
+            t.n_comp = 0;
+            for (size_t b = 0; b < nb; ++b) {
+                const size_t off = b * kBlockData, len = std::min(kBlockData, o.n - off);
+                const size_t cl = bgzf_block(o.v.data() + off, len, lvl, t.comp.data() + t.n_comp);
+                if (!cl) return false;
+                t.n_comp += cl;
+            }
             return true;
         });
+        if (!ok) { w->bad = true; return fail(DCR_IO_EFILE, "BGZF block failed to deflate"); }
         for (int32_t gi = 0; gi < g1 - g0; ++gi)
-            if (!w->write(bufs[(size_t)gi].v.data(), bufs[(size_t)gi].n)) { w->bad = true; return DCR_IO_EFILE; }
+            if (!w->put_compressed(tasks[(size_t)gi].comp.data(), tasks[(size_t)gi].n_comp, tasks[(size_t)gi].raw.n)) {
+                w->bad = true;
+                return DCR_IO_EFILE;
+            }
     }
     return DCR_IO_OK;
 }

@@ -189,6 +189,18 @@ struct dcr_ingest {
         struct Blk { size_t coff, clen, doff; uint32_t isize, crc; };
         std::vector<Blk> blks;
         size_t total = 0;
+        auto top_up = [&]() {
+            std::memmove(cbuf.data(), cbuf.data() + cbeg, cend - cbeg);
+            cend -= cbeg;
+            cbeg = 0;
+            while (!file_eof && cend < cbuf.size()) {
+                const size_t got = std::fread(cbuf.data() + cend, 1, cbuf.size() - cend, f);
+                cend += got;
+                if (got == 0) file_eof = true;
+            }
+        };
+        // compressed bytes are only moved while no parsed block points into them
+        if (!file_eof && cend - cbeg < cbuf.size() / 2) top_up();
         for (;;) {
             while (cend - cbeg >= 18 && total + 0x10000 <= want) {
                 const uint8_t *h = cbuf.data() + cbeg;
@@ -220,18 +232,12 @@ struct dcr_ingest {
                 blks.push_back(b);
                 cbeg += blen;
             }
-            if (total + 0x10000 > want) break;          // enough for this window
+            if (!blks.empty()) break;                   // inflate these; the next refill reads on
             if (file_eof) {
                 if (cend > cbeg) { g_err = "truncated BGZF block at the end of the file"; return false; }
                 break;
             }
-            // more compressed bytes
-            std::memmove(cbuf.data(), cbuf.data() + cbeg, cend - cbeg);
-            cend -= cbeg;
-            cbeg = 0;
-            const size_t got = std::fread(cbuf.data() + cend, 1, cbuf.size() - cend, f);
-            cend += got;
-            if (got == 0) file_eof = true;
+            top_up();
         }
         const std::vector<Blk> *bp = &blks;
         const bool ok = pool->run(blks.size(), [&](size_t i) {

@@ -55,6 +55,12 @@ class HostBatchStruct(ctypes.Structure):
                    ("err_kind", _i32), ("reserved1", _i32), ("err_msg", ctypes.c_char * 512)])
 
 
+class SynthIn(ctypes.Structure):
+    _fields_ = [("n_fam", _i32), ("tid", _i32), ("fam_id0", _i64)] + [
+        (n, _vp) for n in ("sub_off", "read_pos", "read_mapq", "seq_off", "seq_len", "cig_off", "cig_n", "cigar",
+                           "bases", "quals", "umis")]
+
+
 class FmtOut(ctypes.Structure):
     _fields_ = [(n, _vp) for n in ("status", "pos", "mapq", "len", "n_cig", "n_de", "D", "M", "E", "seq", "qual",
                                    "cigar", "d", "e")]
@@ -90,6 +96,7 @@ def load():
             "dcr_bgzw_sizes": (_i32, [_vp, _vp]),
             "dcr_fmt_scan": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp, _vp]),
             "dcr_fmt_write": (_i32, [_vp, _vp, _vp, _vp, _i32]),
+            "dcr_synth_write": (_i32, [_vp, _vp, _i32]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -261,6 +268,19 @@ class BgzfWriter:
         if n_fam and load().dcr_fmt_write(self._h, ctypes.byref(hb.s), ctypes.byref(ss), ctypes.byref(ds),
                                           n_fam) != 0:
             raise _err("consensus write")
+
+    def write_synthetic(self, packed, umis, fam_id0=0, tid=0, n_threads=0):
+        """Records of every family of ``packed`` (dcr_synth_write)."""
+        si = SynthIn()
+        si.n_fam, si.tid, si.fam_id0 = packed.n_fam, tid, fam_id0
+        for k in ("sub_off", "read_pos", "read_mapq", "seq_off", "seq_len", "cig_off", "cig_n", "cigar", "bases",
+                  "quals"):
+            setattr(si, k, getattr(packed, k).ctypes.data)
+        u = np.ascontiguousarray(umis, dtype=np.uint8)
+        assert u.size >= 16 * packed.n_fam
+        si.umis = u.ctypes.data
+        if load().dcr_synth_write(self._h, ctypes.byref(si), n_threads) != 0:
+            raise _err("synthetic write")
 
     def sizes(self):
         out = np.zeros(2, np.int64)

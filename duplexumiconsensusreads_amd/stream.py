@@ -106,9 +106,10 @@ class _HostOut:
 class DeviceStream:
     """Asynchronous batches on one GPU context (``_lib.Context``)."""
 
-    def __init__(self, ctx, n_slots=2):
+    def __init__(self, ctx, n_slots=2, owns_ctx=False):
         from . import _lib
         self.ctx = ctx
+        self.owns_ctx = owns_ctx
         self.lib = _lib.load()
         self.n_slots = n_slots
         self.outs = [_HostOut(self.lib) for _ in range(n_slots)]
@@ -147,6 +148,8 @@ class DeviceStream:
             if self.busy[slot]:
                 self.lib.dcr_wait(self.ctx._ctx, slot)
                 self.busy[slot] = False
+        if self.owns_ctx:
+            self.ctx.close()
 
 
 class CallBackend:

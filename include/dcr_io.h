@@ -190,6 +190,24 @@ int32_t dcr_fmt_scan(const dcr_host_batch *hb, const dcr_fmt_out *ss, const dcr_
 int dcr_fmt_write(dcr_bgzw *w, const dcr_host_batch *hb, const dcr_fmt_out *ss, const dcr_fmt_out *ds,
                   int32_t n_fam);
 
+/* ---- synthetic inputs (bench / tests) ----
+ * Records of n_fam duplex families from dcr_batch-layout arrays (reads of
+ * family f's subfamily k = A1 B2 B1 A2 at sub_off[4f+k] ..), fgbio
+ * GroupReadsByUmi style: flags 99 163 83 147, MI "<fam>/A|B", RX "U1-U2" on
+ * A and "U2-U1" on B (umis: 16 letters per family), names mol<fam>_<k>_<j>. */
+typedef struct dcr_synth_in {
+    int32_t n_fam, tid;
+    int64_t fam_id0;
+    const int32_t *sub_off, *read_pos;
+    const uint8_t *read_mapq;
+    const int64_t *seq_off;
+    const int32_t *seq_len, *cig_off, *cig_n;
+    const uint32_t *cigar;
+    const uint8_t *bases, *quals;
+    const char *umis;
+} dcr_synth_in;
+int dcr_synth_write(dcr_bgzw *w, const dcr_synth_in *in, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

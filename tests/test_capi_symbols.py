@@ -38,6 +38,13 @@ def test_library_exports_every_header_function(lib):
     assert lib.dcr_abi_version() == 1
 
 
+def test_every_header_function_has_a_ctypes_signature():
+    # a missing restype would truncate returned pointers (dcr_host_alloc) to int
+    from duplexumiconsensusreads_amd import _lib
+    declared = set(header_functions()) - {"dcr_oracle_run"}
+    assert declared <= set(_lib.EXPORTS), sorted(declared - set(_lib.EXPORTS))
+
+
 def test_oracle_library_exports_oracle_entry():
     from oracle import dcr_oracle_c
     assert hasattr(dcr_oracle_c.load(), "dcr_oracle_run")
