@@ -37,6 +37,11 @@ EXPORTS = {
     "dcr_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_void_p]),
     "dcr_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "dcr_submit_write": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p]),
+    "dcr_wait_write": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "dcr_slot_fetch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                                      ctypes.c_void_p]),
 }
 
 # HIP-event slots of dcr_last_kernel_timing: k_recmeta<ss> includes k_prep_big,

@@ -286,18 +286,34 @@ class _Driver:
     # -- one batch --------------------------------------------------------------
     def finish(self, hb, handle, last_batch):
         t0 = time.perf_counter()
-        ss, ds, rstat = self.backend.result(handle)
+        res = self.backend.result(handle)
         t1 = time.perf_counter()
         F = hb.n_fam
-        fail_f, kind, which = native_io.first_failure(hb, ss, ds, F, rstat)
-        self._prints(hb, fail_f, kind, which, last_batch)
-        self.cons.write_consensus(hb, ss, ds, fail_f)
         st = self.stats
+        if getattr(self.backend, "device_writer", False):
+            # records formatted and compressed on the device (dcr_submit_write)
+            nz = np.flatnonzero(res.fam_fail)
+            fail_f = int(nz[0]) if len(nz) else F
+            kind, which = None, -1
+            if fail_f < F:
+                code = int(res.fam_fail[fail_f])
+                kind, which = native_io.FAIL_NAMES.get(code & 0xff), code >> 8
+            self._prints(hb, fail_f, kind, which, last_batch)
+            if fail_f == F:
+                self.cons.put_blocks(res.bgzf, res.record_bytes)
+            elif fail_f:
+                self.cons.write(res.record_bytes_of(fail_f))
+            lens = res.ds_len[:2 * fail_f]
+        else:
+            ss, ds, rstat = res
+            fail_f, kind, which = native_io.first_failure(hb, ss, ds, F, rstat)
+            self._prints(hb, fail_f, kind, which, last_batch)
+            self.cons.write_consensus(hb, ss, ds, fail_f)
+            lens = np.ctypeslib.as_array(ctypes.cast(ds.len, ctypes.POINTER(ctypes.c_int32)), (2 * F,))[:2 * fail_f] \
+                if F else np.zeros(0, np.int32)
         st["batches"] += 1
         st["consensus_records"] += 2 * fail_f
-        if fail_f:
-            st["consensus_bases"] += int(np.ctypeslib.as_array(ctypes.cast(ds.len, ctypes.POINTER(ctypes.c_int32)),
-                                                              (2 * fail_f,)).sum())
+        st["consensus_bases"] += int(lens.sum())
         st["wait_s"] += t1 - t0
         if fail_f < F:
             t = int(np.nonzero(hb.a["tab_proc"][:hb.s.n_tab] == fail_f)[0][0])

@@ -14,6 +14,9 @@
 #include <string>
 
 #include "dcr_internal.h"
+#include "dcr_deflate.h"
+#include "dcr_writer.h"
+#include <hipcub/hipcub.hpp>
 
 namespace {
 thread_local std::string g_err;
@@ -65,6 +68,11 @@ struct dcr_ctx {
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
     struct Slot {
         DevBuf buf;
+        DevBuf wbuf;              // device record writer: metadata, record stream, BGZF blocks
+        int64_t *d_rec_off = nullptr, *d_comp_n = nullptr;
+        uint8_t *d_stream = nullptr, *d_comp = nullptr;
+        int64_t n_fam = 0;
+        bool writer = false;
         hipEvent_t ev_h2d = nullptr, ev_comp = nullptr, ev_d2h = nullptr;
         int *h_err = nullptr;     // pinned copy of the batch's capacity flag
         bool busy = false;
@@ -81,6 +89,7 @@ struct dcr_ctx {
     uint16_t *d_llr16 = nullptr;   // device [128]
     uint32_t *d_wtab = nullptr;    // device [DCR_LUT_N] (general kernel's decision pass)
     int n_cu = 256;     // compute units (persistent grid size)
+    int dfl_blocks = 1; // resident k_deflate workgroups per CU (dynamic LDS = sizeof(dfl::Shared))
     int fast_blocks[4] = {1, 1, 1, 1};   // resident k_consensus_fast blocks per CU (ss, ds; exact ss, exact ds)
 };
 
@@ -228,6 +237,12 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->fast_blocks[k], fk[k], dcr::kFastBlock, 0) != hipSuccess ||
             c->fast_blocks[k] < 1)
             c->fast_blocks[k] = 1;
+    if (hipFuncSetAttribute((const void *)dcrw::k_deflate, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(dfl::Shared)) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->dfl_blocks, dcrw::k_deflate, dfl::kT, sizeof(dfl::Shared)) !=
+            hipSuccess ||
+        c->dfl_blocks < 1)
+        c->dfl_blocks = 1;
     c->host_params = *params;
     if (hipMemcpy(c->d_params, params, sizeof(dcr_params), hipMemcpyHostToDevice) != hipSuccess ||
         upload_fast(c, params) != DCR_OK) {
@@ -247,6 +262,7 @@ void dcr_destroy(dcr_ctx *c) {
     for (auto &S : c->slots) {
         if (S.ev_d2h) (void)hipEventSynchronize(S.ev_d2h);
         S.buf.release();
+        S.wbuf.release();
         if (S.ev_h2d) (void)hipEventDestroy(S.ev_h2d);
         if (S.ev_comp) (void)hipEventDestroy(S.ev_comp);
         if (S.ev_d2h) (void)hipEventDestroy(S.ev_d2h);
@@ -666,6 +682,7 @@ int dcr_submit(dcr_ctx *c, int slot, const dcr_batch *h, dcr_out *hss, dcr_out *
     HIP_TRY(download_outputs(&dout[0], hss, 4 * (int64_t)h->n_fam, h->ss_cols, c->s_d2h));
     HIP_TRY(download_outputs(&dout[1], hds, 2 * (int64_t)h->n_fam, h->ds_cols, c->s_d2h));
     HIP_TRY(hipEventRecord(S.ev_d2h, c->s_d2h));
+    S.writer = false;
     S.busy = true;
     return DCR_OK;
 }
@@ -678,6 +695,188 @@ int dcr_wait(dcr_ctx *c, int slot) {
     HIP_TRY(hipEventSynchronize(S.ev_d2h));
     S.busy = false;
     if (*S.h_err) return fail(DCR_ECAPACITY, "a consensus needed more columns than its output region");
+    return DCR_OK;
+}
+
+
+// ---- device record writer ----------------------------------------------------
+
+// Upper bound of the formatted duplex records of a batch (dcr_writer.hip
+// rec_size): regions bound lengths, CIGARs and depth lists.
+static int64_t stream_bound(const dcr_batch *h, const dcr_wmeta *m) {
+    int64_t B = 0;
+    for (int32_t f = 0; f < h->n_fam; ++f) {
+        const int64_t lc = (int64_t)std::strlen(m->names + m->fam_code[f]);
+        for (int j = 0; j < 2; ++j) {
+            const int a = 4 * f + 2 * j, b = a + 1;
+            const int64_t Td = h->ds_col_off[2 * f + j + 1] - h->ds_col_off[2 * f + j];
+            const int64_t Ta = h->ss_col_off[a + 1] - h->ss_col_off[a];
+            const int64_t Tb = h->ss_col_off[b + 1] - h->ss_col_off[b];
+            const int64_t lr = (int64_t)std::strlen(m->names + m->fam_rx[2 * f + j]);
+            B += 400 + 2 * lc + lr + 20 * Td + 16 * (Ta + Tb) + (h->sub_off[a + 1] - h->sub_off[a]) +
+                 (h->sub_off[b + 1] - h->sub_off[b]);
+        }
+    }
+    return B;
+}
+
+int dcr_submit_write(dcr_ctx *c, int slot, const dcr_batch *h, const dcr_wmeta *m, dcr_wres *res) {
+    if (!c || !h || !m || !res) return fail(DCR_EARG, "NULL argument");
+    if (slot < 0 || slot >= DCR_MAX_SLOTS) return fail(DCR_EARG, "slot out of range");
+    HIP_TRY(hipSetDevice(c->device));
+    if (!c->s_h2d) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->s_h2d, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&c->s_d2h, hipStreamNonBlocking));
+    }
+    dcr_ctx::Slot &S = c->slots[slot];
+    if (!S.ev_h2d) {
+        HIP_TRY(hipEventCreateWithFlags(&S.ev_h2d, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&S.ev_comp, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&S.ev_d2h, hipEventDisableTiming));
+        HIP_TRY(hipHostMalloc((void **)&S.h_err, sizeof(int), hipHostMallocDefault));
+        *S.h_err = 0;
+    }
+    if (S.busy) return fail(DCR_EARG, "slot still in flight (dcr_wait it first)");
+    const int64_t F = h->n_fam;
+    // consensus buffers
+    const size_t need = plan_io(h, nullptr, nullptr, nullptr);
+    if (need > S.buf.cap) HIP_TRY(S.buf.ensure(need + need / 8));
+    dcr_batch db;
+    dcr_out dout[2];
+    plan_io(h, (char *)S.buf.p, &db, dout);
+    // writer buffers
+    const int64_t B = stream_bound(h, m);
+    const int64_t nbm = B / (int64_t)dfl::kMaxIn + 2;
+    size_t scan1 = 0, scan2 = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan1, (const int64_t *)nullptr, (int64_t *)nullptr,
+                                             (int)(2 * F + 1)));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan2, (const int64_t *)nullptr, (int64_t *)nullptr,
+                                             (int)(nbm + 1)));
+    size_t wo = 0;
+    auto take = [&](size_t bytes) { size_t o = wo; wo = align_up(wo + std::max<size_t>(bytes, 1)); return o; };
+    const size_t o_names = take((size_t)m->n_names + 1);
+    const size_t o_code = take(8 * (size_t)F), o_rx = take(16 * (size_t)F), o_tid = take(4 * (size_t)F);
+    const size_t o_fail = take(4 * (size_t)F), o_dlen = take(8 * (size_t)F);
+    const size_t o_rsz = take(8 * (size_t)(2 * F + 1)), o_roff = take(8 * (size_t)(2 * F + 1));
+    const size_t o_scan = take(std::max(scan1, scan2));
+    const size_t o_stream = take((size_t)B);
+    const size_t o_slots = take((size_t)nbm * dfl::kSlot);
+    const size_t o_bsz = take(8 * (size_t)(nbm + 1)), o_boff = take(8 * (size_t)(nbm + 1));
+    const size_t o_comp = take((size_t)nbm * dfl::kSlot);
+    const size_t o_tot = take(8 * 4);
+    if (wo > S.wbuf.cap) HIP_TRY(S.wbuf.ensure(wo + wo / 8));
+    char *wb = (char *)S.wbuf.p;
+    // H2D: inputs and writer metadata on the copy stream
+    HIP_TRY(upload_inputs(h, db, c->s_h2d));
+    if (m->n_names) HIP_TRY(hipMemcpyAsync(wb + o_names, m->names, (size_t)m->n_names, hipMemcpyHostToDevice, c->s_h2d));
+    if (F) {
+        HIP_TRY(hipMemcpyAsync(wb + o_code, m->fam_code, 8 * (size_t)F, hipMemcpyHostToDevice, c->s_h2d));
+        HIP_TRY(hipMemcpyAsync(wb + o_rx, m->fam_rx, 16 * (size_t)F, hipMemcpyHostToDevice, c->s_h2d));
+        HIP_TRY(hipMemcpyAsync(wb + o_tid, m->fam_tid, 4 * (size_t)F, hipMemcpyHostToDevice, c->s_h2d));
+    }
+    HIP_TRY(hipEventRecord(S.ev_h2d, c->s_h2d));
+    // consensus kernels on the compute stream
+    HIP_TRY(hipStreamWaitEvent(c->stream, S.ev_h2d, 0));
+    int rc = dcr_run_batch(c, &db, &dout[0], &dout[1]);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(S.h_err, c->w.err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    // record writer
+    dcrw::FmtArgs A{};
+    A.ss = dout[0];
+    A.ds = dout[1];
+    A.sub_off = db.sub_off;
+    A.read_mapq = db.read_mapq;
+    A.ss_col_off = db.ss_col_off;
+    A.ds_col_off = db.ds_col_off;
+    A.info = c->w.info;
+    A.names = wb + o_names;
+    A.fam_code = (const int64_t *)(wb + o_code);
+    A.fam_rx = (const int64_t *)(wb + o_rx);
+    A.fam_tid = (const int32_t *)(wb + o_tid);
+    A.n_fam = (int32_t)F;
+    A.fam_fail = (int32_t *)(wb + o_fail);
+    A.ds_len_out = (int32_t *)(wb + o_dlen);
+    int64_t *rsz = (int64_t *)(wb + o_rsz);
+    A.rec_size = rsz;
+    A.rec_off = (int64_t *)(wb + o_roff);
+    A.stream = (uint8_t *)(wb + o_stream);
+    HIP_TRY(hipMemsetAsync(rsz, 0, 8 * (size_t)(2 * F + 1), c->stream));
+    HIP_TRY(hipMemsetAsync(wb + o_bsz, 0, 8 * (size_t)(nbm + 1), c->stream));
+    if (F) {
+        hipLaunchKernelGGL(dcrw::k_famfail, dim3((unsigned)((F + 255) / 256)), dim3(256), 0, c->stream, A);
+        const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((2 * F + 3) / 4, (int64_t)c->n_cu * 8));
+        hipLaunchKernelGGL(dcrw::k_fmt_size, dim3(g), dim3(256), 0, c->stream, A);
+        HIP_TRY(hipGetLastError());
+        size_t tb = std::max(scan1, scan2);
+        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(wb + o_scan, tb, rsz, A.rec_off, (int)(2 * F + 1), c->stream));
+        hipLaunchKernelGGL(dcrw::k_fmt_write, dim3(g), dim3(256), 0, c->stream, A);
+        HIP_TRY(hipGetLastError());
+    } else {
+        HIP_TRY(hipMemsetAsync(A.rec_off, 0, 8, c->stream));
+    }
+    int64_t *bsz = (int64_t *)(wb + o_bsz);
+    dcrw::DflArgs D{A.stream, A.rec_off + 2 * F, (uint8_t *)(wb + o_slots), bsz};
+    const unsigned gd = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nbm, (int64_t)c->n_cu * c->dfl_blocks));
+    hipLaunchKernelGGL(dcrw::k_deflate, dim3(gd), dim3(dfl::kT), sizeof(dfl::Shared), c->stream, D);
+    HIP_TRY(hipGetLastError());
+    size_t tb = std::max(scan1, scan2);
+    int64_t *boff = (int64_t *)(wb + o_boff);
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(wb + o_scan, tb, bsz, boff, (int)(nbm + 1), c->stream));
+    dcrw::CompactArgs C{(const uint8_t *)(wb + o_slots), bsz, boff, A.rec_off + 2 * F,
+                        (uint8_t *)(wb + o_comp), (int64_t *)(wb + o_tot)};
+    hipLaunchKernelGGL(dcrw::k_compact, dim3(gd), dim3(256), 0, c->stream, C);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(S.ev_comp, c->stream));
+    // D2H of the per-family outcome and the totals on the second copy stream
+    HIP_TRY(hipStreamWaitEvent(c->s_d2h, S.ev_comp, 0));
+    if (F) {
+        HIP_TRY(hipMemcpyAsync(res->fam_fail, A.fam_fail, 4 * (size_t)F, hipMemcpyDeviceToHost, c->s_d2h));
+        HIP_TRY(hipMemcpyAsync(res->ds_len, A.ds_len_out, 8 * (size_t)F, hipMemcpyDeviceToHost, c->s_d2h));
+    }
+    HIP_TRY(hipMemcpyAsync(res->totals, wb + o_tot, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, c->s_d2h));
+    HIP_TRY(hipEventRecord(S.ev_d2h, c->s_d2h));
+    S.d_rec_off = A.rec_off;
+    S.d_stream = A.stream;
+    S.d_comp = (uint8_t *)(wb + o_comp);
+    S.n_fam = F;
+    S.writer = true;
+    S.busy = true;
+    return DCR_OK;
+}
+
+int dcr_wait_write(dcr_ctx *c, int slot, dcr_wres *res) {
+    if (!c || !res || slot < 0 || slot >= DCR_MAX_SLOTS) return fail(DCR_EARG, "bad argument");
+    dcr_ctx::Slot &S = c->slots[slot];
+    if (!S.busy || !S.writer) return fail(DCR_EARG, "slot has no writer batch in flight");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipEventSynchronize(S.ev_d2h));
+    S.busy = false;
+    if (*S.h_err) return fail(DCR_ECAPACITY, "a consensus needed more columns than its output region");
+    const int64_t n = res->totals[0];
+    if (n > res->cap_bgzf) return fail(DCR_ECAPACITY, "BGZF output larger than cap_bgzf (see totals[0])");
+    if (n > 0) {
+        HIP_TRY(hipMemcpyAsync(res->bgzf, S.d_comp, (size_t)n, hipMemcpyDeviceToHost, c->s_d2h));
+        HIP_TRY(hipStreamSynchronize(c->s_d2h));
+    }
+    return DCR_OK;
+}
+
+int dcr_slot_fetch(dcr_ctx *c, int slot, int what, int64_t off, int64_t n, void *dst) {
+    if (!c || !dst || slot < 0 || slot >= DCR_MAX_SLOTS || off < 0 || n < 0) return fail(DCR_EARG, "bad argument");
+    dcr_ctx::Slot &S = c->slots[slot];
+    if (!S.writer) return fail(DCR_EARG, "slot holds no writer batch");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipEventSynchronize(S.ev_d2h));
+    if (what == 0) {
+        if (n) HIP_TRY(hipMemcpy(dst, S.d_stream + off, (size_t)n, hipMemcpyDeviceToHost));
+    } else if (what == 1) {
+        if (off + n > 2 * S.n_fam + 1) return fail(DCR_EARG, "record offsets out of range");
+        if (n) HIP_TRY(hipMemcpy(dst, S.d_rec_off + off, 8 * (size_t)n, hipMemcpyDeviceToHost));
+    } else if (what == 2) {
+        if (n) HIP_TRY(hipMemcpy(dst, S.d_comp + off, (size_t)n, hipMemcpyDeviceToHost));
+    } else {
+        return fail(DCR_EARG, "what must be 0 (record bytes), 1 (record offsets) or 2 (BGZF blocks)");
+    }
     return DCR_OK;
 }
 

@@ -1,0 +1,563 @@
+// dcr_deflate.h — BGZF block compressor for gfx950: one 256-lane workgroup
+// per block of <= 0xff00 input bytes, producing one RFC 1951 dynamic-Huffman
+// block (or a stored block when that is smaller) inside an RFC 1952 member
+// with the BGZF "BC" extra field (SAM spec v1.6 §4.1), CRC32 and ISIZE.
+//
+// The same phase functions run as the device kernel (dcr_writer.hip, one
+// lane per thread, barriers between phases) and as a sequential lane-by-lane
+// emulation on the host (dcr_deflate_emulate in libdcr_io.so), so the CPU
+// tests can check the GPU's algorithm against zlib / libdeflate inflate.
+//
+// Algorithm (per block):
+//   P0  stage the block in LDS, clear the tables / histograms
+//   P1  hash every 4-byte position: earliest position per hash in each 32 KiB
+//       half and latest in the first half (LDS atomics)
+//   P2  each lane greedily parses its contiguous sub-block (256 sub-blocks per
+//       block; matches end at the sub-block end) against those candidates and
+//       distances 1..4, counting literal/length and distance symbols
+//   P3  thread 0: Huffman code lengths (in-place minimum-redundancy code of
+//       Moffat & Katajainen, lengths limited to 15 / 7), canonical codes, the
+//       run-length-coded header; every lane: the CRC32 of its sub-block
+//   P4  each lane parses again and counts its bits; exclusive scan
+//   P5  each lane parses a third time and writes its bits (word atomics on
+//       the zeroed output slot); thread 0 writes header, EOB, BGZF framing
+// The parse is deterministic, so the three passes see the same tokens.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#if defined(__HIPCC__)
+#define DFL_HD __host__ __device__
+#else
+#define DFL_HD
+#endif
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DFL_DEVICE 1
+#else
+#define DFL_DEVICE 0
+#endif
+
+namespace dfl {
+
+constexpr int kT = 256;                   // lanes per block
+constexpr uint32_t kMaxIn = 0xff00;       // input bytes per BGZF block
+constexpr int kHB = 11;
+constexpr int kHN = 1 << kHB;
+constexpr uint32_t kNone = 0xffffffffu;
+constexpr uint32_t kSlot = 65536;         // output slot bytes (one BGZF block at most)
+constexpr uint32_t kMaxDeflate = kSlot - 26;
+constexpr int kLS = 32;                   // lane-private recency table: sets x 2 ways
+
+struct Shared {
+    uint8_t in[kMaxIn + 16];
+    uint32_t a_min[kHN], a_max[kHN], b_min[kHN];   // positions (a_max: position + 1, 0 none)
+    uint16_t lt[kT][2 * kLS];             // per lane: latest positions + 1 per hash set (2 ways)
+    uint32_t lit_freq[288], dist_freq[32];
+    uint8_t lit_len[288], dist_len[32], cl_len[19];
+    uint16_t lit_code[288], dist_code[32], cl_code[19];   // bit-reversed (LSB-first) codes
+    uint32_t lane_bits[kT];
+    uint32_t lane_off[kT];
+    uint32_t lane_crc[kT];
+    uint32_t extra_bits;                  // extra bits of all matches (pass P2)
+    uint32_t sort_a[320];                 // (freq << 9 | symbol) then in-place code lengths
+    uint16_t rle[320];                    // header: code-length symbol | extra << 8
+    uint32_t n_rle;
+    uint32_t hlit, hdist, hclen;
+    uint32_t hdr_bits, body_bits;
+    uint32_t stored;
+    uint32_t crc;
+};
+
+// ---- tables -------------------------------------------------------------
+#if DFL_DEVICE
+#define DFL_CONST __constant__
+#else
+#define DFL_CONST static const
+#endif
+DFL_CONST uint16_t kLenBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59, 67, 83, 99,
+                                   115, 131, 163, 195, 227, 258};
+DFL_CONST uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+DFL_CONST uint16_t kDistBase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769,
+                                    1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+DFL_CONST uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12,
+                                    12, 13, 13};
+DFL_CONST uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// ---- atomics (host emulation: plain operations) -------------------------------
+DFL_HD inline void amin(uint32_t *a, uint32_t v) {
+#if DFL_DEVICE
+    atomicMin(a, v);
+#else
+    if (v < *a) *a = v;
+#endif
+}
+DFL_HD inline void amax(uint32_t *a, uint32_t v) {
+#if DFL_DEVICE
+    atomicMax(a, v);
+#else
+    if (v > *a) *a = v;
+#endif
+}
+DFL_HD inline void aadd(uint32_t *a, uint32_t v) {
+#if DFL_DEVICE
+    atomicAdd(a, v);
+#else
+    *a += v;
+#endif
+}
+DFL_HD inline void aor(uint32_t *a, uint32_t v) {
+#if DFL_DEVICE
+    atomicOr(a, v);
+#else
+    *a |= v;
+#endif
+}
+
+// ---- CRC32 (reflected, 0xEDB88320), zlib's multmodp / x2nmodp ----------------
+DFL_HD inline uint32_t crc_byte(uint32_t c) {
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+    return c;
+}
+DFL_HD inline uint32_t multmodp(uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
+        }
+        m >>= 1;
+        b = (b & 1) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+    }
+    return p;
+}
+// x^(n * 2^3) mod P: the register shift of n zero bytes
+DFL_HD inline uint32_t x8nmodp(uint32_t n) {
+    // x^(2^k) mod P for k = 3.. computed by squaring (k starts at 3: one byte)
+    uint32_t sq = 1u << 23;        // x^8  (x^(2^3)) in the reflected representation
+    uint32_t p = 1u << 31;         // 1
+    while (n) {
+        if (n & 1) p = multmodp(sq, p);
+        n >>= 1;
+        sq = multmodp(sq, sq);
+    }
+    return p;
+}
+
+// ---- input access -------------------------------------------------------------
+DFL_HD inline uint32_t ld32(const Shared &s, uint32_t p) {
+    return (uint32_t)s.in[p] | ((uint32_t)s.in[p + 1] << 8) | ((uint32_t)s.in[p + 2] << 16) |
+           ((uint32_t)s.in[p + 3] << 24);
+}
+DFL_HD inline uint32_t hash4(uint32_t v) { return (v * 0x9E3779B1u) >> (32 - kHB); }
+
+DFL_HD inline void lane_range(uint32_t n, int lane, uint32_t &lo, uint32_t &hi) {
+    const uint32_t S = (n + kT - 1) / kT;
+    lo = (uint32_t)lane * S;
+    if (lo > n) lo = n;
+    hi = lo + S;
+    if (hi > n) hi = n;
+}
+
+DFL_HD inline uint32_t match_len(const Shared &s, uint32_t c, uint32_t p, uint32_t lim) {
+    uint32_t l = 0;
+    while (l + 4 <= lim && ld32(s, c + l) == ld32(s, p + l)) l += 4;
+    while (l < lim && s.in[c + l] == s.in[p + l]) ++l;
+    return l;
+}
+
+DFL_HD inline int len_sym(uint32_t len) {   // 0..28 (symbol 257 + i)
+    int lo = 0, hi = 28;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (kLenBase[mid] <= len) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+DFL_HD inline int dist_sym(uint32_t d) {    // 0..29
+    int lo = 0, hi = 29;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (kDistBase[mid] <= d) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// lane-private recency table (deterministic: one lane, positions in order)
+DFL_HD inline void lt_insert(uint16_t *t, uint32_t h, uint32_t p) {
+    const uint32_t set = (h & (kLS - 1)) * 2;
+    t[set + 1] = t[set];
+    t[set] = (uint16_t)(p + 1);
+}
+
+// greedy parse of [lo, hi): v.lit(byte) / v.match(len, dist).  Candidates:
+// the lane's two latest positions with the same hash set (its table holds
+// the previous sub-block and its own positions so far), the earliest /
+// latest block positions with the same hash (P1), and distances 1..4.
+template <class V>
+DFL_HD inline void parse(Shared &s, uint32_t n, int lane, uint32_t lo, uint32_t hi, V &v) {
+    uint16_t *t = s.lt[lane];
+    for (int i = 0; i < 2 * kLS; ++i) t[i] = 0;
+    const uint32_t S = hi - lo;
+    for (uint32_t q = lo >= S ? lo - S : 0; q < lo; ++q)
+        if (q + 4 <= n) lt_insert(t, hash4(ld32(s, q)), q);
+    uint32_t p = lo;
+    while (p < hi) {
+        uint32_t best = 0, bd = 0;
+        const uint32_t lim = (hi - p) < 258 ? (hi - p) : 258;
+        uint32_t h = 0;
+        const bool hashed = p + 4 <= n;
+        if (hashed) h = hash4(ld32(s, p));
+        if (lim >= 4) {
+            uint32_t cand[8];
+            int nc = 0;
+            const uint32_t set = (h & (kLS - 1)) * 2;
+            cand[nc++] = t[set] ? (uint32_t)t[set] - 1 : kNone;
+            cand[nc++] = t[set + 1] ? (uint32_t)t[set + 1] - 1 : kNone;
+            if (p >= 32768) {
+                cand[nc++] = s.b_min[h];
+                const uint32_t am = s.a_max[h];
+                cand[nc++] = am ? am - 1 : kNone;
+            } else {
+                cand[nc++] = s.a_min[h];
+            }
+            for (uint32_t d = 1; d <= 4; ++d) cand[nc++] = p >= d ? p - d : kNone;
+            for (int i = 0; i < nc; ++i) {
+                const uint32_t c = cand[i];
+                if (c == kNone || c >= p || p - c > 32768) continue;
+                const uint32_t l = match_len(s, c, p, lim);
+                if (l > best) { best = l; bd = p - c; }
+            }
+        }
+        if (hashed) lt_insert(t, h, p);
+        if (best >= 4) {
+            v.match(best, bd);
+            for (uint32_t q = p + 1; q < p + best; ++q)
+                if (q + 4 <= n) lt_insert(t, hash4(ld32(s, q)), q);
+            p += best;
+        } else {
+            v.lit(s.in[p]);
+            ++p;
+        }
+    }
+}
+
+struct CountV {            // P2: symbol histogram, extra bits
+    Shared &s;
+    uint32_t extra = 0;
+    DFL_HD void lit(uint8_t b) { aadd(&s.lit_freq[b], 1); }
+    DFL_HD void match(uint32_t len, uint32_t d) {
+        const int ls = len_sym(len), ds = dist_sym(d);
+        aadd(&s.lit_freq[257 + ls], 1);
+        aadd(&s.dist_freq[ds], 1);
+        extra += kLenExtra[ls] + kDistExtra[ds];
+    }
+};
+
+struct BitsV {             // P4: bits of a lane's tokens
+    const Shared &s;
+    uint32_t bits = 0;
+    DFL_HD void lit(uint8_t b) { bits += s.lit_len[b]; }
+    DFL_HD void match(uint32_t len, uint32_t d) {
+        const int ls = len_sym(len), ds = dist_sym(d);
+        bits += s.lit_len[257 + ls] + kLenExtra[ls] + s.dist_len[ds] + kDistExtra[ds];
+    }
+};
+
+// LSB-first bit writer over a zeroed word array; words that may be shared
+// with a neighbour are or-ed atomically
+struct BitOut {
+    uint32_t *w;
+    uint64_t acc = 0;
+    uint32_t nacc = 0;      // bits in acc
+    uint32_t word;          // index of acc's first word
+    DFL_HD BitOut(uint32_t *words, uint32_t bitpos) : w(words), word(bitpos >> 5) { nacc = bitpos & 31; }
+    DFL_HD void put(uint32_t v, uint32_t nb) {
+        if (!nb) return;
+        acc |= (uint64_t)v << nacc;
+        nacc += nb;
+        if (nacc >= 32) {
+            aor(&w[word], (uint32_t)acc);
+            ++word;
+            acc >>= 32;
+            nacc -= 32;
+        }
+    }
+    DFL_HD void flush() {
+        if (nacc) aor(&w[word], (uint32_t)acc);
+        acc = 0;
+        nacc = 0;
+    }
+};
+
+struct EmitV {             // P5: write a lane's tokens
+    const Shared &s;
+    BitOut &o;
+    DFL_HD void lit(uint8_t b) { o.put(s.lit_code[b], s.lit_len[b]); }
+    DFL_HD void match(uint32_t len, uint32_t d) {
+        const int ls = len_sym(len), ds = dist_sym(d);
+        o.put(s.lit_code[257 + ls], s.lit_len[257 + ls]);
+        o.put(len - kLenBase[ls], kLenExtra[ls]);
+        o.put(s.dist_code[ds], s.dist_len[ds]);
+        o.put(d - kDistBase[ds], kDistExtra[ds]);
+    }
+};
+
+// ---- Huffman code lengths (thread 0) ----------------------------------------------
+// In-place minimum-redundancy code lengths (Moffat & Katajainen 1995) over
+// a[0..m) = frequencies sorted ascending; on return a[i] is the code length
+// of the i-th symbol (non-increasing in i).
+DFL_HD inline void mr_lengths(uint32_t *a, int m) {
+    if (m == 1) { a[0] = 1; return; }
+    // phase 1: internal-node weights and parent pointers
+    a[0] += a[1];
+    int root = 0, leaf = 2;
+    for (int next = 1; next < m - 1; ++next) {
+        if (leaf >= m || a[root] < a[leaf]) { a[next] = a[root]; a[root++] = (uint32_t)next; }
+        else a[next] = a[leaf++];
+        if (leaf >= m || (root < next && a[root] < a[leaf])) { a[next] += a[root]; a[root++] = (uint32_t)next; }
+        else a[next] += a[leaf++];
+    }
+    // phase 2: internal-node depths
+    a[m - 2] = 0;
+    for (int next = m - 3; next >= 0; --next) a[next] = a[a[next]] + 1;
+    // phase 3: leaf depths
+    int avail = 1, used = 0, depth = 0;
+    root = m - 2;
+    int next = m - 1;
+    while (avail > 0) {
+        while (root >= 0 && (int)a[root] == depth) { ++used; --root; }
+        while (avail > used) { a[next--] = (uint32_t)depth; --avail; }
+        avail = 2 * used;
+        ++depth;
+        used = 0;
+    }
+}
+
+// Code lengths <= max_len for freq[0..n) into len[0..n); scratch holds >= n words.
+// At least `min_used` symbols get a code (padding with the lowest symbols).
+DFL_HD inline void build_lengths(const uint32_t *freq, int n, int max_len, uint8_t *len, uint32_t *scratch,
+                                 int min_used) {
+    int m = 0;
+    for (int i = 0; i < n; ++i) {
+        len[i] = 0;
+        if (freq[i]) scratch[m++] = (freq[i] << 9) | (uint32_t)i;
+    }
+    for (int i = 0; i < n && m < min_used; ++i)
+        if (!freq[i]) scratch[m++] = (0u << 9) | (uint32_t)i;
+    if (m == 0) return;
+    if (m == 1) {                          // one code of length 1 (inflate accepts it)
+        len[scratch[0] & 511] = 1;
+        return;
+    }
+    // insertion sort by (freq, symbol) ascending (m <= 288)
+    for (int i = 1; i < m; ++i) {
+        const uint32_t v = scratch[i];
+        int j = i - 1;
+        while (j >= 0 && scratch[j] > v) { scratch[j + 1] = scratch[j]; --j; }
+        scratch[j + 1] = v;
+    }
+    uint16_t sym[288];
+    uint32_t f[288];
+    for (int i = 0; i < m; ++i) {
+        sym[i] = (uint16_t)(scratch[i] & 511);
+        const uint32_t fr = scratch[i] >> 9;
+        f[i] = fr ? fr : 1;               // padded (unused) symbols weigh 1
+    }
+    mr_lengths(f, m);
+    // limit to max_len: count per length, move overflow to max_len, restore the Kraft sum
+    uint32_t num[33] = {0};
+    for (int i = 0; i < m; ++i) num[f[i] > 32 ? 32 : f[i]]++;
+    for (int i = max_len + 1; i <= 32; ++i) { num[max_len] += num[i]; num[i] = 0; }
+    uint32_t total = 0;
+    for (int i = max_len; i > 0; --i) total += num[i] << (max_len - i);
+    while (total != (1u << max_len)) {
+        num[max_len]--;
+        for (int i = max_len - 1; i > 0; --i)
+            if (num[i]) { num[i]--; num[i + 1] += 2; break; }
+        total--;
+    }
+    // the rarest symbols take the longest codes
+    int k = 0;
+    for (int l = max_len; l >= 1; --l)
+        for (uint32_t c = 0; c < num[l]; ++c) len[sym[k++]] = (uint8_t)l;
+}
+
+DFL_HD inline uint32_t reverse_bits(uint32_t v, int nb) {
+    uint32_t r = 0;
+    for (int i = 0; i < nb; ++i) { r = (r << 1) | (v & 1); v >>= 1; }
+    return r;
+}
+
+DFL_HD inline void canonical(const uint8_t *len, int n, uint16_t *code) {
+    uint32_t cnt[16] = {0}, next[16] = {0};
+    for (int i = 0; i < n; ++i) cnt[len[i]]++;
+    cnt[0] = 0;
+    uint32_t c = 0;
+    for (int l = 1; l < 16; ++l) { c = (c + cnt[l - 1]) << 1; next[l] = c; }
+    for (int i = 0; i < n; ++i)
+        code[i] = len[i] ? (uint16_t)reverse_bits(next[len[i]]++, len[i]) : 0;
+}
+
+// P3 on thread 0: code lengths, codes, header; returns header bits
+DFL_HD inline void build_codes(Shared &s) {
+    s.lit_freq[256] = 1;                                   // end of block
+    build_lengths(s.lit_freq, 286, 15, s.lit_len, s.sort_a, 2);
+    build_lengths(s.dist_freq, 30, 15, s.dist_len, s.sort_a, 1);
+    s.lit_len[286] = s.lit_len[287] = 0;
+    s.dist_len[30] = s.dist_len[31] = 0;
+    canonical(s.lit_len, 286, s.lit_code);
+    canonical(s.dist_len, 30, s.dist_code);
+    int nlit = 286;
+    while (nlit > 257 && !s.lit_len[nlit - 1]) --nlit;
+    int ndist = 30;
+    while (ndist > 1 && !s.dist_len[ndist - 1]) --ndist;
+    s.hlit = (uint32_t)(nlit - 257);
+    s.hdist = (uint32_t)(ndist - 1);
+    // run-length code the lengths (symbols 16 / 17 / 18)
+    uint8_t L[320];
+    const int N = nlit + ndist;
+    for (int i = 0; i < nlit; ++i) L[i] = s.lit_len[i];
+    for (int i = 0; i < ndist; ++i) L[nlit + i] = s.dist_len[i];
+    uint32_t clf[19] = {0};
+    uint32_t nr = 0;
+    for (int i = 0; i < N;) {
+        const uint8_t v = L[i];
+        int run = 1;
+        while (i + run < N && L[i + run] == v) ++run;
+        i += run;
+        if (v == 0) {
+            while (run >= 11) { const int r = run < 138 ? run : 138; s.rle[nr++] = (uint16_t)(18 | ((r - 11) << 8)); clf[18]++; run -= r; }
+            if (run >= 3) { s.rle[nr++] = (uint16_t)(17 | ((run - 3) << 8)); clf[17]++; run = 0; }
+            while (run-- > 0) { s.rle[nr++] = 0; clf[0]++; }
+        } else {
+            s.rle[nr++] = v; clf[v]++; --run;
+            while (run >= 3) { const int r = run < 6 ? run : 6; s.rle[nr++] = (uint16_t)(16 | ((r - 3) << 8)); clf[16]++; run -= r; }
+            while (run-- > 0) { s.rle[nr++] = v; clf[v]++; }
+        }
+    }
+    s.n_rle = nr;
+    build_lengths(clf, 19, 7, s.cl_len, s.sort_a, 2);
+    canonical(s.cl_len, 19, s.cl_code);
+    int ncl = 19;
+    while (ncl > 4 && !s.cl_len[kClOrder[ncl - 1]]) --ncl;
+    s.hclen = (uint32_t)(ncl - 4);
+    uint32_t bits = 3 + 5 + 5 + 4 + 3 * (uint32_t)ncl;
+    for (uint32_t i = 0; i < nr; ++i) {
+        const uint32_t sym = s.rle[i] & 31;
+        bits += s.cl_len[sym] + (sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0);
+    }
+    s.hdr_bits = bits;
+}
+
+DFL_HD inline void write_header(const Shared &s, BitOut &o) {
+    o.put(1, 1);          // BFINAL
+    o.put(2, 2);          // BTYPE = 10 (dynamic Huffman)
+    o.put(s.hlit, 5);
+    o.put(s.hdist, 5);
+    o.put(s.hclen, 4);
+    for (uint32_t i = 0; i < s.hclen + 4; ++i) o.put(s.cl_len[kClOrder[i]], 3);
+    for (uint32_t i = 0; i < s.n_rle; ++i) {
+        const uint32_t sym = s.rle[i] & 31, ex = s.rle[i] >> 8;
+        o.put(s.cl_code[sym], s.cl_len[sym]);
+        if (sym == 16) o.put(ex, 2);
+        else if (sym == 17) o.put(ex, 3);
+        else if (sym == 18) o.put(ex, 7);
+    }
+}
+
+// or `nb` (<= 4) little-endian bytes of v at byte offset `at` of a zeroed word array
+DFL_HD inline void or_bytes(uint32_t *w, uint32_t at, uint32_t v, int nb) {
+    for (int i = 0; i < nb; ++i) {
+        const uint32_t b = (v >> (8 * i)) & 0xff, a = at + (uint32_t)i;
+        aor(&w[a >> 2], b << (8 * (a & 3)));
+    }
+}
+
+// ---- the phases (lane = thread index) -----------------------------------------
+DFL_HD inline void p0_clear(Shared &s, int lane) {
+    for (int i = lane; i < kHN; i += kT) { s.a_min[i] = kNone; s.b_min[i] = kNone; s.a_max[i] = 0; }
+    for (int i = lane; i < 288; i += kT) s.lit_freq[i] = 0;
+    if (lane < 32) s.dist_freq[lane] = 0;
+    if (lane == 0) s.extra_bits = 0;
+}
+DFL_HD inline void p1_hash(Shared &s, uint32_t n, int lane) {
+    uint32_t lo, hi;
+    lane_range(n, lane, lo, hi);
+    for (uint32_t p = lo; p < hi && p + 4 <= n; ++p) {
+        const uint32_t h = hash4(ld32(s, p));
+        if (p < 32768) { amin(&s.a_min[h], p); amax(&s.a_max[h], p + 1); }
+        else amin(&s.b_min[h], p);
+    }
+}
+DFL_HD inline void p2_count(Shared &s, uint32_t n, int lane) {
+    uint32_t lo, hi;
+    lane_range(n, lane, lo, hi);
+    CountV v{s};
+    parse(s, n, lane, lo, hi, v);
+    if (v.extra) aadd(&s.extra_bits, v.extra);
+    // CRC32 register of the sub-block (no init / final xor), shifted past the rest
+    uint32_t c = 0;
+    for (uint32_t p = lo; p < hi; ++p) c = crc_byte((c ^ s.in[p]) & 0xff) ^ (c >> 8);
+    s.lane_crc[lane] = (hi > lo) ? multmodp(x8nmodp(n - hi), c) : 0;
+}
+DFL_HD inline void p4_bits(Shared &s, uint32_t n, int lane) {
+    uint32_t lo, hi;
+    lane_range(n, lane, lo, hi);
+    BitsV v{s};
+    parse(s, n, lane, lo, hi, v);
+    s.lane_bits[lane] = v.bits;
+}
+// thread 0 between P4 and P5: offsets, stored decision, CRC
+DFL_HD inline void p4_scan(Shared &s, uint32_t n) {
+    uint32_t acc = 3 * 8 * 6 + s.hdr_bits;    // deflate data begins at byte 18 of the slot
+    for (int l = 0; l < kT; ++l) { s.lane_off[l] = acc; acc += s.lane_bits[l]; }
+    s.body_bits = acc - 144 + s.lit_len[256];
+    const uint32_t dbytes = (s.body_bits + 7) / 8;
+    s.stored = (dbytes > kMaxDeflate || dbytes > n + 5) ? 1u : 0u;
+    uint32_t c = multmodp(x8nmodp(n), 0xffffffffu);
+    for (int l = 0; l < kT; ++l) c ^= s.lane_crc[l];
+    s.crc = ~c;
+}
+DFL_HD inline void p5_emit(Shared &s, uint32_t n, int lane, uint32_t *out) {
+    if (s.stored) {
+        // stored block: BFINAL=1 BTYPE=00, LEN, NLEN, raw bytes (byte-aligned after the 3 bits)
+        uint32_t lo, hi;
+        lane_range(n, lane, lo, hi);
+        for (uint32_t p = lo; p < hi; ++p) or_bytes(out, 18 + 5 + p, s.in[p], 1);
+        return;
+    }
+    uint32_t lo, hi;
+    lane_range(n, lane, lo, hi);
+    BitOut o(out, s.lane_off[lane]);
+    EmitV v{s, o};
+    parse(s, n, lane, lo, hi, v);
+    if (lane == kT - 1) o.put(s.lit_code[256], s.lit_len[256]);
+    o.flush();
+}
+// thread 0 after P5: header bits and the BGZF framing
+DFL_HD inline uint32_t p6_frame(const Shared &s, uint32_t n, uint32_t *out) {
+    uint32_t dbytes;
+    if (s.stored) {
+        dbytes = 5 + n;
+        or_bytes(out, 18, 1, 1);
+        or_bytes(out, 19, n, 2);
+        or_bytes(out, 21, ~n & 0xffff, 2);
+    } else {
+        BitOut o(out, 144);
+        write_header(s, o);
+        o.flush();
+        dbytes = (s.body_bits + 7) / 8;
+    }
+    // 1f 8b 08 04 | mtime 0 | xfl 0 | os ff | xlen 6 | 'B' 'C' 2 0 | BSIZE
+    or_bytes(out, 0, 0x04088b1fu, 4);
+    or_bytes(out, 8, 0xff00u, 2);
+    or_bytes(out, 10, 6, 2);
+    or_bytes(out, 12, 0x00024342u, 4);
+    or_bytes(out, 16, dbytes + 25, 2);
+    or_bytes(out, 18 + dbytes, s.crc, 4);
+    or_bytes(out, 22 + dbytes, n, 4);
+    return dbytes + 26;
+}
+
+}  // namespace dfl

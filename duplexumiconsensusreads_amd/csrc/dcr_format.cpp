@@ -360,6 +360,20 @@ int dcr_bgzw_write(dcr_bgzw *w, const void *bytes, int64_t n) {
     return DCR_IO_OK;
 }
 
+int dcr_bgzw_put_blocks(dcr_bgzw *w, const void *blocks, int64_t n, int64_t raw_bytes) {
+    if (!w || n < 0 || (n > 0 && !blocks)) return fail(DCR_IO_EARG, "bad arguments");
+    if (w->bad) return fail(DCR_IO_EFILE, "writer failed earlier");
+    if (w->n_in) {                      // pending bytes first: blocks stay in order
+        if (!w->flush(w->n_in)) { w->bad = true; return DCR_IO_EFILE; }
+        w->n_in = 0;
+    }
+    if (n && !w->put_compressed((const uint8_t *)blocks, (size_t)n, (size_t)raw_bytes)) {
+        w->bad = true;
+        return DCR_IO_EFILE;
+    }
+    return DCR_IO_OK;
+}
+
 int dcr_bgzw_close(dcr_bgzw *w) {
     if (!w) return fail(DCR_IO_EARG, "NULL writer");
     int rc = DCR_IO_OK;
@@ -417,10 +431,7 @@ int dcr_fmt_write(dcr_bgzw *w, const dcr_host_batch *hb, const dcr_fmt_out *ss, 
                   int32_t n_fam) {
     if (!w || !hb || !ss || !ds || n_fam < 0 || n_fam > hb->n_fam) return fail(DCR_IO_EARG, "bad arguments");
     if (w->bad) return fail(DCR_IO_EFILE, "writer failed earlier");
-    // family code per processed family (from the family table)
-    std::vector<int64_t> code_of((size_t)n_fam, -1);
-    for (int32_t t = 0; t < hb->n_tab; ++t)
-        if (hb->tab_kind[t] == DCR_FAM_PROCESSED && hb->tab_proc[t] < n_fam) code_of[(size_t)hb->tab_proc[t]] = hb->tab_code[t];
+    const int64_t *code_of = hb->fam_code;
     const Ctx c{hb, ss, ds};
     // pending bytes first (blocks stay in order)
     if (w->n_in) {
@@ -443,7 +454,7 @@ int dcr_fmt_write(dcr_bgzw *w, const dcr_host_batch *hb, const dcr_fmt_out *ss, 
             o.n = 0;
             const int32_t f0 = (g0 + (int32_t)gi) * chunk, f1 = std::min(n_fam, f0 + chunk);
             for (int32_t f = f0; f < f1; ++f) {
-                const char *code = hb->names + code_of[(size_t)f];
+                const char *code = hb->names + code_of[f];
                 const size_t lc = std::strlen(code);
                 for (int j = 0; j < 2; ++j) {
                     o.reserve(record_bound(c, f, j, lc));

@@ -561,6 +561,7 @@ struct dcr_ingest {
         b->tab_exc_cut[t] = b->n_side_exc;
         b->tab_filt_cut[t] = b->n_side_filt;
         b->tab_code[t] = put_name(code.data(), code.size());
+        const int64_t code_off = b->tab_code[t];
         if (!enough) {
             // filtered family: its reads to _filteredfamilies.bam in input order (:1550-1551)
             b->tab_kind[t] = DCR_FAM_FILTERED;
@@ -577,6 +578,7 @@ struct dcr_ingest {
         b->tab_kind[t] = DCR_FAM_PROCESSED;
         b->tab_proc[t] = f;
         b->fam_tid[f] = r0.tid;
+        b->fam_code[f] = code_off;
         int64_t mn[4], mx[4];
         for (int k = 0; k < 4; ++k) {
             int16_t eqx = 0;

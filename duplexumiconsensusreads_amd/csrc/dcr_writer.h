@@ -1,0 +1,50 @@
+// dcr_writer.h — kernel arguments of the device record writer
+// (dcr_writer.hip); not part of the C-ABI (include/dcr.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dcr.h"
+
+namespace dcrw {
+
+struct FmtArgs {
+    dcr_out ss, ds;                 // device kernel outputs
+    const int32_t *sub_off;         // [4F+1]
+    const uint8_t *read_mapq;
+    const int64_t *ss_col_off, *ds_col_off;
+    const dcr_read_info *info;      // per-read preprocessing status
+    const char *names;
+    const int64_t *fam_code, *fam_rx;
+    const int32_t *fam_tid;
+    int32_t n_fam;
+    int32_t *fam_fail;              // [F] DCR_FAIL_* | which << 8
+    int32_t *ds_len_out;            // [2F]
+    int64_t *rec_size;              // [2F+1] (the last one 0: the scan's total)
+    int64_t *rec_off;               // [2F+1]
+    uint8_t *stream;                // formatted records
+};
+
+struct DflArgs {
+    const uint8_t *stream;
+    const int64_t *stream_bytes;    // device scalar (rec_off[2F])
+    uint8_t *slots;                 // 64 KiB per block
+    int64_t *sizes;                 // per block (0 past the last block)
+};
+
+struct CompactArgs {
+    const uint8_t *slots;
+    const int64_t *sizes;
+    const int64_t *offs;            // exclusive scan of sizes
+    const int64_t *stream_bytes;
+    uint8_t *out;
+    int64_t *totals;                // [3] compressed bytes, formatted bytes, blocks
+};
+
+__global__ void k_famfail(FmtArgs A);
+__global__ void k_fmt_size(FmtArgs A);
+__global__ void k_fmt_write(FmtArgs A);
+__global__ void k_deflate(DflArgs D);
+__global__ void k_compact(CompactArgs C);
+
+}  // namespace dcrw

@@ -38,7 +38,8 @@ _HB_ARRAYS = [
     ("seq_off", np.int64, "r"), ("seq_len", np.int32, "r"), ("cig_off", np.int32, "r"),
     ("cig_n", np.int32, "r"), ("cigar", np.uint32, "c"), ("bases", np.uint8, "b"), ("quals", np.uint8, "b"),
     ("ss_col_off", np.int64, "4f1"), ("ds_col_off", np.int64, "2f1"),
-    ("fam_tid", np.int32, "f"), ("fam_rx", np.int64, "2f"), ("fam_eqx", np.uint16, "4f"),
+    ("fam_tid", np.int32, "f"), ("fam_code", np.int64, "f"), ("fam_rx", np.int64, "2f"),
+    ("fam_eqx", np.uint16, "4f"),
     ("tab_kind", np.int32, "t"), ("tab_proc", np.int32, "t"), ("tab_sampled", np.int32, "t"),
     ("tab_code", np.int64, "t"), ("tab_exc_cut", np.int64, "t"), ("tab_filt_cut", np.int64, "t"),
     ("names", np.uint8, "n"), ("side_exc", np.uint8, "s"), ("side_filt", np.uint8, "s"),
@@ -93,10 +94,12 @@ def load():
             "dcr_bgzw_open": (_vp, [ctypes.c_char_p, _i32, _i32]),
             "dcr_bgzw_write": (_i32, [_vp, _vp, _i64]),
             "dcr_bgzw_close": (_i32, [_vp]),
+            "dcr_bgzw_put_blocks": (_i32, [_vp, _vp, _i64, _i64]),
             "dcr_bgzw_sizes": (_i32, [_vp, _vp]),
             "dcr_fmt_scan": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp, _vp]),
             "dcr_fmt_write": (_i32, [_vp, _vp, _vp, _vp, _i32]),
             "dcr_synth_write": (_i32, [_vp, _vp, _i32]),
+            "dcr_deflate_emulate": (_i64, [_vp, _i64, _vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -264,6 +267,11 @@ class BgzfWriter:
         if n and load().dcr_bgzw_write(self._h, ptr, n) != 0:
             raise _err("BGZF write")
 
+    def put_blocks(self, blocks: np.ndarray, raw_bytes: int):
+        """Append BGZF blocks compressed elsewhere (the device writer)."""
+        if load().dcr_bgzw_put_blocks(self._h, blocks.ctypes.data, blocks.nbytes, raw_bytes) != 0:
+            raise _err("BGZF put_blocks")
+
     def write_consensus(self, hb: HostBatch, ss: FmtOut, ds: FmtOut, n_fam: int):
         if n_fam and load().dcr_fmt_write(self._h, ctypes.byref(hb.s), ctypes.byref(ss), ctypes.byref(ds),
                                           n_fam) != 0:
@@ -311,6 +319,16 @@ def first_failure(hb: HostBatch, ss: FmtOut, ds: FmtOut, n_fam: int, read_status
     f = load().dcr_fmt_scan(ctypes.byref(hb.s), ctypes.byref(ss), ctypes.byref(ds), rs, n_fam,
                             ctypes.byref(kind), ctypes.byref(which))
     return f, FAIL_NAMES.get(kind.value), which.value
+
+
+def deflate_emulate(data: bytes) -> bytes:
+    """One BGZF block from the GPU compressor's algorithm, emulated on the host."""
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    out = ctypes.create_string_buffer(65536)
+    n = load().dcr_deflate_emulate(buf, len(data), out)
+    if n < 0:
+        raise IOError_("deflate_emulate: bad input size")
+    return out.raw[:n]
 
 
 def py_sample(state, n, k):

@@ -103,16 +103,83 @@ class _HostOut:
         return o
 
 
-class DeviceStream:
-    """Asynchronous batches on one GPU context (``_lib.Context``)."""
+class WMeta(ctypes.Structure):
+    _fields_ = [("names", ctypes.c_void_p), ("n_names", ctypes.c_int64), ("fam_code", ctypes.c_void_p),
+                ("fam_rx", ctypes.c_void_p), ("fam_tid", ctypes.c_void_p)]
 
-    def __init__(self, ctx, n_slots=2, owns_ctx=False):
+
+class WRes(ctypes.Structure):
+    _fields_ = [("bgzf", ctypes.c_void_p), ("cap_bgzf", ctypes.c_int64), ("fam_fail", ctypes.c_void_p),
+                ("ds_len", ctypes.c_void_p), ("totals", ctypes.c_void_p)]
+
+
+class _WriterOut:
+    """Pinned host arrays of one slot's device-writer results (grow-only)."""
+
+    def __init__(self, lib):
+        self.lib = lib
+        self.cap_f = 0
+        self.cap_b = 0
+        self.small = None
+        self.blocks = None
+
+    def ensure(self, n_fam, bgzf_bytes):
+        if n_fam > self.cap_f or self.small is None:
+            self.cap_f = int(n_fam * 1.25) + 64
+            self.small = Pinned(self.lib, 12 * self.cap_f + 64)
+            a = self.small.array
+            self.fam_fail = a[:4 * self.cap_f].view(np.int32)
+            self.ds_len = a[4 * self.cap_f:12 * self.cap_f].view(np.int32)
+            self.totals = a[12 * self.cap_f:12 * self.cap_f + 24].view(np.int64)
+        if bgzf_bytes > self.cap_b:
+            self.cap_b = int(bgzf_bytes * 1.25) + (1 << 20)
+            self.blocks = Pinned(self.lib, self.cap_b)
+
+    def wres(self):
+        r = WRes()
+        r.bgzf, r.cap_bgzf = self.blocks.ptr, self.cap_b
+        r.fam_fail, r.ds_len, r.totals = self.fam_fail.ctypes.data, self.ds_len.ctypes.data, self.totals.ctypes.data
+        return r
+
+
+class WriterResult:
+    """One batch through the device writer: per-family outcomes (0: written),
+    duplex lengths, and the BGZF blocks of the records of every family that
+    does not fail."""
+
+    def __init__(self, stream, slot, out, n_fam):
+        self._stream, self._slot = stream, slot
+        self.fam_fail = out.fam_fail[:n_fam]
+        self.ds_len = out.ds_len[:2 * n_fam]
+        self.bgzf_bytes, self.record_bytes, self.blocks = (int(x) for x in out.totals[:3])
+        self.bgzf = out.blocks.array[:self.bgzf_bytes]
+
+    def record_bytes_of(self, n_fam):
+        """Formatted records of families [0, n_fam) (fetched from the device slot)."""
+        lib, ctx = self._stream.lib, self._stream.ctx._ctx
+        from . import _lib
+        end = np.zeros(1, np.int64)
+        _lib._check(lib.dcr_slot_fetch(ctx, self._slot, 1, 2 * n_fam, 1, end.ctypes.data))
+        buf = np.zeros(max(int(end[0]), 1), np.uint8)
+        _lib._check(lib.dcr_slot_fetch(ctx, self._slot, 0, 0, int(end[0]), buf.ctypes.data))
+        return buf[:int(end[0])]
+
+
+class DeviceStream:
+    """Asynchronous batches on one GPU context (``_lib.Context``).  With
+    ``device_writer`` the records are formatted and BGZF-compressed on the
+    device (dcr_submit_write); otherwise the kernel outputs come back for the
+    host writer (dcr_submit)."""
+
+    def __init__(self, ctx, n_slots=2, owns_ctx=False, device_writer=True):
         from . import _lib
         self.ctx = ctx
         self.owns_ctx = owns_ctx
+        self.device_writer = device_writer
         self.lib = _lib.load()
         self.n_slots = n_slots
         self.outs = [_HostOut(self.lib) for _ in range(n_slots)]
+        self.wouts = [_WriterOut(self.lib) for _ in range(n_slots)]
         self.busy = [False] * n_slots
         self.next_slot = 0
         self._pins = []
@@ -126,6 +193,21 @@ class DeviceStream:
         if self.busy[slot]:
             raise RuntimeError("DeviceStream: slot reused before its result was taken")
         s = hb.s
+        if self.device_writer:
+            from . import _lib
+            wo = self.wouts[slot]
+            # compressed records are far smaller than the kernel outputs; grown on demand
+            wo.ensure(s.n_fam, max(64 << 20, 2 * s.n_bases // 3))
+            self._b = hb.batch_struct()
+            m = WMeta()
+            m.names, m.n_names = hb.a["names"].ctypes.data, s.n_names
+            m.fam_code, m.fam_rx, m.fam_tid = (hb.a["fam_code"].ctypes.data, hb.a["fam_rx"].ctypes.data,
+                                               hb.a["fam_tid"].ctypes.data)
+            self._wres = wo.wres()
+            _lib._check(self.lib.dcr_submit_write(self.ctx._ctx, slot, ctypes.byref(self._b), ctypes.byref(m),
+                                                  ctypes.byref(self._wres)))
+            self.busy[slot] = True
+            return (slot, s.n_fam)
         out = self.outs[slot]
         out.ensure(4 * s.n_fam, s.ss_cols, 2 * s.n_fam, s.ds_cols, s.n_reads)
         self._b = hb.batch_struct()
@@ -136,8 +218,24 @@ class DeviceStream:
         self.busy[slot] = True
         return slot
 
-    def result(self, slot):
+    def result(self, handle):
         from . import _lib
+        if self.device_writer:
+            slot, n_fam = handle
+            wo = self.wouts[slot]
+            r = wo.wres()
+            rc = self.lib.dcr_wait_write(self.ctx._ctx, slot, ctypes.byref(r))
+            self.busy[slot] = False
+            if rc == 3 and int(wo.totals[0]) > wo.cap_b:      # DCR_ECAPACITY: grow, fetch again
+                n = int(wo.totals[0])
+                tot = wo.totals[:3].copy()
+                wo.ensure(n_fam, n)
+                wo.totals[:3] = tot
+                _lib._check(self.lib.dcr_slot_fetch(self.ctx._ctx, slot, 2, 0, n, wo.blocks.ptr))
+            else:
+                _lib._check(rc)
+            return WriterResult(self, slot, wo, n_fam)
+        slot = handle
         _lib._check(self.lib.dcr_wait(self.ctx._ctx, slot))
         self.busy[slot] = False
         out = self.outs[slot]
@@ -146,7 +244,10 @@ class DeviceStream:
     def close(self):
         for slot in range(self.n_slots):
             if self.busy[slot]:
-                self.lib.dcr_wait(self.ctx._ctx, slot)
+                if self.device_writer:
+                    self.lib.dcr_wait_write(self.ctx._ctx, slot, ctypes.byref(self.wouts[slot].wres()))
+                else:
+                    self.lib.dcr_wait(self.ctx._ctx, slot)
                 self.busy[slot] = False
         if self.owns_ctx:
             self.ctx.close()

@@ -183,6 +183,36 @@ int dcr_submit(dcr_ctx *ctx, int slot, const dcr_batch *host_in, dcr_out *host_s
                int32_t *read_status);
 int dcr_wait(dcr_ctx *ctx, int slot);
 
+/* Device record writer.  dcr_submit_write is dcr_submit followed, on the
+ * device, by the reference's per-family outcome (what make_consensus_read /
+ * preprocess_family raise, in its order), the two duplex BAM records of every
+ * family that does not fail (make_consensus_read :1352-1384, add_tags
+ * :1076-1120, fix_paired_end_fields :1390-1419), formatted as the host writer
+ * (libdcr_io dcr_fmt_write) formats them, and their BGZF compression; only
+ * the compressed blocks, the outcomes and the duplex lengths come back.
+ * dcr_wait_write waits for the slot and copies the blocks into res->bgzf.
+ * The formatted records stay in the slot until it is submitted again
+ * (dcr_slot_fetch: what 0 = record bytes, 1 = int64 record offsets [2F+1],
+ * 2 = the BGZF blocks again, e.g. after dcr_wait_write found cap_bgzf too
+ * small: totals[0] holds the size). */
+typedef struct dcr_wmeta {
+    const char *names;           /* string arena (dcr_host_batch.names)          */
+    int64_t n_names;
+    const int64_t *fam_code;     /* [F] offsets of the family codes (MI prefix)  */
+    const int64_t *fam_rx;       /* [2F] offsets of RX of the A1 / B1 read0      */
+    const int32_t *fam_tid;      /* [F] reference_id                             */
+} dcr_wmeta;
+typedef struct dcr_wres {        /* pinned host memory                          */
+    uint8_t *bgzf;               /* BGZF blocks of the batch's records, in order */
+    int64_t cap_bgzf;
+    int32_t *fam_fail;           /* [F] DCR_FAIL_* | which << 8 (include/dcr_io.h), 0: written */
+    int32_t *ds_len;             /* [2F] duplex consensus lengths                */
+    int64_t *totals;             /* [3] BGZF bytes, record bytes, BGZF blocks    */
+} dcr_wres;
+int dcr_submit_write(dcr_ctx *ctx, int slot, const dcr_batch *host_in, const dcr_wmeta *meta, dcr_wres *res);
+int dcr_wait_write(dcr_ctx *ctx, int slot, dcr_wres *res);
+int dcr_slot_fetch(dcr_ctx *ctx, int slot, int what, int64_t off, int64_t n, void *dst);
+
 /* CPU restatement with the same contract (oracle/, test infrastructure):
    host pointers, single thread (or n_threads > 1) */
 int dcr_oracle_run(const dcr_params *params, const dcr_batch *in, dcr_out *ss, dcr_out *ds,

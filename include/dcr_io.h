@@ -104,6 +104,7 @@ typedef struct dcr_host_batch {
     int64_t *ds_col_off;    /* [2*cap_fam+1] */
     /* per processed family (writer metadata) */
     int32_t *fam_tid;       /* [cap_fam] reference_id of the family          */
+    int64_t *fam_code;      /* [cap_fam] names offset of the family code (MI prefix) */
     int64_t *fam_rx;        /* [2*cap_fam] names offsets: RX of A1 read0, of B1 read0 */
     uint16_t *fam_eqx;      /* [4*cap_fam] reads whose CIGAR still holds =/X after the trim (:374-375) */
     /* family table */
@@ -152,6 +153,9 @@ typedef struct dcr_bgzw dcr_bgzw;
 /* level 0..12 (libdeflate levels; htslib's default is 6) */
 dcr_bgzw *dcr_bgzw_open(const char *path, int level, int n_threads);
 int dcr_bgzw_write(dcr_bgzw *w, const void *bytes, int64_t n);
+/* append already compressed BGZF blocks (n bytes, holding raw_bytes of
+   data), after flushing what write() left pending */
+int dcr_bgzw_put_blocks(dcr_bgzw *w, const void *blocks, int64_t n, int64_t raw_bytes);
 /* flush, write the BGZF EOF marker, close; 0 on success */
 int dcr_bgzw_close(dcr_bgzw *w);
 /* bytes written so far (compressed, uncompressed) */
@@ -189,6 +193,11 @@ int32_t dcr_fmt_scan(const dcr_host_batch *hb, const dcr_fmt_out *ss, const dcr_
  * of families that fail must not be in the range) and write them. */
 int dcr_fmt_write(dcr_bgzw *w, const dcr_host_batch *hb, const dcr_fmt_out *ss, const dcr_fmt_out *ds,
                   int32_t n_fam);
+
+/* ---- the GPU BGZF block compressor (csrc/dcr_deflate.h) emulated lane by
+ * lane on the host, for tests: one BGZF block of in[0, n) (n <= 0xff00) into
+ * out (>= 64 KiB); returns its size or -1 */
+int64_t dcr_deflate_emulate(const uint8_t *in, int64_t n, uint8_t *out);
 
 /* ---- synthetic inputs (bench / tests) ----
  * Records of n_fam duplex families from dcr_batch-layout arrays (reads of
