@@ -23,6 +23,7 @@ EXPORTS = {
     "dcr_create": (ctypes.c_void_p, [ctypes.c_int, ctypes.c_void_p]),
     "dcr_destroy": (None, [ctypes.c_void_p]),
     "dcr_set_params": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "dcr_set_options": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "dcr_reserve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "dcr_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
     "dcr_run_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
@@ -92,7 +93,9 @@ def _check(rc):
 class Context:
     """One GPU context (``dcr_ctx``): stream, parameters, workspace."""
 
-    def __init__(self, params: ConsensusParams = ConsensusParams(), device: int = 0):
+    def __init__(self, params: ConsensusParams = ConsensusParams(), device: int = 0, want_info: bool = False):
+        """``want_info``: write every read's preprocessing info (DCR_OPT_READ_INFO,
+        parity tests); the product path only needs failing reads'."""
         lib = load()
         self.params = params
         self._p = build_dcr_params(params)
@@ -100,6 +103,8 @@ class Context:
         self._ctx = lib.dcr_create(device, ctypes.byref(self._p))
         if not self._ctx:
             raise DcrError(f"dcr_create failed: {lib.dcr_last_error().decode()}")
+        if want_info:
+            _check(lib.dcr_set_options(self._ctx, 1))
 
     def close(self):
         if getattr(self, "_ctx", None):

@@ -81,6 +81,7 @@ struct dcr_ctx {
     int64_t last_reads = 0;
     bool timed = false;
     int fast_ok = 0;    // fast_allowed(): the fast kernel may take records
+    int options = 0;    // DCR_OPT_*
     int wide_ok = 0;    // the general kernel's decision pass may run (wide_table)
     dcr_params host_params{};
     // fast-kernel constants (fast_constants)
@@ -292,6 +293,13 @@ int dcr_set_params(dcr_ctx *c, const dcr_params *params) {
 
 void *dcr_stream(dcr_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
+int dcr_set_options(dcr_ctx *c, int flags) {
+    if (!c) return fail(DCR_EARG, "ctx is NULL");
+    if (flags & ~DCR_OPT_READ_INFO) return fail(DCR_EARG, "unknown option");
+    c->options = flags;
+    return DCR_OK;
+}
+
 int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     if (!c || !s) return fail(DCR_EARG, "NULL argument");
     HIP_TRY(hipSetDevice(c->device));
@@ -393,6 +401,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         f.minbq = duplex ? -1 : c->host_params.min_base_quality;
         f.lo_check = duplex || c->host_params.min_base_quality < c->fast_qlo;
         f.llr16 = c->d_llr16;
+        f.want_info = (c->options & DCR_OPT_READ_INFO) ? 1 : 0;
         return f;
     };
     auto strand = [&](bool duplex) -> int {

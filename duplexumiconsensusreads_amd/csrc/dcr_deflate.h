@@ -49,7 +49,7 @@ constexpr uint32_t kSlot = 65536;         // output slot bytes (one BGZF block a
 constexpr uint32_t kMaxDeflate = kSlot - 26;
 constexpr int kLS = 32;                   // lane-private recency table: sets x 2 ways
 
-struct Shared {
+struct alignas(16) Shared {
     uint8_t in[kMaxIn + 16];
     uint32_t a_min[kHN], a_max[kHN], b_min[kHN];   // positions (a_max: position + 1, 0 none)
     uint16_t lt[kT][2 * kLS];             // per lane: latest positions + 1 per hash set (2 ways)
@@ -60,7 +60,11 @@ struct Shared {
     uint32_t lane_off[kT];
     uint32_t lane_crc[kT];
     uint32_t extra_bits;                  // extra bits of all matches (pass P2)
-    uint32_t sort_a[320];                 // (freq << 9 | symbol) then in-place code lengths
+    uint32_t sort_a[320];                 // scratch of the small (code-length code) build
+    uint32_t key_lit[288], key_dist[32];  // (freq << 9 | symbol), 0 = unused; then sorted ascending
+    uint32_t srt_lit[288], srt_dist[32];  // sorted keys, then in-place code lengths
+    uint32_t m_lit, m_dist;               // used symbols
+    uint32_t next_code[3][16];            // canonical first codes per length: lit, dist, cl
     uint16_t rle[320];                    // header: code-length symbol | extra << 8
     uint32_t n_rle;
     uint32_t hlit, hdist, hclen;
@@ -146,8 +150,14 @@ DFL_HD inline uint32_t x8nmodp(uint32_t n) {
 
 // ---- input access -------------------------------------------------------------
 DFL_HD inline uint32_t ld32(const Shared &s, uint32_t p) {
+#if DFL_DEVICE
+    // two aligned LDS dwords and a byte funnel shift
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(s.in);
+    return __builtin_amdgcn_alignbyte(w[(p >> 2) + 1], w[p >> 2], p & 3);
+#else
     return (uint32_t)s.in[p] | ((uint32_t)s.in[p + 1] << 8) | ((uint32_t)s.in[p + 2] << 16) |
            ((uint32_t)s.in[p + 3] << 24);
+#endif
 }
 DFL_HD inline uint32_t hash4(uint32_t v) { return (v * 0x9E3779B1u) >> (32 - kHB); }
 
@@ -334,40 +344,13 @@ DFL_HD inline void mr_lengths(uint32_t *a, int m) {
     }
 }
 
-// Code lengths <= max_len for freq[0..n) into len[0..n); scratch holds >= n words.
-// At least `min_used` symbols get a code (padding with the lowest symbols).
-DFL_HD inline void build_lengths(const uint32_t *freq, int n, int max_len, uint8_t *len, uint32_t *scratch,
-                                 int min_used) {
-    int m = 0;
-    for (int i = 0; i < n; ++i) {
-        len[i] = 0;
-        if (freq[i]) scratch[m++] = (freq[i] << 9) | (uint32_t)i;
-    }
-    for (int i = 0; i < n && m < min_used; ++i)
-        if (!freq[i]) scratch[m++] = (0u << 9) | (uint32_t)i;
-    if (m == 0) return;
-    if (m == 1) {                          // one code of length 1 (inflate accepts it)
-        len[scratch[0] & 511] = 1;
-        return;
-    }
-    // insertion sort by (freq, symbol) ascending (m <= 288)
-    for (int i = 1; i < m; ++i) {
-        const uint32_t v = scratch[i];
-        int j = i - 1;
-        while (j >= 0 && scratch[j] > v) { scratch[j + 1] = scratch[j]; --j; }
-        scratch[j + 1] = v;
-    }
-    uint16_t sym[288];
-    uint32_t f[288];
-    for (int i = 0; i < m; ++i) {
-        sym[i] = (uint16_t)(scratch[i] & 511);
-        const uint32_t fr = scratch[i] >> 9;
-        f[i] = fr ? fr : 1;               // padded (unused) symbols weigh 1
-    }
-    mr_lengths(f, m);
-    // limit to max_len: count per length, move overflow to max_len, restore the Kraft sum
-    uint32_t num[33] = {0};
-    for (int i = 0; i < m; ++i) num[f[i] > 32 ? 32 : f[i]]++;
+// Length-limit code lengths a[0..m) (non-increasing, from mr_lengths) to
+// max_len and hand them to the symbols of keys[0..m) (ascending frequency):
+// the rarest symbols take the longest codes.
+DFL_HD inline void limit_assign(uint32_t *a, const uint32_t *keys, int m, int max_len, uint8_t *len) {
+    uint32_t num[33];
+    for (int i = 0; i <= 32; ++i) num[i] = 0;
+    for (int i = 0; i < m; ++i) num[a[i] > 32 ? 32 : a[i]]++;
     for (int i = max_len + 1; i <= 32; ++i) { num[max_len] += num[i]; num[i] = 0; }
     uint32_t total = 0;
     for (int i = max_len; i > 0; --i) total += num[i] << (max_len - i);
@@ -377,37 +360,117 @@ DFL_HD inline void build_lengths(const uint32_t *freq, int n, int max_len, uint8
             if (num[i]) { num[i]--; num[i + 1] += 2; break; }
         total--;
     }
-    // the rarest symbols take the longest codes
     int k = 0;
     for (int l = max_len; l >= 1; --l)
-        for (uint32_t c = 0; c < num[l]; ++c) len[sym[k++]] = (uint8_t)l;
+        for (uint32_t c = 0; c < num[l]; ++c) len[keys[k++] & 511] = (uint8_t)l;
+}
+
+// Code lengths <= max_len for freq[0..n) (n <= 32) into len[0..n) on one
+// thread; scratch holds 2n words.  At least `min_used` symbols get a code.
+DFL_HD inline void build_lengths_small(const uint32_t *freq, int n, int max_len, uint8_t *len, uint32_t *scratch,
+                                       int min_used) {
+    int m = 0;
+    uint32_t *keys = scratch, *f = scratch + n;
+    for (int i = 0; i < n; ++i) {
+        len[i] = 0;
+        if (freq[i]) keys[m++] = (freq[i] << 9) | (uint32_t)i;
+    }
+    for (int i = 0; i < n && m < min_used; ++i)
+        if (!freq[i]) keys[m++] = (uint32_t)i;
+    if (m == 0) return;
+    if (m == 1) { len[keys[0] & 511] = 1; return; }
+    for (int i = 1; i < m; ++i) {
+        const uint32_t v = keys[i];
+        int j = i - 1;
+        while (j >= 0 && keys[j] > v) { keys[j + 1] = keys[j]; --j; }
+        keys[j + 1] = v;
+    }
+    for (int i = 0; i < m; ++i) f[i] = (keys[i] >> 9) ? (keys[i] >> 9) : 1;
+    mr_lengths(f, m);
+    limit_assign(f, keys, m, max_len, len);
 }
 
 DFL_HD inline uint32_t reverse_bits(uint32_t v, int nb) {
+#if DFL_DEVICE
+    return __brev(v) >> (32 - nb);
+#else
     uint32_t r = 0;
     for (int i = 0; i < nb; ++i) { r = (r << 1) | (v & 1); v >>= 1; }
     return r;
+#endif
 }
 
-DFL_HD inline void canonical(const uint8_t *len, int n, uint16_t *code) {
-    uint32_t cnt[16] = {0}, next[16] = {0};
+DFL_HD inline void first_codes(const uint8_t *len, int n, uint32_t *next) {
+    uint32_t cnt[16];
+    for (int l = 0; l < 16; ++l) cnt[l] = 0;
     for (int i = 0; i < n; ++i) cnt[len[i]]++;
     cnt[0] = 0;
     uint32_t c = 0;
+    next[0] = 0;
     for (int l = 1; l < 16; ++l) { c = (c + cnt[l - 1]) << 1; next[l] = c; }
-    for (int i = 0; i < n; ++i)
-        code[i] = len[i] ? (uint16_t)reverse_bits(next[len[i]]++, len[i]) : 0;
 }
 
-// P3 on thread 0: code lengths, codes, header; returns header bits
-DFL_HD inline void build_codes(Shared &s) {
-    s.lit_freq[256] = 1;                                   // end of block
-    build_lengths(s.lit_freq, 286, 15, s.lit_len, s.sort_a, 2);
-    build_lengths(s.dist_freq, 30, 15, s.dist_len, s.sort_a, 1);
-    s.lit_len[286] = s.lit_len[287] = 0;
-    s.dist_len[30] = s.dist_len[31] = 0;
-    canonical(s.lit_len, 286, s.lit_code);
-    canonical(s.dist_len, 30, s.dist_code);
+// canonical code of symbol i: the first code of its length + the symbols of
+// that length before it (parallel over symbols)
+DFL_HD inline uint16_t code_of(const uint8_t *len, int i, const uint32_t *next) {
+    const int L = len[i];
+    if (!L) return 0;
+    uint32_t r = 0;
+    for (int j = 0; j < i; ++j) r += len[j] == L;
+    return (uint16_t)reverse_bits(next[L] + r, L);
+}
+
+// P3a (all lanes): symbol keys and their ranks (sorted ascending by (freq, symbol))
+DFL_HD inline void p3a_keys(Shared &s, int lane) {
+    if (lane == 0) { s.lit_freq[256] = 1; s.m_lit = 0; s.m_dist = 0; }   // end of block
+    for (int i = lane; i < 288; i += kT) {
+        const uint32_t f = (i < 286) ? (i == 256 ? 1u : s.lit_freq[i]) : 0u;
+        s.key_lit[i] = f ? ((f << 9) | (uint32_t)i) : 0u;
+    }
+    if (lane < 32) {
+        const uint32_t f = lane < 30 ? s.dist_freq[lane] : 0u;
+        s.key_dist[lane] = f ? ((f << 9) | (uint32_t)lane) : 0u;
+    }
+}
+DFL_HD inline void p3b_rank(Shared &s, int lane) {
+    for (int i = lane; i < 288; i += kT) {
+        const uint32_t k = s.key_lit[i];
+        if (!k) continue;
+        uint32_t r = 0;
+        for (int j = 0; j < 288; ++j) { const uint32_t o = s.key_lit[j]; r += (o != 0) & (o < k); }
+        s.srt_lit[r] = k;
+        aadd(&s.m_lit, 1);
+    }
+    if (lane < 32) {
+        const uint32_t k = s.key_dist[lane];
+        if (k) {
+            uint32_t r = 0;
+            for (int j = 0; j < 32; ++j) { const uint32_t o = s.key_dist[j]; r += (o != 0) & (o < k); }
+            s.srt_dist[r] = k;
+            aadd(&s.m_dist, 1);
+        }
+    }
+}
+
+// P3c (thread 0): code lengths, first codes, the run-length-coded header
+DFL_HD inline void p3c_lengths(Shared &s) {
+    for (int i = 0; i < 288; ++i) s.lit_len[i] = 0;
+    for (int i = 0; i < 32; ++i) s.dist_len[i] = 0;
+    const int ml = (int)s.m_lit;
+    uint32_t *f = s.sort_a;
+    for (int i = 0; i < ml; ++i) f[i] = s.srt_lit[i] >> 9;
+    mr_lengths(f, ml);                               // >= 2 symbols: a literal and end of block
+    limit_assign(f, s.srt_lit, ml, 15, s.lit_len);
+    const int md = (int)s.m_dist;
+    if (md == 0) s.dist_len[0] = 1;                  // no match: one unused code of length 1
+    else if (md == 1) s.dist_len[s.srt_dist[0] & 511] = 1;
+    else {
+        for (int i = 0; i < md; ++i) f[i] = s.srt_dist[i] >> 9;
+        mr_lengths(f, md);
+        limit_assign(f, s.srt_dist, md, 15, s.dist_len);
+    }
+    first_codes(s.lit_len, 286, s.next_code[0]);
+    first_codes(s.dist_len, 30, s.next_code[1]);
     int nlit = 286;
     while (nlit > 257 && !s.lit_len[nlit - 1]) --nlit;
     int ndist = 30;
@@ -415,16 +478,15 @@ DFL_HD inline void build_codes(Shared &s) {
     s.hlit = (uint32_t)(nlit - 257);
     s.hdist = (uint32_t)(ndist - 1);
     // run-length code the lengths (symbols 16 / 17 / 18)
-    uint8_t L[320];
     const int N = nlit + ndist;
-    for (int i = 0; i < nlit; ++i) L[i] = s.lit_len[i];
-    for (int i = 0; i < ndist; ++i) L[nlit + i] = s.dist_len[i];
-    uint32_t clf[19] = {0};
+    auto L = [&](int i) -> uint8_t { return i < nlit ? s.lit_len[i] : s.dist_len[i - nlit]; };
+    uint32_t clf[19];
+    for (int i = 0; i < 19; ++i) clf[i] = 0;
     uint32_t nr = 0;
     for (int i = 0; i < N;) {
-        const uint8_t v = L[i];
+        const uint8_t v = L(i);
         int run = 1;
-        while (i + run < N && L[i + run] == v) ++run;
+        while (i + run < N && L(i + run) == v) ++run;
         i += run;
         if (v == 0) {
             while (run >= 11) { const int r = run < 138 ? run : 138; s.rle[nr++] = (uint16_t)(18 | ((r - 11) << 8)); clf[18]++; run -= r; }
@@ -437,8 +499,8 @@ DFL_HD inline void build_codes(Shared &s) {
         }
     }
     s.n_rle = nr;
-    build_lengths(clf, 19, 7, s.cl_len, s.sort_a, 2);
-    canonical(s.cl_len, 19, s.cl_code);
+    build_lengths_small(clf, 19, 7, s.cl_len, s.sort_a, 2);
+    first_codes(s.cl_len, 19, s.next_code[2]);
     int ncl = 19;
     while (ncl > 4 && !s.cl_len[kClOrder[ncl - 1]]) --ncl;
     s.hclen = (uint32_t)(ncl - 4);
@@ -448,6 +510,13 @@ DFL_HD inline void build_codes(Shared &s) {
         bits += s.cl_len[sym] + (sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0);
     }
     s.hdr_bits = bits;
+}
+
+// P3d (all lanes): canonical codes
+DFL_HD inline void p3d_codes(Shared &s, int lane) {
+    for (int i = lane; i < 288; i += kT) s.lit_code[i] = i < 286 ? code_of(s.lit_len, i, s.next_code[0]) : 0;
+    if (lane < 32) s.dist_code[lane] = lane < 30 ? code_of(s.dist_len, lane, s.next_code[1]) : 0;
+    if (lane < 19) s.cl_code[lane] = code_of(s.cl_len, lane, s.next_code[2]);
 }
 
 DFL_HD inline void write_header(const Shared &s, BitOut &o) {

@@ -19,7 +19,10 @@ extern "C" int64_t dcr_deflate_emulate(const uint8_t *in, int64_t n, uint8_t *ou
     for (int l = 0; l < dfl::kT; ++l) dfl::p0_clear(s, l);
     for (int l = 0; l < dfl::kT; ++l) dfl::p1_hash(s, N, l);
     for (int l = 0; l < dfl::kT; ++l) dfl::p2_count(s, N, l);
-    dfl::build_codes(s);
+    for (int l = 0; l < dfl::kT; ++l) dfl::p3a_keys(s, l);
+    for (int l = 0; l < dfl::kT; ++l) dfl::p3b_rank(s, l);
+    dfl::p3c_lengths(s);
+    for (int l = 0; l < dfl::kT; ++l) dfl::p3d_codes(s, l);
     for (int l = 0; l < dfl::kT; ++l) dfl::p4_bits(s, N, l);
     dfl::p4_scan(s, N);
     for (int l = 0; l < dfl::kT; ++l) dfl::p5_emit(s, N, l, w.data());

@@ -395,7 +395,7 @@ int32_t dcr_fmt_scan(const dcr_host_batch *hb, const dcr_fmt_out *ss, const dcr_
                      const int32_t *read_status, int32_t n_fam, int32_t *kind, int32_t *which) {
     *kind = DCR_FAIL_NONE;
     *which = -1;
-    auto st_fail = [](int st) { return st != 0 && st != DCR_ST_UPSTREAM && !(st & 0x10); };
+    auto st_fail = [](int st) { return st != 0 && st != DCR_ST_UPSTREAM && !(st & DCR_ST_PREP); };
     auto unicode = [&](int32_t s) {
         const int64_t o = hb->ss_col_off[s];
         for (int32_t i = 0; i < ss->len[s]; ++i)
@@ -403,20 +403,15 @@ int32_t dcr_fmt_scan(const dcr_host_batch *hb, const dcr_fmt_out *ss, const dcr_
         return false;
     };
     for (int32_t f = 0; f < n_fam; ++f) {
-        // preprocess_family's read loop (:1272-1283): the first failing read
-        if (read_status) {
-            for (int32_t r = hb->sub_off[4 * f]; r < hb->sub_off[4 * f + 4]; ++r)
-                if (read_status[r]) {
-                    *kind = read_status[r];
-                    int k = 0;
-                    while (r >= hb->sub_off[4 * f + k + 1]) ++k;
-                    *which = 8 + k;
-                    return f;
-                }
-        } else {
-            for (int k = 0; k < 4; ++k)
-                if (ss->status[4 * f + k] & 0x10) { *kind = ss->status[4 * f + k] & 0x0f; *which = 8 + k; return f; }
-        }
+        // preprocess_family's read loop (:1272-1283): the first subfamily
+        // holding a failing read (DCR_ST_PREP | that read's status)
+        (void)read_status;
+        for (int k = 0; k < 4; ++k)
+            if (ss->status[4 * f + k] & DCR_ST_PREP) {
+                *kind = ss->status[4 * f + k] & 0x0f;
+                *which = 8 + k;
+                return f;
+            }
         for (int k = 0; k < 4; ++k)                   // make_consensus_read x4 (:1564-1569)
             if (st_fail(ss->status[4 * f + k])) { *kind = ss->status[4 * f + k]; *which = k; return f; }
         for (int j = 0; j < 2; ++j) {                 // x2 duplex (:1581-1582), then its set_tags (:1384)

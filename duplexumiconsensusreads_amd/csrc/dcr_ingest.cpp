@@ -13,6 +13,10 @@
 #include <zlib.h>
 
 #include <cmath>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -148,17 +152,170 @@ struct Job {
 
 }  // namespace
 
+// Background BGZF inflate: a thread reads the file and inflates ~32 MiB runs
+// of whole blocks (on its own worker pool) into chunks, two ahead of the
+// record walk; each chunk keeps headroom in front of its data so the walk
+// can put the bytes it still needs (the open family, a partial record)
+// right before the new data without moving the new data.
+struct Chunk {
+    std::vector<uint8_t> buf;       // [kHead headroom][len inflated bytes]
+    size_t len = 0;
+    bool eof = false;               // nothing follows this chunk
+    std::string err;
+};
+
+class Inflater {
+  public:
+    static constexpr size_t kHead = (size_t)8 << 20;
+    static constexpr size_t kWant = (size_t)32 << 20;
+
+    Inflater(FILE *f, int n_threads) : f_(f), pool_(n_threads) {
+        cbuf_.resize((size_t)48 << 20);
+        for (auto &c : chunks_) {
+            c.buf.resize(kHead + kWant + 0x10000);
+            empty_.push_back(&c);
+        }
+        th_ = std::thread([this] { loop(); });
+    }
+    ~Inflater() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    Chunk *next() {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !full_.empty(); });
+        Chunk *c = full_.front();
+        full_.pop_front();
+        return c;
+    }
+    void give_back(Chunk *c) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            empty_.push_back(c);
+        }
+        cv_.notify_all();
+    }
+
+  private:
+    void loop() {
+        for (;;) {
+            Chunk *c;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || !empty_.empty(); });
+                if (stop_) return;
+                c = empty_.front();
+                empty_.pop_front();
+            }
+            fill(*c);
+            const bool last = c->eof || !c->err.empty();
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                full_.push_back(c);
+            }
+            cv_.notify_all();
+            if (last) return;
+        }
+    }
+    void top_up() {
+        std::memmove(cbuf_.data(), cbuf_.data() + cbeg_, cend_ - cbeg_);
+        cend_ -= cbeg_;
+        cbeg_ = 0;
+        while (!file_eof_ && cend_ < cbuf_.size()) {
+            const size_t got = std::fread(cbuf_.data() + cend_, 1, cbuf_.size() - cend_, f_);
+            cend_ += got;
+            if (got == 0) file_eof_ = true;
+        }
+    }
+    // inflate the next run of whole blocks into c (after its headroom)
+    void fill(Chunk &c) {
+        c.len = 0;
+        c.eof = false;
+        c.err.clear();
+        struct Blk { size_t coff, clen, doff; uint32_t isize, crc; };
+        std::vector<Blk> blks;
+        size_t total = 0;
+        // compressed bytes are only moved while no parsed block points into them
+        if (!file_eof_ && cend_ - cbeg_ < cbuf_.size() / 2) top_up();
+        for (;;) {
+            while (cend_ - cbeg_ >= 18 && total + 0x10000 <= kWant) {
+                const uint8_t *h = cbuf_.data() + cbeg_;
+                if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) { c.err = "not a BGZF file"; return; }
+                const size_t xlen = rd16(h + 10);
+                if (cend_ - cbeg_ < 12 + xlen) break;
+                long bsize = -1;
+                for (size_t i = 0; i + 4 <= xlen;) {
+                    const uint8_t *sf = h + 12 + i;
+                    const size_t slen = rd16(sf + 2);
+                    if (sf[0] == 66 && sf[1] == 67 && slen == 2) bsize = rd16(sf + 4);
+                    i += 4 + slen;
+                }
+                if (bsize < 0) { c.err = "BGZF block without BC field"; return; }
+                const size_t blen = (size_t)bsize + 1;
+                if (blen < 12 + xlen + 8) { c.err = "BGZF block size too small"; return; }
+                if (cend_ - cbeg_ < blen) break;
+                Blk b;
+                b.coff = cbeg_ + 12 + xlen;
+                b.clen = blen - 12 - xlen - 8;
+                b.crc = rd32(h + blen - 8);
+                b.isize = rd32(h + blen - 4);
+                if (b.isize > 0x10000) { c.err = "BGZF ISIZE above 64 KiB"; return; }
+                b.doff = Inflater::kHead + total;
+                total += b.isize;
+                blks.push_back(b);
+                cbeg_ += blen;
+            }
+            if (!blks.empty()) break;
+            if (file_eof_) {
+                if (cend_ > cbeg_) { c.err = "truncated BGZF block at the end of the file"; return; }
+                break;
+            }
+            top_up();
+        }
+        uint8_t *dst = c.buf.data();
+        const uint8_t *src = cbuf_.data();
+        const bool ok = pool_.run(blks.size(), [&](size_t i) {
+            const Blk &b = blks[i];
+            if (b.isize == 0) return b.clen <= 2;      // empty block (the EOF marker)
+            size_t got = 0;
+            if (libdeflate_deflate_decompress(tl_dec.get(), src + b.coff, b.clen, dst + b.doff, b.isize, &got) != 0 ||
+                got != b.isize)
+                return false;
+            return libdeflate_crc32(0, dst + b.doff, b.isize) == b.crc;
+        });
+        if (!ok) { c.err = "BGZF block failed to inflate or CRC mismatch"; return; }
+        c.len = total;
+        if (blks.empty() && file_eof_ && cend_ == cbeg_) c.eof = true;
+    }
+
+    FILE *f_;
+    Pool pool_;
+    std::vector<uint8_t> cbuf_;
+    size_t cbeg_ = 0, cend_ = 0;
+    bool file_eof_ = false;
+    Chunk chunks_[3];
+    std::deque<Chunk *> empty_, full_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    bool stop_ = false;
+    std::thread th_;
+};
+
 struct dcr_ingest {
     FILE *f = nullptr;
     dcr_ingest_cfg cfg{};
-    std::unique_ptr<Pool> pool;
-    // compressed input
-    std::vector<uint8_t> cbuf;
-    size_t cbeg = 0, cend = 0;
-    bool file_eof = false;
-    // decompressed window
-    std::vector<uint8_t> win;
+    std::unique_ptr<Pool> pool;          // pack jobs
+    std::unique_ptr<Inflater> infl;
+    // decompressed window: wb[wpos, wend) (a chunk's buffer, or big[] for huge leftovers)
+    const uint8_t *wb = nullptr;
     size_t wpos = 0, wend = 0;
+    Chunk *cur = nullptr;
+    std::vector<uint8_t> big[2];
+    int big_i = 0;
     bool data_eof = false;
     std::vector<uint8_t> header;
     // the open family (passing reads, input order)
@@ -173,86 +330,9 @@ struct dcr_ingest {
     std::vector<Job> jobs;
     std::vector<int> idx_tmp;
 
-    // -- BGZF ----------------------------------------------------------------
-    // Inflate the next run of whole BGZF blocks, appending to the window
-    // after moving [keep, wend) to its front.  Returns false on error.
-    bool refill(size_t keep) {
-        const size_t left = wend - keep;
-        if (keep > 0) {
-            std::memmove(win.data(), win.data() + keep, left);
-            for (auto &r : fam) r.off -= keep;
-            wpos -= keep;
-            wend = left;
-        }
-        const size_t want = (size_t)32 << 20;
-        if (win.size() < wend + want + 0x10000) win.resize(wend + want + 0x10000);
-        struct Blk { size_t coff, clen, doff; uint32_t isize, crc; };
-        std::vector<Blk> blks;
-        size_t total = 0;
-        auto top_up = [&]() {
-            std::memmove(cbuf.data(), cbuf.data() + cbeg, cend - cbeg);
-            cend -= cbeg;
-            cbeg = 0;
-            while (!file_eof && cend < cbuf.size()) {
-                const size_t got = std::fread(cbuf.data() + cend, 1, cbuf.size() - cend, f);
-                cend += got;
-                if (got == 0) file_eof = true;
-            }
-        };
-        // compressed bytes are only moved while no parsed block points into them
-        if (!file_eof && cend - cbeg < cbuf.size() / 2) top_up();
-        for (;;) {
-            while (cend - cbeg >= 18 && total + 0x10000 <= want) {
-                const uint8_t *h = cbuf.data() + cbeg;
-                if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) {
-                    g_err = "not a BGZF file";
-                    return false;
-                }
-                const size_t xlen = rd16(h + 10);
-                if (cend - cbeg < 12 + xlen) break;
-                long bsize = -1;
-                for (size_t i = 0; i + 4 <= xlen;) {
-                    const uint8_t *s = h + 12 + i;
-                    const size_t slen = rd16(s + 2);
-                    if (s[0] == 66 && s[1] == 67 && slen == 2) bsize = rd16(s + 4);
-                    i += 4 + slen;
-                }
-                if (bsize < 0) { g_err = "BGZF block without BC field"; return false; }
-                const size_t blen = (size_t)bsize + 1;
-                if (blen < 12 + xlen + 8) { g_err = "BGZF block size too small"; return false; }
-                if (cend - cbeg < blen) break;
-                Blk b;
-                b.coff = cbeg + 12 + xlen;
-                b.clen = blen - 12 - xlen - 8;
-                b.crc = rd32(h + blen - 8);
-                b.isize = rd32(h + blen - 4);
-                if (b.isize > 0x10000) { g_err = "BGZF ISIZE above 64 KiB"; return false; }
-                b.doff = wend + total;
-                total += b.isize;
-                blks.push_back(b);
-                cbeg += blen;
-            }
-            if (!blks.empty()) break;                   // inflate these; the next refill reads on
-            if (file_eof) {
-                if (cend > cbeg) { g_err = "truncated BGZF block at the end of the file"; return false; }
-                break;
-            }
-            top_up();
-        }
-        const std::vector<Blk> *bp = &blks;
-        const bool ok = pool->run(blks.size(), [&](size_t i) {
-            const Blk &b = (*bp)[i];
-            if (b.isize == 0) return b.clen <= 2;      // empty block (the EOF marker)
-            size_t got = 0;
-            if (libdeflate_deflate_decompress(tl_dec.get(), cbuf.data() + b.coff, b.clen, win.data() + b.doff,
-                                              b.isize, &got) != 0 || got != b.isize)
-                return false;
-            return libdeflate_crc32(0, win.data() + b.doff, b.isize) == b.crc;
-        });
-        if (!ok) { g_err = "BGZF block failed to inflate or CRC mismatch"; return false; }
-        wend += total;
-        if (blks.empty() && file_eof && cend == cbeg) data_eof = true;
-        return true;
+    ~dcr_ingest() {
+        infl.reset();             // stops the inflate thread before the file closes
+        if (f) std::fclose(f);
     }
 
     // make at least n bytes available at wpos (keeping the open family);
@@ -260,9 +340,38 @@ struct dcr_ingest {
     int need(size_t n) {
         while (wend - wpos < n) {
             if (data_eof) return 0;
-            flush_jobs();
+            flush_jobs();                           // the jobs point into the current window
+            Chunk *nx = infl->next();
+            if (!nx->err.empty()) {
+                g_err = nx->err;
+                data_eof = true;
+                return -1;
+            }
             const size_t keep = fam.empty() ? wpos : std::min(wpos, fam.front().off);
-            if (!refill(keep)) return -1;
+            const size_t left = wend - keep;
+            size_t base;
+            const uint8_t *nbuf;
+            if (left <= Inflater::kHead) {
+                base = Inflater::kHead - left;
+                if (left) std::memcpy(nx->buf.data() + base, wb + keep, left);
+                nbuf = nx->buf.data();
+            } else {                                 // a leftover larger than the headroom
+                std::vector<uint8_t> &bg = big[big_i];
+                big_i ^= 1;
+                bg.resize(left + nx->len + 16);
+                std::memcpy(bg.data(), wb + keep, left);
+                std::memcpy(bg.data() + left, nx->buf.data() + Inflater::kHead, nx->len);
+                base = 0;
+                nbuf = bg.data();
+            }
+            for (auto &r : fam) r.off = r.off - keep + base;
+            wpos = wpos - keep + base;
+            wend = base + left + nx->len;
+            wb = nbuf;
+            if (cur) infl->give_back(cur);
+            if (nbuf == nx->buf.data()) cur = nx;
+            else { cur = nullptr; infl->give_back(nx); }
+            if (nx->eof) data_eof = true;
         }
         return 1;
     }
@@ -273,7 +382,7 @@ struct dcr_ingest {
         if (jobs.empty()) return;
         const size_t chunk = 2048;
         const size_t nchunks = (jobs.size() + chunk - 1) / chunk;
-        const uint8_t *w = win.data();
+        const uint8_t *w = wb;
         dcr_host_batch *b = hb;
         pool->run(nchunks, [&](size_t c) {
             const size_t j1 = std::min(jobs.size(), (c + 1) * chunk);
@@ -305,14 +414,14 @@ struct dcr_ingest {
             if (st == 0 && wend > wpos) { g_err = "truncated BAM record at the end of the file"; return -1; }
             return st;
         }
-        const int32_t bs = rdi32(win.data() + wpos);
+        const int32_t bs = rdi32(wb + wpos);
         if (bs < 32) { g_err = "malformed BAM record (block_size < 32)"; return -1; }
         st = need(4 + (size_t)bs);
         if (st <= 0) {
             if (st == 0) g_err = "truncated BAM record at the end of the file";
             return -1;
         }
-        const uint8_t *base = win.data() + wpos;
+        const uint8_t *base = wb + wpos;
         const uint8_t *r = base + 4;
         rc.off = wpos;
         rc.len = 4u + (uint32_t)bs;
@@ -378,7 +487,7 @@ struct dcr_ingest {
         return 1;
     }
 
-    const uint8_t *at(const Rec &r, uint32_t o) const { return win.data() + r.off + o; }
+    const uint8_t *at(const Rec &r, uint32_t o) const { return wb + r.off + o; }
 
     // pass_filters (:1135-1181): 1 pass, 0 excluded, -1 the reference stops (err set)
     int filters(const Rec &r, int &err_kind, std::string &msg) const {
@@ -737,37 +846,33 @@ dcr_ingest *dcr_ingest_open(const char *path, const dcr_ingest_cfg *cfg) {
     ing->f = f;
     ing->cfg = *cfg;
     ing->pool.reset(new Pool(pick_threads(cfg->n_threads)));
-    ing->cbuf.resize((size_t)48 << 20);
+    ing->infl.reset(new Inflater(f, pick_threads(cfg->n_threads)));
     // seed like an unseeded random.Random is not reproducible; callers pass
     // their state with dcr_ingest_set_rng.  Default: random.seed(0).
     for (int i = 0; i < 624; ++i) ing->rng.mt[i] = 0;
     ing->rng.index = 624;
     // header: magic, l_text, text, n_ref, refs
     int st = ing->need(12);
-    if (st <= 0) { std::fclose(f); ing->f = nullptr; if (st == 0) g_err = "empty BAM"; return nullptr; }
-    const uint8_t *h = ing->win.data() + ing->wpos;
-    if (std::memcmp(h, "BAM\1", 4) != 0) { g_err = "not a BAM file"; std::fclose(f); ing->f = nullptr; return nullptr; }
+    if (st <= 0) { if (st == 0) g_err = "empty BAM"; return nullptr; }
+    const uint8_t *h = ing->wb + ing->wpos;
+    if (std::memcmp(h, "BAM\1", 4) != 0) { g_err = "not a BAM file"; return nullptr; }
     const int32_t l_text = rdi32(h + 4);
-    if (l_text < 0 || ing->need(12 + (size_t)l_text) <= 0) { g_err = "truncated BAM header"; std::fclose(f); ing->f = nullptr; return nullptr; }
+    if (l_text < 0 || ing->need(12 + (size_t)l_text) <= 0) { g_err = "truncated BAM header"; return nullptr; }
     size_t p = 8 + (size_t)l_text;
-    const int32_t n_ref = rdi32(ing->win.data() + ing->wpos + p);
+    const int32_t n_ref = rdi32(ing->wb + ing->wpos + p);
     p += 4;
     for (int32_t i = 0; i < n_ref; ++i) {
-        if (ing->need(p + 4) <= 0) { g_err = "truncated BAM header"; std::fclose(f); ing->f = nullptr; return nullptr; }
-        const int32_t ln = rdi32(ing->win.data() + ing->wpos + p);
-        if (ln < 0 || ing->need(p + 8 + (size_t)ln) <= 0) { g_err = "truncated BAM header"; std::fclose(f); ing->f = nullptr; return nullptr; }
+        if (ing->need(p + 4) <= 0) { g_err = "truncated BAM header"; return nullptr; }
+        const int32_t ln = rdi32(ing->wb + ing->wpos + p);
+        if (ln < 0 || ing->need(p + 8 + (size_t)ln) <= 0) { g_err = "truncated BAM header"; return nullptr; }
         p += 8 + (size_t)ln;
     }
-    ing->header.assign(ing->win.data() + ing->wpos, ing->win.data() + ing->wpos + p);
+    ing->header.assign(ing->wb + ing->wpos, ing->wb + ing->wpos + p);
     ing->wpos += p;
     return ing.release();
 }
 
-void dcr_ingest_close(dcr_ingest *ing) {
-    if (!ing) return;
-    if (ing->f) std::fclose(ing->f);
-    delete ing;
-}
+void dcr_ingest_close(dcr_ingest *ing) { delete ing; }
 
 int64_t dcr_ingest_header(dcr_ingest *ing, const uint8_t **bytes) {
     if (!ing || !bytes) return -1;

@@ -84,6 +84,7 @@ struct FastArgs {
     int minbq;                      // single-strand: min_base_quality (masked rows in the table); duplex: -1
     int lo_check;                   // some unmasked quality may lie below fast_qlo: check the bytes
     const uint16_t *llr16;          // [123] per-quality LLR term, 1/16 nat, rounded down
+    int want_info;                  // single-strand: write every read's dcr_read_info (DCR_OPT_READ_INFO)
 };
 
 __global__ void k_prep(dcr_batch in, const dcr_params *P, Workspace ws);

@@ -944,10 +944,13 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
     }
 
     // ---- setup: lane = read
-    int minpos = 0x7fffffff, maxend = -0x7fffffff, up = 0, empty = 0, ins = 0, msum = 0;
+    int minpos = 0x7fffffff, maxend = -0x7fffffff, up = 0, empty = 0, ins = 0, msum = 0, fst = 0;
     ReadRef myrd{};
     for (int c = 0; c < R; c += kWave) {
         const int r = c + lane;
+        const int rst = r < R ? get_read<DUPLEX>(a, rec, r).status : 0;
+        const unsigned long long fm = __ballot(rst != 0);
+        if (!fst && fm) fst = __shfl(rst, __ffsll((long long)fm) - 1);   // the first failing read (:1272-1283)
         if (r < R) {
             const ReadRef rd = get_read<DUPLEX>(a, rec, r);
             if (r < kWave) myrd = rd;
@@ -983,7 +986,8 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
             O.E[rec] = 0.0;
         }
     };
-    if (R == 0 || up) { write_status(DCR_ST_UPSTREAM); return; }
+    if (R == 0) { write_status(DCR_ST_VALUE_ERROR); return; }      // min([]) (:458)
+    if (up) { write_status(DUPLEX ? DCR_ST_UPSTREAM : (DCR_ST_PREP | (fst & 15))); return; }
     if (empty) { write_status(DCR_ST_TYPE_ERROR); return; }     // list(None) at :402
     const int T = maxend - minpos;                                  // :458-459
     if (T > cap) {
@@ -1868,6 +1872,7 @@ __device__ __forceinline__ int read_record(int64_t c, int g0, int R, int *mark, 
 struct RecAgg {
     int minpos, maxend, flags, kind;
     unsigned long long lo, hi;     // kept byte window; lo becomes base_al for fast records
+    unsigned long long fst;        // first failing read: global index << 4 | its status
     int pos0, pad;                 // pos of the record's first read
 };
 
@@ -1899,7 +1904,7 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
         gbeg = 2 * rb;
         gend = 2 * rend;
     }
-    agg[lane] = RecAgg{0x7fffffff, -0x7fffffff, 0, -1, ~0ull, 0ull, 0, 0};
+    agg[lane] = RecAgg{0x7fffffff, -0x7fffffff, 0, -1, ~0ull, 0ull, ~0ull, 0, 0};
     lds_fence();
     // one pass: fold every read into its record, and write the read's word for
     // the fast kernel (relative to the record's first read, so it needs no
@@ -1940,6 +1945,7 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
             atomicMin(&agg[k].minpos, rd.pos);
             atomicMax(&agg[k].maxend, rd.pos + rd.len);
             if (fl) atomicOr(&agg[k].flags, fl);
+            if (rd.status) atomicMin(&agg[k].fst, ((unsigned long long)gr << 4) | (unsigned)(rd.status & 15));
             atomicMin(&agg[k].lo, (unsigned long long)rd.seq_start);
             atomicMax(&agg[k].hi, (unsigned long long)(rd.seq_start + rd.len));
             a.ws.rmeta[gr] = make_uint2(((uint32_t)rd.len & 255u) | (((uint32_t)rd.mapq & 255u) << 8) |
@@ -1959,9 +1965,9 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
         const uint8_t *gq = DUPLEX ? a.ss.qual : a.in.quals;
         const RecAgg g = agg[lane];
         int st = -1;
-        if (R == 0) st = DCR_ST_UPSTREAM;
+        if (R == 0) st = DCR_ST_VALUE_ERROR;         // min([]) in reconstruct_alignment (:458)
         else if (R > kWave) kind = 1;
-        else if (g.flags & 1) st = DCR_ST_UPSTREAM;
+        else if (g.flags & 1) st = DUPLEX ? DCR_ST_UPSTREAM : (DCR_ST_PREP | (int)(g.fst & 15));
         else if (g.flags & 2) st = DCR_ST_TYPE_ERROR;
         else {
             const int T = g.maxend - g.minpos;
@@ -2362,7 +2368,7 @@ __device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &
                 go = go && tl > 0;
             }
         }
-        if (lane < R) {
+        if (lane < R && (a.want_info || tl == 0)) {
             dcr_read_info inf;
             inf.seq_start = m.base_al + y;
             inf.len = tl;
@@ -2374,7 +2380,7 @@ __device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &
         rm.x = (rm.x & ~0xFF00u) | ((uint32_t)tl << 8);
         s.T = wave_max(lane < R ? col + tl : 0);
         if (__ballot(lane < R && tl == 0)) {
-            if (lane == 0) write_status_at(a.O, m.rec, DCR_ST_UPSTREAM);
+            if (lane == 0) write_status_at(a.O, m.rec, DCR_ST_PREP | DCR_ST_INDEX_ERROR);
             s.state = 2;
         }
     }

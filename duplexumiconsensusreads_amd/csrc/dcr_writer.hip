@@ -302,15 +302,11 @@ __global__ __launch_bounds__(256) void k_famfail(FmtArgs A) {
     const int32_t f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= A.n_fam) return;
     int32_t kind = 0, which = -1;
-    // preprocessing: the family's first failing read (:1272-1283)
-    for (int32_t r = A.sub_off[4 * f]; r < A.sub_off[4 * f + 4] && !kind; ++r) {
-        const int32_t st = A.info[r].status;
-        if (st) {
-            kind = st;
-            int k = 0;
-            while (r >= A.sub_off[4 * f + k + 1]) ++k;
-            which = 8 + k;
-        }
+    // preprocessing of every read comes first (:1272-1283): the first
+    // subfamily holding a failing read (DCR_ST_PREP | its status)
+    for (int k = 0; k < 4 && !kind; ++k) {
+        const int st = A.ss.status[4 * f + k];
+        if (st & DCR_ST_PREP) { kind = st & 15; which = 8 + k; }
     }
     auto st_fail = [](int st) { return st != 0 && st != DCR_ST_UPSTREAM; };
     for (int k = 0; k < 4 && !kind; ++k) {
@@ -350,7 +346,13 @@ __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
         __syncthreads();
         dfl::p2_count(s, n, lane);
         __syncthreads();
-        if (lane == 0) dfl::build_codes(s);
+        dfl::p3a_keys(s, lane);
+        __syncthreads();
+        dfl::p3b_rank(s, lane);
+        __syncthreads();
+        if (lane == 0) dfl::p3c_lengths(s);
+        __syncthreads();
+        dfl::p3d_codes(s, lane);
         __syncthreads();
         dfl::p4_bits(s, n, lane);
         __syncthreads();

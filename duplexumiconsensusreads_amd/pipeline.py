@@ -29,6 +29,7 @@ from .batch import OutArrays, pack_families
 from .params import ConsensusParams
 
 STATUS_NAME = {1: "IndexError", 2: "TypeError", 3: "ValueError", 4: "OverflowError", 5: "exit"}
+UPSTREAM, PREP = 6, 0x10       # include/dcr.h DCR_ST_UPSTREAM, DCR_ST_PREP
 
 
 class FamilyExit(Exception):
@@ -125,23 +126,23 @@ def run_batch(results: List[FamilyResult], params: ConsensusParams, backend: Bac
 
 def finish_batch(todo, packed, ss: OutArrays, ds: OutArrays, info):
     """Resolve statuses in the reference's execution order and build records."""
-    rstat = info["status"] if info is not None else np.zeros(packed.n_reads, np.int32)
     for f, fam in enumerate(todo):
-        a, b = packed.sub_off[4 * f], packed.sub_off[4 * f + 4]
         crash = None
-        bad = np.nonzero(rstat[a:b])[0]
-        if len(bad):                                   # preprocess_family (:1272-1283)
-            crash = STATUS_NAME[int(rstat[a + bad[0]])]
+        for k in range(4):                             # preprocess_family (:1272-1283): the first
+            st = int(ss.status[4 * f + k])             # subfamily with a failing read (DCR_ST_PREP | s)
+            if st & PREP:
+                crash = STATUS_NAME[st & 15]
+                break
         if crash is None:
             for k in range(4):                         # single-strand calls in order
                 st = int(ss.status[4 * f + k])
-                if st and st != 6:
+                if st and st != UPSTREAM:
                     crash = STATUS_NAME[st]
                     break
         if crash is None:
             for j in range(2):
                 st = int(ds.status[2 * f + j])
-                if st and st != 6:
+                if st and st != UPSTREAM:
                     crash = STATUS_NAME[st]
                     break
         if crash is not None:

@@ -214,7 +214,7 @@ class DeviceStream:
         so, do = out.dcr_out("ss"), out.dcr_out("ds")
         from . import _lib
         _lib._check(self.lib.dcr_submit(self.ctx._ctx, slot, ctypes.byref(self._b), ctypes.byref(so),
-                                        ctypes.byref(do), out.arr["rs"]["status"].ctypes.data))
+                                        ctypes.byref(do), None))
         self.busy[slot] = True
         return slot
 
@@ -239,7 +239,7 @@ class DeviceStream:
         _lib._check(self.lib.dcr_wait(self.ctx._ctx, slot))
         self.busy[slot] = False
         out = self.outs[slot]
-        return out.fmt_out("ss"), out.fmt_out("ds"), out.arr["rs"]["status"]
+        return out.fmt_out("ss"), out.fmt_out("ds"), None
 
     def close(self):
         for slot in range(self.n_slots):

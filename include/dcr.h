@@ -54,8 +54,14 @@ enum {
     DCR_ST_VALUE_ERROR = 3,    /* ValueError: max() of an empty depth list (:1005)     */
     DCR_ST_OVERFLOW_ERROR = 4, /* OverflowError: quality outside uint8 (:1383)         */
     DCR_ST_EXIT_BADCHAR = 5,   /* sys.exit(1): invalid nucleotide (:582-585)           */
-    DCR_ST_UPSTREAM = 6        /* not computed: an input consensus already failed      */
+    DCR_ST_UPSTREAM = 6,       /* duplex, not computed: an input consensus failed      */
+    DCR_ST_PREP = 0x10         /* single-strand: DCR_ST_PREP | s = the preprocessing of a read
+                                  raised s (the subfamily's first failing read, :1272-1283) */
 };
+
+/* context options (dcr_set_options) */
+#define DCR_OPT_READ_INFO 1    /* every read's dcr_read_info is written (parity tests; costs
+                                  24 B of HBM writes per read); otherwise only failing reads' */
 
 /* Numeric flags (:1432-1469) plus host-built tables.  The tables are built on
  * the host with the reference's own Python arithmetic (params.py), so the
@@ -146,6 +152,7 @@ const char *dcr_last_error(void);
 dcr_ctx *dcr_create(int device, const dcr_params *params);
 void dcr_destroy(dcr_ctx *ctx);
 int dcr_set_params(dcr_ctx *ctx, const dcr_params *params);
+int dcr_set_options(dcr_ctx *ctx, int flags);   /* DCR_OPT_* */
 /* pre-size internal scratch so a timed loop never allocates */
 int dcr_reserve(dcr_ctx *ctx, const dcr_batch *sizes);
 void *dcr_stream(dcr_ctx *ctx);   /* the context's hipStream_t */
@@ -155,7 +162,8 @@ int dcr_run_batch(dcr_ctx *ctx, const dcr_batch *in, dcr_out *ss, dcr_out *ds);
 /* host-pointer batch: stages H2D, runs, D2H; synchronous */
 int dcr_run_batch_host(dcr_ctx *ctx, const dcr_batch *in, dcr_out *ss, dcr_out *ds);
 int dcr_sync(dcr_ctx *ctx);
-/* copy the last batch's per-read preprocessing info (host pointer, n_reads) */
+/* copy the last batch's per-read preprocessing info (host pointer, n_reads);
+   complete only with DCR_OPT_READ_INFO */
 int dcr_read_info_host(dcr_ctx *ctx, dcr_read_info *out, int64_t n_reads);
 /* timing of the last dcr_run_batch (HIP events on the context stream), ms:
    [0] prep, [1] single-strand, [2] duplex, [3] whole batch */

@@ -185,8 +185,8 @@ enum {
 /* First failing processed family in [0, n_fam), or n_fam if none; its
  * DCR_FAIL_* in *kind and where it fails in *which: 0..3 the single-strand
  * consensus of that subfamily, 4..5 the duplex one, 8 + k the preprocessing
- * of a read of subfamily k.  read_status (optional, per read) are the per-read
- * preprocessing statuses (dcr_read_info.status). */
+ * of a read of subfamily k (single-strand status DCR_ST_PREP | s, include/dcr.h).
+ * read_status is unused (kept for the ABI). */
 int32_t dcr_fmt_scan(const dcr_host_batch *hb, const dcr_fmt_out *ss, const dcr_fmt_out *ds,
                      const int32_t *read_status, int32_t n_fam, int32_t *kind, int32_t *which);
 /* Format the two duplex records of processed families [0, n_fam) (records

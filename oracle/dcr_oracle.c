@@ -339,10 +339,12 @@ static void run_family(const dcr_params *P, const dcr_batch *in, dcr_out *ss, dc
         for (int r = 0; r < R; ++r) {
             dcr_read_info tmp;
             prep_read(P, in, a + r, &rd[r], info ? &info[a + r] : &tmp);
-            if ((info ? info[a + r].status : tmp.status) != 0) pre_fail = 1;
+            const int st = info ? info[a + r].status : tmp.status;
+            if (st != 0 && !pre_fail) pre_fail = DCR_ST_PREP | st;   /* the first failing read :1272-1283 */
         }
         int64_t o = in->ss_col_off[s], cap = in->ss_col_off[s + 1] - o;
-        if (pre_fail || R == 0) { memset(&sc[k], 0, sizeof(ocore)); sc[k].status = DCR_ST_UPSTREAM; }
+        if (R == 0) { memset(&sc[k], 0, sizeof(ocore)); sc[k].status = DCR_ST_VALUE_ERROR; }   /* min([]) :458 */
+        else if (pre_fail) { memset(&sc[k], 0, sizeof(ocore)); sc[k].status = pre_fail; }
         else consensus(P, rd, R, cap, &sc[k], ss->seq + o, ss->qual + o, ss->cigar + o, ss->d + o, ss->e + o);
         write_core(ss, s, &sc[k]);
         failed[k] = sc[k].status != 0;

@@ -20,7 +20,7 @@ FIELDS = ("status", "pos", "mapq", "len", "n_cig", "n_de", "D", "M", "E")
 
 @pytest.fixture(scope="module")
 def ctx():
-    c = _lib.Context(ConsensusParams(), device=0)
+    c = _lib.Context(ConsensusParams(), device=0, want_info=True)
     yield c
     c.close()
 

@@ -58,20 +58,31 @@ def run_device_vs_oracle(ctx, packed, params):
     ctx.run_device(db.batch_struct, db.ss_struct, db.ds_struct)
     ctx.sync()
     ss, ds = db.download()
-    info = ctx.read_info(packed.n_reads)
+    info = ctx.read_info(packed.n_reads) if ctx.want_info else None
     del db
     want_ss, want_ds, want_info = dcr_oracle_c.run(packed, params, n_threads=16)
     assert_same_kind("ss", packed.ss_col_off, ss, want_ss)
     assert_same_kind("ds", packed.ds_col_off, ds, want_ds)
-    for k in ("seq_start", "len", "status", "has_ins"):
-        bad = np.nonzero(info[k] != want_info[k])[0]
-        assert len(bad) == 0, f"read info {k} differs at {len(bad)} reads, first {bad[:8]}"
+    if info is not None:
+        for k in ("seq_start", "len", "status", "has_ins"):
+            bad = np.nonzero(info[k] != want_info[k])[0]
+            assert len(bad) == 0, f"read info {k} differs at {len(bad)} reads, first {bad[:8]}"
     return ss, ds
 
 
 @pytest.fixture(scope="module")
 def ctx():
+    # the bench's configuration: per-read info only for failing reads
     c = _lib.Context(ConsensusParams(), device=0)
+    c.want_info = False
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def ctx_info():
+    c = _lib.Context(ConsensusParams(), device=0, want_info=True)
+    c.want_info = True
     yield c
     c.close()
 
@@ -86,3 +97,9 @@ def test_gpu_scale_c2_full_bench_batch(ctx):
 def test_gpu_scale_config_shards(ctx, config, families):
     packed = synth.packed_config(synth.CONFIGS[config], families, seed=23, max_reads=1000)
     run_device_vs_oracle(ctx, packed, ConsensusParams(max_reads=1000))
+
+
+def test_gpu_scale_c3_read_info(ctx_info):
+    """With DCR_OPT_READ_INFO every read's preprocessing info matches too."""
+    packed = synth.packed_config(synth.CONFIGS["C3"], 30_000, seed=29, max_reads=1000)
+    run_device_vs_oracle(ctx_info, packed, ConsensusParams(max_reads=1000))
