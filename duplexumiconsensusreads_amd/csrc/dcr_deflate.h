@@ -65,6 +65,7 @@ struct alignas(16) Shared {
     uint32_t srt_lit[288], srt_dist[32];  // sorted keys, then in-place code lengths
     uint32_t m_lit, m_dist;               // used symbols
     uint32_t next_code[3][16];            // canonical first codes per length: lit, dist, cl
+    uint32_t t0_num[33], t0_cnt[16], t0_clf[19];   // thread-0 scratch (kept out of private memory)
     uint16_t rle[320];                    // header: code-length symbol | extra << 8
     uint32_t n_rle;
     uint32_t hlit, hdist, hclen;
@@ -219,24 +220,26 @@ DFL_HD inline void parse(Shared &s, uint32_t n, int lane, uint32_t lo, uint32_t 
         const bool hashed = p + 4 <= n;
         if (hashed) h = hash4(ld32(s, p));
         if (lim >= 4) {
-            uint32_t cand[8];
-            int nc = 0;
-            const uint32_t set = (h & (kLS - 1)) * 2;
-            cand[nc++] = t[set] ? (uint32_t)t[set] - 1 : kNone;
-            cand[nc++] = t[set + 1] ? (uint32_t)t[set + 1] - 1 : kNone;
-            if (p >= 32768) {
-                cand[nc++] = s.b_min[h];
-                const uint32_t am = s.a_max[h];
-                cand[nc++] = am ? am - 1 : kNone;
-            } else {
-                cand[nc++] = s.a_min[h];
-            }
-            for (uint32_t d = 1; d <= 4; ++d) cand[nc++] = p >= d ? p - d : kNone;
-            for (int i = 0; i < nc; ++i) {
-                const uint32_t c = cand[i];
-                if (c == kNone || c >= p || p - c > 32768) continue;
+            auto tryc = [&](uint32_t c) {
+                if (c == kNone || c >= p || p - c > 32768) return;
                 const uint32_t l = match_len(s, c, p, lim);
                 if (l > best) { best = l; bd = p - c; }
+            };
+            const uint32_t set = (h & (kLS - 1)) * 2;
+            tryc(t[set] ? (uint32_t)t[set] - 1 : kNone);
+            tryc(t[set + 1] ? (uint32_t)t[set + 1] - 1 : kNone);
+            if (p >= 32768) {
+                tryc(s.b_min[h]);
+                const uint32_t am = s.a_max[h];
+                tryc(am ? am - 1 : kNone);
+            } else {
+                tryc(s.a_min[h]);
+            }
+            if (best < 258) {
+                tryc(p >= 1 ? p - 1 : kNone);
+                tryc(p >= 2 ? p - 2 : kNone);
+                tryc(p >= 3 ? p - 3 : kNone);
+                tryc(p >= 4 ? p - 4 : kNone);
             }
         }
         if (hashed) lt_insert(t, h, p);
@@ -347,8 +350,7 @@ DFL_HD inline void mr_lengths(uint32_t *a, int m) {
 // Length-limit code lengths a[0..m) (non-increasing, from mr_lengths) to
 // max_len and hand them to the symbols of keys[0..m) (ascending frequency):
 // the rarest symbols take the longest codes.
-DFL_HD inline void limit_assign(uint32_t *a, const uint32_t *keys, int m, int max_len, uint8_t *len) {
-    uint32_t num[33];
+DFL_HD inline void limit_assign(uint32_t *a, const uint32_t *keys, int m, int max_len, uint8_t *len, uint32_t *num) {
     for (int i = 0; i <= 32; ++i) num[i] = 0;
     for (int i = 0; i < m; ++i) num[a[i] > 32 ? 32 : a[i]]++;
     for (int i = max_len + 1; i <= 32; ++i) { num[max_len] += num[i]; num[i] = 0; }
@@ -368,7 +370,7 @@ DFL_HD inline void limit_assign(uint32_t *a, const uint32_t *keys, int m, int ma
 // Code lengths <= max_len for freq[0..n) (n <= 32) into len[0..n) on one
 // thread; scratch holds 2n words.  At least `min_used` symbols get a code.
 DFL_HD inline void build_lengths_small(const uint32_t *freq, int n, int max_len, uint8_t *len, uint32_t *scratch,
-                                       int min_used) {
+                                       int min_used, uint32_t *num) {
     int m = 0;
     uint32_t *keys = scratch, *f = scratch + n;
     for (int i = 0; i < n; ++i) {
@@ -387,7 +389,7 @@ DFL_HD inline void build_lengths_small(const uint32_t *freq, int n, int max_len,
     }
     for (int i = 0; i < m; ++i) f[i] = (keys[i] >> 9) ? (keys[i] >> 9) : 1;
     mr_lengths(f, m);
-    limit_assign(f, keys, m, max_len, len);
+    limit_assign(f, keys, m, max_len, len, num);
 }
 
 DFL_HD inline uint32_t reverse_bits(uint32_t v, int nb) {
@@ -400,8 +402,7 @@ DFL_HD inline uint32_t reverse_bits(uint32_t v, int nb) {
 #endif
 }
 
-DFL_HD inline void first_codes(const uint8_t *len, int n, uint32_t *next) {
-    uint32_t cnt[16];
+DFL_HD inline void first_codes(const uint8_t *len, int n, uint32_t *next, uint32_t *cnt) {
     for (int l = 0; l < 16; ++l) cnt[l] = 0;
     for (int i = 0; i < n; ++i) cnt[len[i]]++;
     cnt[0] = 0;
@@ -460,17 +461,17 @@ DFL_HD inline void p3c_lengths(Shared &s) {
     uint32_t *f = s.sort_a;
     for (int i = 0; i < ml; ++i) f[i] = s.srt_lit[i] >> 9;
     mr_lengths(f, ml);                               // >= 2 symbols: a literal and end of block
-    limit_assign(f, s.srt_lit, ml, 15, s.lit_len);
+    limit_assign(f, s.srt_lit, ml, 15, s.lit_len, s.t0_num);
     const int md = (int)s.m_dist;
     if (md == 0) s.dist_len[0] = 1;                  // no match: one unused code of length 1
     else if (md == 1) s.dist_len[s.srt_dist[0] & 511] = 1;
     else {
         for (int i = 0; i < md; ++i) f[i] = s.srt_dist[i] >> 9;
         mr_lengths(f, md);
-        limit_assign(f, s.srt_dist, md, 15, s.dist_len);
+        limit_assign(f, s.srt_dist, md, 15, s.dist_len, s.t0_num);
     }
-    first_codes(s.lit_len, 286, s.next_code[0]);
-    first_codes(s.dist_len, 30, s.next_code[1]);
+    first_codes(s.lit_len, 286, s.next_code[0], s.t0_cnt);
+    first_codes(s.dist_len, 30, s.next_code[1], s.t0_cnt);
     int nlit = 286;
     while (nlit > 257 && !s.lit_len[nlit - 1]) --nlit;
     int ndist = 30;
@@ -480,7 +481,7 @@ DFL_HD inline void p3c_lengths(Shared &s) {
     // run-length code the lengths (symbols 16 / 17 / 18)
     const int N = nlit + ndist;
     auto L = [&](int i) -> uint8_t { return i < nlit ? s.lit_len[i] : s.dist_len[i - nlit]; };
-    uint32_t clf[19];
+    uint32_t *clf = s.t0_clf;
     for (int i = 0; i < 19; ++i) clf[i] = 0;
     uint32_t nr = 0;
     for (int i = 0; i < N;) {
@@ -499,8 +500,8 @@ DFL_HD inline void p3c_lengths(Shared &s) {
         }
     }
     s.n_rle = nr;
-    build_lengths_small(clf, 19, 7, s.cl_len, s.sort_a, 2);
-    first_codes(s.cl_len, 19, s.next_code[2]);
+    build_lengths_small(clf, 19, 7, s.cl_len, s.sort_a, 2, s.t0_num);
+    first_codes(s.cl_len, 19, s.next_code[2], s.t0_cnt);
     int ncl = 19;
     while (ncl > 4 && !s.cl_len[kClOrder[ncl - 1]]) --ncl;
     s.hclen = (uint32_t)(ncl - 4);

@@ -142,7 +142,27 @@ struct Rec {
     uint16_t l_mi, l_rx;             // string lengths
     uint8_t mi_type, rx_type;        // tag type codes ('Z' expected)
     uint16_t l_code;                 // MI prefix before the first '/'
+    int8_t pf;                       // pass_filters: 1 pass, 0 excluded, -1 the reference stops
+    uint8_t fmsg;                    // which stop (kFilterMsg)
+    uint8_t perr;                    // malformed record (kParseErr), 0 ok
+    uint8_t eqx;                     // CIGAR still holds '=' / 'X' after the trim (:374-375)
+    int64_t end_kept;                // pos + length after clip removal (the T bound)
+    char code[24];                   // the MI prefix, when l_code <= 24 (else read from the window)
+    char rx[32];                     // RX, when l_rx <= 32
 };
+
+const char *const kParseErr[] = {"", "malformed BAM record (l_seq < 0)",
+                                 "malformed BAM record (fields past block_size)",
+                                 "malformed BAM aux field (unterminated string)", "malformed BAM aux array",
+                                 "malformed BAM aux field type", "malformed BAM aux field (past block_size)"};
+struct FilterMsg { int kind; const char *msg; };
+const FilterMsg kFilterMsg[] = {
+    {0, ""},
+    {DCR_ERR_EXIT, "ERROR: family code tag (MI) not found in file"},
+    {DCR_ERR_EXIT, "ERROR: family code tag (RX) not found in file"},
+    {DCR_ERR_TYPE, "argument of type 'NoneType' is not iterable"},
+    {DCR_ERR_EXIT, "ERROR: unexpected symbols (P, N, B, *) were found in CIGAR strings."},
+    {DCR_ERR_EXIT, "ERROR: softclips (S) found in the middle of the read."}};
 
 struct Job {
     size_t rec;         // window offset of the record
@@ -407,24 +427,12 @@ struct dcr_ingest {
     }
 
     // -- record parse ------------------------------------------------------------
-    // 1 ok, 0 end of data, -1 error (g_err)
-    int parse(Rec &rc) {
-        int st = need(4);
-        if (st <= 0) {
-            if (st == 0 && wend > wpos) { g_err = "truncated BAM record at the end of the file"; return -1; }
-            return st;
-        }
-        const int32_t bs = rdi32(wb + wpos);
-        if (bs < 32) { g_err = "malformed BAM record (block_size < 32)"; return -1; }
-        st = need(4 + (size_t)bs);
-        if (st <= 0) {
-            if (st == 0) g_err = "truncated BAM record at the end of the file";
-            return -1;
-        }
-        const uint8_t *base = wb + wpos;
+    // the fields of the whole record at window offset off (0 ok, else kParseErr)
+    int parse_at(size_t off, Rec &rc) const {
+        const uint8_t *base = wb + off;
         const uint8_t *r = base + 4;
-        rc.off = wpos;
-        rc.len = 4u + (uint32_t)bs;
+        rc.off = off;
+        rc.len = 4u + (uint32_t)rdi32(base);
         rc.tid = rdi32(r);
         rc.pos = rdi32(r + 4);
         const uint32_t l_rn = r[8];
@@ -432,12 +440,13 @@ struct dcr_ingest {
         rc.n_cig = rd16(r + 12);
         rc.flag = rd16(r + 14);
         rc.l_seq = rdi32(r + 16);
-        if (rc.l_seq < 0) { g_err = "malformed BAM record (l_seq < 0)"; return -1; }
+        rc.perr = 0;
+        if (rc.l_seq < 0) return 1;
         rc.o_cig = 4 + 32 + l_rn;
         rc.o_seq = rc.o_cig + 4u * rc.n_cig;
         rc.o_qual = rc.o_seq + (uint32_t)((rc.l_seq + 1) >> 1);
         size_t p = rc.o_qual + (size_t)rc.l_seq;
-        if (p > rc.len) { g_err = "malformed BAM record (fields past block_size)"; return -1; }
+        if (p > rc.len) return 2;
         rc.o_mi = rc.o_rx = 0;
         rc.l_mi = rc.l_rx = 0;
         rc.mi_type = rc.rx_type = 0;
@@ -452,21 +461,21 @@ struct dcr_ingest {
                 case 'd': e = v + 8; break;
                 case 'Z': case 'H': {
                     const void *z = std::memchr(base + v, 0, rc.len - v);
-                    if (!z) { g_err = "malformed BAM aux field (unterminated string)"; return -1; }
+                    if (!z) return 3;
                     e = (size_t)((const uint8_t *)z - base) + 1;
                     break;
                 }
                 case 'B': {
-                    if (v + 5 > rc.len) { g_err = "malformed BAM aux array"; return -1; }
+                    if (v + 5 > rc.len) return 4;
                     const uint8_t sub = base[v];
                     const uint32_t n = rd32(base + v + 1);
                     size_t es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
                     e = v + 5 + es * (size_t)n;
                     break;
                 }
-                default: g_err = "malformed BAM aux field type"; return -1;
+                default: return 5;
             }
-            if (e > rc.len) { g_err = "malformed BAM aux field (past block_size)"; return -1; }
+            if (e > rc.len) return 6;
             // the first occurrence, as pysam's get_tag (bam_aux_get)
             if (t0 == 'M' && t1 == 'I' && !rc.mi_type) {
                 rc.mi_type = ty;
@@ -484,38 +493,94 @@ struct dcr_ingest {
             const void *sl = std::memchr(base + rc.o_mi, '/', rc.l_mi);
             if (sl) rc.l_code = (uint16_t)((const uint8_t *)sl - (base + rc.o_mi));
         }
+        if (rc.mi_type == 'Z' && rc.l_code <= sizeof rc.code) std::memcpy(rc.code, base + rc.o_mi, rc.l_code);
+        if (rc.rx_type == 'Z' && rc.l_rx <= sizeof rc.rx) std::memcpy(rc.rx, base + rc.o_rx, rc.l_rx);
+        int msg = 0;
+        rc.pf = (int8_t)filters(rc, msg);
+        rc.fmsg = (uint8_t)msg;
+        rc.end_kept = (int64_t)rc.pos + rc.l_seq - clip_total(rc);
+        rc.eqx = rc.pf == 1 && eqx_after_trim(rc);
+        return 0;
+    }
+
+    // parsed records ahead of the walk: rq[rq_pos, rq_n)
+    std::vector<Rec> rq;
+    std::vector<size_t> rq_off;
+    size_t rq_pos = 0, rq_n = 0;
+
+    // scan the next complete records of the window (block_size chain) and
+    // parse them on the pool; 1 some, 0 end of data, -1 error (g_err)
+    int prefetch_records() {
+        constexpr size_t kRQ = 16384;
+        if (rq.size() < kRQ) { rq.resize(kRQ); rq_off.resize(kRQ); }
+        rq_pos = rq_n = 0;
+        size_t n = 0;
+        for (;;) {
+            size_t p = wpos;
+            while (n < kRQ && wend - p >= 4) {
+                __builtin_prefetch(wb + p + 4096);
+                __builtin_prefetch(wb + p + 4096 + 64);
+                __builtin_prefetch(wb + p + 4096 + 128);
+                __builtin_prefetch(wb + p + 4096 + 192);
+                const int32_t bs = rdi32(wb + p);
+                if (bs < 32) {
+                    if (n == 0) { g_err = "malformed BAM record (block_size < 32)"; return -1; }
+                    break;
+                }
+                if (wend - p - 4 < (size_t)bs) break;
+                rq_off[n++] = p;
+                p += 4 + (size_t)bs;
+            }
+            if (n > 0) break;
+            int st;
+            if (wend - wpos >= 4) {
+                const int32_t bs = rdi32(wb + wpos);
+                if (bs < 32) { g_err = "malformed BAM record (block_size < 32)"; return -1; }
+                st = need(4 + (size_t)bs);
+            } else {
+                st = need(4);
+            }
+            if (st < 0) return -1;
+            if (st == 0) {
+                if (wend > wpos) { g_err = "truncated BAM record at the end of the file"; return -1; }
+                return 0;
+            }
+        }
+        const size_t chunk = 512;
+        pool->run((n + chunk - 1) / chunk, [&](size_t c) {
+            const size_t e = std::min(n, (c + 1) * chunk);
+            for (size_t i = c * chunk; i < e; ++i) rq[i].perr = (uint8_t)parse_at(rq_off[i], rq[i]);
+            return true;
+        });
+        rq_n = n;
         return 1;
     }
 
     const uint8_t *at(const Rec &r, uint32_t o) const { return wb + r.off + o; }
 
     // pass_filters (:1135-1181): 1 pass, 0 excluded, -1 the reference stops (err set)
-    int filters(const Rec &r, int &err_kind, std::string &msg) const {
-        if (!r.mi_type) { err_kind = DCR_ERR_EXIT; msg = "ERROR: family code tag (MI) not found in file"; return -1; }
-        if (!r.rx_type) { err_kind = DCR_ERR_EXIT; msg = "ERROR: family code tag (RX) not found in file"; return -1; }
-        if (r.n_cig == 0) { err_kind = DCR_ERR_TYPE; msg = "argument of type 'NoneType' is not iterable"; return -1; }
+    int filters(const Rec &r, int &msg) const {
+        if (!r.mi_type) { msg = 1; return -1; }
+        if (!r.rx_type) { msg = 2; return -1; }
+        if (r.n_cig == 0) { msg = 3; return -1; }
         const uint8_t *c = at(r, r.o_cig);
         for (uint32_t i = 0; i < r.n_cig; ++i) {
             const uint32_t op = rd32(c + 4 * i) & 15;
-            if (op == 3 || op == 6 || op >= 9) {
-                err_kind = DCR_ERR_EXIT;
-                msg = "ERROR: unexpected symbols (P, N, B, *) were found in CIGAR strings.";
-                return -1;
-            }
+            if (op == 3 || op == 6 || op >= 9) { msg = 4; return -1; }
         }
         for (uint32_t i = 1; i + 1 < r.n_cig; ++i)
-            if ((rd32(c + 4 * i) & 15) == 4) {
-                err_kind = DCR_ERR_EXIT;
-                msg = "ERROR: softclips (S) found in the middle of the read.";
-                return -1;
-            }
+            if ((rd32(c + 4 * i) & 15) == 4) { msg = 5; return -1; }
         const uint16_t fl = r.flag;
         return (fl & 1) && (fl & 2) && !(fl & 4) && !(fl & 8) && !(fl & 2048) && !(fl & 512) &&
                (int)r.mapq >= cfg.min_map_quality;
     }
 
+    const char *code_of(const Rec &r) const {
+        return r.l_code <= sizeof r.code ? r.code : (const char *)at(r, r.o_mi);
+    }
+    const char *rx_of(const Rec &r) const { return r.l_rx <= sizeof r.rx ? r.rx : (const char *)at(r, r.o_rx); }
     bool same_code(const Rec &a, const Rec &b) const {
-        return a.l_code == b.l_code && std::memcmp(at(a, a.o_mi), at(b, b.o_mi), a.l_code) == 0;
+        return a.l_code == b.l_code && std::memcmp(code_of(a), code_of(b), a.l_code) == 0;
     }
 
     // -- the family -------------------------------------------------------------
@@ -597,7 +662,7 @@ struct dcr_ingest {
     int complete_family() {
         dcr_host_batch *b = hb;
         const Rec &r0 = fam.front();
-        const std::string code((const char *)at(r0, r0.o_mi), r0.l_code);
+        const std::string code(code_of(r0), r0.l_code);
         // capacity check first, with the unsampled family as the bound
         int64_t nb = 0, nc = 0;
         for (const Rec &r : fam) { nb += r.l_seq; nc += r.n_cig; }
@@ -616,7 +681,7 @@ struct dcr_ingest {
         }
         // check_family_UMIs (:100-113)
         if (r0.rx_type != 'Z') return stop(DCR_ERR_ATTRIBUTE, "'int' object has no attribute 'split'");
-        const char *rx0 = (const char *)at(r0, r0.o_rx);
+        const char *rx0 = rx_of(r0);
         const std::string umi1(rx0, r0.l_rx);
         const size_t d1 = umi1.find('-');
         if (d1 == std::string::npos) return stop(DCR_ERR_INDEX, "list index out of range");
@@ -625,7 +690,7 @@ struct dcr_ingest {
                                  "-" + umi1.substr(0, d1);
         for (const Rec &r : fam) {
             if (r.rx_type != 'Z') return stop(DCR_ERR_ATTRIBUTE, "RX tag is not a string");
-            const char *x = (const char *)at(r, r.o_rx);
+            const char *x = rx_of(r);
             const bool eq1 = r.l_rx == umi1.size() && std::memcmp(x, umi1.data(), r.l_rx) == 0;
             const bool eq2 = r.l_rx == umi2.size() && std::memcmp(x, umi2.data(), r.l_rx) == 0;
             if (!eq1 && !eq2)
@@ -704,11 +769,11 @@ struct dcr_ingest {
                 jobs.push_back(Job{r.off, b->n_bases, b->n_cigar});
                 b->n_bases += r.l_seq;
                 b->n_cigar += r.n_cig;
-                const int64_t end = (int64_t)r.pos + r.l_seq - clip_total(r);
+                const int64_t end = r.end_kept;
                 if (first || r.pos < mn[k]) mn[k] = r.pos;
                 if (first || end > mx[k]) mx[k] = end;
                 first = false;
-                if (eqx < 0x7fff && eqx_after_trim(r)) ++eqx;
+                if (eqx < 0x7fff && r.eqx) ++eqx;
             }
             b->fam_eqx[4 * f + k] = (uint16_t)eqx;
             b->sub_off[4 * f + k + 1] = b->n_reads;
@@ -786,26 +851,26 @@ struct dcr_ingest {
     int walk() {
         dcr_host_batch *b = hb;
         for (;;) {
-            Rec r;
-            const int st = parse(r);
-            if (st < 0) return -1;
-            if (st == 0) {
-                // end of input: the last family (:1610-1631)
-                if (!started) return stop(DCR_ERR_TYPE, "'NoneType' object is not subscriptable");
-                if (!fam.empty()) {
-                    const int c = complete_family();
-                    if (c <= 0) return c;
-                    fam.clear();
+            if (rq_pos == rq_n) {
+                const int st = prefetch_records();
+                if (st < 0) return -1;
+                if (st == 0) {
+                    // end of input: the last family (:1610-1631)
+                    if (!started) return stop(DCR_ERR_TYPE, "'NoneType' object is not subscriptable");
+                    if (!fam.empty()) {
+                        const int c = complete_family();
+                        if (c <= 0) return c;
+                        fam.clear();
+                    }
+                    finished = true;
+                    b->end_kind = DCR_END_EOF;
+                    return 1;
                 }
-                finished = true;
-                b->end_kind = DCR_END_EOF;
-                return 1;
             }
-            int ek = 0;
-            std::string msg;
-            const int pf = filters(r, ek, msg);
-            if (pf < 0) return stop(ek, msg);
-            if (pf == 0) {
+            const Rec &r = rq[rq_pos];
+            if (r.perr) { g_err = kParseErr[r.perr]; return -1; }
+            if (r.pf < 0) return stop(kFilterMsg[r.fmsg].kind, kFilterMsg[r.fmsg].msg);
+            if (r.pf == 0) {
                 // excluded read -> _filteredreads.bam (:1523-1528)
                 if (b->n_side_exc + r.len > b->cap_side) {
                     if (b->n_tab == 0 && b->n_side_exc == 0) return fail_capacity("a record exceeds cap_side");
@@ -815,7 +880,8 @@ struct dcr_ingest {
                 b->n_side_exc += r.len;
                 ++excluded;
                 ++records;
-                wpos += r.len;
+                wpos = r.off + r.len;
+                ++rq_pos;
                 continue;
             }
             if (r.mi_type != 'Z') return stop(DCR_ERR_ATTRIBUTE, "'int' object has no attribute 'split'");
@@ -828,7 +894,8 @@ struct dcr_ingest {
             ++records;
             started = true;
             fam.push_back(r);
-            wpos += r.len;
+            wpos = r.off + r.len;
+            ++rq_pos;
         }
     }
 };

@@ -77,3 +77,44 @@ def test_cli_case_matches_reference_main_gpu(tmp_path, name):
     args = cli.parse_args(["-i", "x.bam", *CASES[name]["args"]])
     be = cli.default_backend(ConsensusParams.from_args(args))
     assert_case(run_case(tmp_path, name, be, 300), name)
+
+
+def _ascii_case(tmp_path, backend):
+    """With --max_base_quality >= 95 a single-strand quality of 95 or more
+    makes the duplex aq / bq tag text non-ASCII; pysam's set_tags encodes Z
+    tags with force_bytes(ascii) and raises UnicodeEncodeError in the duplex
+    make_consensus_read (:1384).  Parity unpinned: the goldens come from a
+    pysam stand-in (tests/golden/pysam_shim.py), so this pins our reading of
+    pysam, not a reference run.  Families before the failing one are written."""
+    from duplexumiconsensusreads_amd import synth
+    path = str(tmp_path / "q.bam")
+    cfg = synth.SynthConfig("t", 6, sub_size="fixed8", fixed_size=1, seed=3, low_mapq_frac=0.0)
+    fams = synth.family_splits(cfg)
+    for k, fam in enumerate(fams):             # one read per subfamily: its quality is the consensus's
+        for sub in fam:
+            for r in sub:
+                r.query_qualities = [30 if k < 3 else 99] * len(r.query_sequence)
+    from duplexumiconsensusreads_amd.bam import AlignmentFile, BamHeader
+    hdr = BamHeader("@HD\tVN:1.6\n@SQ\tSN:chr1\tLN:248956422\n", ["chr1"], [248956422])
+    with AlignmentFile(path, "wb", header=hdr) as out:
+        for fam in fams:
+            for sub in fam:
+                for r in sub:
+                    out.write(r)
+    out = str(tmp_path / "cons.bam")
+    with pytest.raises(UnicodeEncodeError):
+        cli.main(["-i", path, "-o", out, "--max_base_quality", "100"], backend=backend, rng=random.Random(1))
+    with bam.AlignmentFile(out, "rb") as f:
+        recs = list(f)
+    assert len(recs) == 6          # the three families before the first Q99 family
+    assert all(max(r.query_qualities) <= 94 for r in recs)
+
+
+def test_cli_quality_tags_outside_ascii_raise_like_pysam(tmp_path):
+    _ascii_case(tmp_path, dcr_oracle_c.run)
+
+
+@pytest.mark.gpu
+def test_cli_quality_tags_outside_ascii_raise_like_pysam_gpu(tmp_path):
+    from duplexumiconsensusreads_amd.params import ConsensusParams
+    _ascii_case(tmp_path, cli.default_backend(ConsensusParams(max_base_quality=100)))
