@@ -12,6 +12,7 @@
 #include <cstddef>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "dcr_internal.h"
 #include "dcr_deflate.h"
@@ -773,6 +774,8 @@ int dcr_submit_write(dcr_ctx *c, int slot, const dcr_batch *h, const dcr_wmeta *
     const size_t o_bsz = take(8 * (size_t)(nbm + 1)), o_boff = take(8 * (size_t)(nbm + 1));
     const size_t o_comp = take((size_t)nbm * dfl::kSlot);
     const size_t o_tot = take(8 * 4);
+    const unsigned gd = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nbm, (int64_t)c->n_cu * c->dfl_blocks));
+    const size_t o_tok = take((size_t)gd * dfl::kTokWords * 4);
     if (wo > S.wbuf.cap) HIP_TRY(S.wbuf.ensure(wo + wo / 8));
     char *wb = (char *)S.wbuf.p;
     // H2D: inputs and writer metadata on the copy stream
@@ -824,8 +827,7 @@ int dcr_submit_write(dcr_ctx *c, int slot, const dcr_batch *h, const dcr_wmeta *
         HIP_TRY(hipMemsetAsync(A.rec_off, 0, 8, c->stream));
     }
     int64_t *bsz = (int64_t *)(wb + o_bsz);
-    dcrw::DflArgs D{A.stream, A.rec_off + 2 * F, (uint8_t *)(wb + o_slots), bsz};
-    const unsigned gd = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nbm, (int64_t)c->n_cu * c->dfl_blocks));
+    dcrw::DflArgs D{A.stream, A.rec_off + 2 * F, (uint8_t *)(wb + o_slots), bsz, (uint32_t *)(wb + o_tok), nullptr};
     hipLaunchKernelGGL(dcrw::k_deflate, dim3(gd), dim3(dfl::kT), sizeof(dfl::Shared), c->stream, D);
     HIP_TRY(hipGetLastError());
     size_t tb = std::max(scan1, scan2);
@@ -886,6 +888,55 @@ int dcr_slot_fetch(dcr_ctx *c, int slot, int what, int64_t off, int64_t n, void 
     } else {
         return fail(DCR_EARG, "what must be 0 (record bytes), 1 (record offsets) or 2 (BGZF blocks)");
     }
+    return DCR_OK;
+}
+
+// diagnostic (not in include/dcr.h): k_deflate alone over n host bytes with
+// per-phase s_memtime cycle totals (summed over workgroups) and the HIP-event
+// time; returns the compressed bytes in *comp_bytes
+int dcr_deflate_probe(dcr_ctx *c, const uint8_t *host, int64_t n, unsigned long long *stamps10, float *ms,
+                      int64_t *comp_bytes) {
+    if (!c || !host || n <= 0 || !stamps10 || !ms || !comp_bytes) return fail(DCR_EARG, "bad argument");
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t nb = (n + dfl::kMaxIn - 1) / dfl::kMaxIn;
+    uint8_t *d_in = nullptr, *d_slots = nullptr;
+    int64_t *d_n = nullptr, *d_sizes = nullptr;
+    unsigned long long *d_st = nullptr;
+    uint32_t *d_tok = nullptr;
+    HIP_TRY(hipMalloc(&d_in, (size_t)n));
+    HIP_TRY(hipMalloc(&d_slots, (size_t)nb * dfl::kSlot));
+    HIP_TRY(hipMalloc(&d_n, 8));
+    HIP_TRY(hipMalloc(&d_sizes, 8 * (size_t)nb));
+    HIP_TRY(hipMalloc(&d_st, 8 * 10));
+    const unsigned gd = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nb, (int64_t)c->n_cu * c->dfl_blocks));
+    HIP_TRY(hipMalloc(&d_tok, (size_t)gd * dfl::kTokWords * 4));
+    HIP_TRY(hipMemcpy(d_in, host, (size_t)n, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_n, &n, 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemset(d_st, 0, 80));
+    dcrw::DflArgs D{d_in, d_n, d_slots, d_sizes, d_tok, d_st};
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, c->stream));
+    hipLaunchKernelGGL(dcrw::k_deflate, dim3(gd), dim3(dfl::kT), sizeof(dfl::Shared), c->stream, D);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(e1, c->stream));
+    HIP_TRY(hipEventSynchronize(e1));
+    HIP_TRY(hipEventElapsedTime(ms, e0, e1));
+    HIP_TRY(hipMemcpy(stamps10, d_st, 80, hipMemcpyDeviceToHost));
+    std::vector<int64_t> sz((size_t)nb);
+    HIP_TRY(hipMemcpy(sz.data(), d_sizes, 8 * (size_t)nb, hipMemcpyDeviceToHost));
+    int64_t tot = 0;
+    for (int64_t v : sz) tot += v;
+    *comp_bytes = tot;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(d_in);
+    (void)hipFree(d_slots);
+    (void)hipFree(d_n);
+    (void)hipFree(d_sizes);
+    (void)hipFree(d_st);
+    (void)hipFree(d_tok);
     return DCR_OK;
 }
 

@@ -14,14 +14,20 @@
 //       half and latest in the first half (LDS atomics)
 //   P2  each lane greedily parses its contiguous sub-block (256 sub-blocks per
 //       block; matches end at the sub-block end) against those candidates and
-//       distances 1..4, counting literal/length and distance symbols
-//   P3  thread 0: Huffman code lengths (in-place minimum-redundancy code of
-//       Moffat & Katajainen, lengths limited to 15 / 7), canonical codes, the
-//       run-length-coded header; every lane: the CRC32 of its sub-block
-//   P4  each lane parses again and counts its bits; exclusive scan
-//   P5  each lane parses a third time and writes its bits (word atomics on
-//       the zeroed output slot); thread 0 writes header, EOB, BGZF framing
-// The parse is deterministic, so the three passes see the same tokens.
+//       distances 1..4, counting literal/length and distance symbols and
+//       keeping its tokens (one word per match, literals by run length) in a
+//       per-workgroup token buffer; every lane: the CRC32 of its sub-block
+//   P3  symbol ranks (all lanes), then thread 0: Huffman code lengths
+//       (in-place minimum-redundancy code of Moffat & Katajainen, lengths
+//       limited to 15 / 7) and the run-length-coded header; canonical codes
+//   P4  each lane replays its tokens and counts its bits; exclusive scan,
+//       CRC combine, stored-or-compressed decision
+//   P5  each lane replays its tokens and writes its bits (plain stores for
+//       the words it owns, atomic or for the one or two it shares with its
+//       neighbours, which the scan zeroed); lane 0 writes the gzip / BGZF
+//       header and the Huffman header ahead of its tokens, the last lane
+//       end of block, CRC32 and ISIZE after its own.  A stored block (when
+//       that is smaller) is written with plain byte stores instead.
 #pragma once
 #include <stdint.h>
 #include <string.h>
@@ -30,6 +36,12 @@
 #define DFL_HD __host__ __device__
 #else
 #define DFL_HD
+#endif
+
+#if defined(__clang__)
+#define DFL_UNROLL _Pragma("unroll")
+#else
+#define DFL_UNROLL
 #endif
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -48,19 +60,33 @@ constexpr uint32_t kNone = 0xffffffffu;
 constexpr uint32_t kSlot = 65536;         // output slot bytes (one BGZF block at most)
 constexpr uint32_t kMaxDeflate = kSlot - 26;
 constexpr int kLS = 32;                   // lane-private recency table: sets x 2 ways
+// tokens per lane: <= 63 matches (>= 4 bytes each in <= 255 bytes) and the
+// tail literal run; entry e of lane l at tok[e * kT + l]:
+//   bit 31 tail | bits 23..30 literal run before | 15..22 length - 4 | 0..14 distance - 1
+constexpr int kTokE = 64;
+constexpr uint32_t kTokWords = (uint32_t)kTokE * kT;
 
 struct alignas(16) Shared {
-    uint8_t in[kMaxIn + 16];
-    uint32_t a_min[kHN], a_max[kHN], b_min[kHN];   // positions (a_max: position + 1, 0 none)
-    uint16_t lt[kT][2 * kLS];             // per lane: latest positions + 1 per hash set (2 ways)
+    uint8_t in[kMaxIn + 32];              // zero padding: match_len reads past the end
+    union {
+        struct {
+            uint32_t a_min[kHN], a_max[kHN], b_min[kHN];   // positions (a_max: position + 1, 0 none)
+            uint16_t lt[kT][2 * kLS];     // per lane: latest positions + 1 per hash set (2 ways)
+        };
+        uint32_t stage[(3 * kHN * 4 + kT * 2 * kLS * 2) / 4];   // P5: the compressed member (after P2)
+    };
     uint32_t lit_freq[288], dist_freq[32];
     uint8_t lit_len[288], dist_len[32], cl_len[19];
     uint16_t lit_code[288], dist_code[32], cl_code[19];   // bit-reversed (LSB-first) codes
     uint32_t lane_bits[kT];
     uint32_t lane_off[kT];
     uint32_t lane_crc[kT];
+    uint32_t wave_sum[kT / 64], wave_crc[kT / 64];   // device scan
     uint32_t extra_bits;                  // extra bits of all matches (pass P2)
-    uint32_t sort_a[320];                 // scratch of the small (code-length code) build
+    uint32_t sort_a[320];                 // literal/length frequencies by rank, then code lengths; scratch
+    uint32_t sort_d[32];                  // the same for distances
+    uint32_t num_lit[33], num_dist[33];   // codes per length (length-limited)
+    uint32_t last_lit, last_dist;         // highest symbol with a code
     uint32_t key_lit[288], key_dist[32];  // (freq << 9 | symbol), 0 = unused; then sorted ascending
     uint32_t srt_lit[288], srt_dist[32];  // sorted keys, then in-place code lengths
     uint32_t m_lit, m_dist;               // used symbols
@@ -71,6 +97,7 @@ struct alignas(16) Shared {
     uint32_t hlit, hdist, hclen;
     uint32_t hdr_bits, body_bits;
     uint32_t stored;
+    uint32_t use_stage;                   // the member is assembled in stage[] (LDS)
     uint32_t crc;
 };
 
@@ -136,16 +163,15 @@ DFL_HD inline uint32_t multmodp(uint32_t a, uint32_t b) {
     }
     return p;
 }
-// x^(n * 2^3) mod P: the register shift of n zero bytes
+// x^(8 * 2^k) mod P, k = 0..15 (reflected), by repeated squaring of x^8
+DFL_CONST uint32_t kX8Pow2[16] = {0x00800000u, 0x00008000u, 0xedb88320u, 0xb1e6b092u, 0xa06a2517u, 0xed627daeu,
+                                  0x88d14467u, 0xd7bbfe6au, 0xec447f11u, 0x8e7ea170u, 0x6427800eu, 0x4d47bae0u,
+                                  0x09fe548fu, 0x83852d0fu, 0x30362f1au, 0x7b5a9cc3u};
+// x^(8n) mod P (n < 65536): the register shift of n zero bytes
 DFL_HD inline uint32_t x8nmodp(uint32_t n) {
-    // x^(2^k) mod P for k = 3.. computed by squaring (k starts at 3: one byte)
-    uint32_t sq = 1u << 23;        // x^8  (x^(2^3)) in the reflected representation
     uint32_t p = 1u << 31;         // 1
-    while (n) {
-        if (n & 1) p = multmodp(sq, p);
-        n >>= 1;
-        sq = multmodp(sq, sq);
-    }
+    for (int k = 0; n; ++k, n >>= 1)
+        if (n & 1) p = multmodp(kX8Pow2[k], p);
     return p;
 }
 
@@ -170,11 +196,42 @@ DFL_HD inline void lane_range(uint32_t n, int lane, uint32_t &lo, uint32_t &hi) 
     if (hi > n) hi = n;
 }
 
+// length of the common prefix of in[c..] and in[p..], at most lim (reads
+// stay below p + lim + 20 <= n + 20, inside the zero padding of in[])
 DFL_HD inline uint32_t match_len(const Shared &s, uint32_t c, uint32_t p, uint32_t lim) {
+#if DFL_DEVICE
+    // 16 bytes per step: four new aligned LDS dwords per side issued
+    // together (one LDS round trip), byte funnel shifts, the first
+    // differing byte from the lowest set bit of the xor
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(s.in);
+    uint32_t ia = c >> 2, ib = p >> 2;
+    const uint32_t sa = c & 3, sb = p & 3;
+    uint32_t a0 = w[ia], b0 = w[ib], l = 0;
+    while (l < lim) {
+        const uint32_t a1 = w[ia + 1], a2 = w[ia + 2], a3 = w[ia + 3], a4 = w[ia + 4];
+        const uint32_t b1 = w[ib + 1], b2 = w[ib + 2], b3 = w[ib + 3], b4 = w[ib + 4];
+        const uint32_t x0 = __builtin_amdgcn_alignbyte(a1, a0, sa) ^ __builtin_amdgcn_alignbyte(b1, b0, sb);
+        const uint32_t x1 = __builtin_amdgcn_alignbyte(a2, a1, sa) ^ __builtin_amdgcn_alignbyte(b2, b1, sb);
+        const uint32_t x2 = __builtin_amdgcn_alignbyte(a3, a2, sa) ^ __builtin_amdgcn_alignbyte(b3, b2, sb);
+        const uint32_t x3 = __builtin_amdgcn_alignbyte(a4, a3, sa) ^ __builtin_amdgcn_alignbyte(b4, b3, sb);
+        if (x0 | x1 | x2 | x3) {
+            const uint32_t k = x0 ? 0 : x1 ? 4 : x2 ? 8 : 12;
+            const uint32_t x = x0 ? x0 : x1 ? x1 : x2 ? x2 : x3;
+            l += k + ((uint32_t)__builtin_ctz(x) >> 3);
+            break;
+        }
+        l += 16;
+        ia += 4;
+        ib += 4;
+        a0 = a4;
+        b0 = b4;
+    }
+    return l < lim ? l : lim;
+#else
     uint32_t l = 0;
-    while (l + 4 <= lim && ld32(s, c + l) == ld32(s, p + l)) l += 4;
     while (l < lim && s.in[c + l] == s.in[p + l]) ++l;
     return l;
+#endif
 }
 
 DFL_HD inline int len_sym(uint32_t len) {   // 0..28 (symbol 257 + i)
@@ -201,10 +258,20 @@ DFL_HD inline void lt_insert(uint16_t *t, uint32_t h, uint32_t p) {
     t[set] = (uint16_t)(p + 1);
 }
 
-// greedy parse of [lo, hi): v.lit(byte) / v.match(len, dist).  Candidates:
-// the lane's two latest positions with the same hash set (its table holds
-// the previous sub-block and its own positions so far), the earliest /
-// latest block positions with the same hash (P1), and distances 1..4.
+// greedy parse of [lo, hi): v.lit(byte) / v.match(len, dist).  Candidates
+// for position p, in this order: the lane's two latest positions with the
+// same hash set (its table holds the previous sub-block and its own
+// positions so far), the earliest / latest block positions with the same
+// hash (P1), and distances 1..4; the first longest match wins.
+// Positions inside a match are not inserted into the lane's table: lanes
+// of a wave would wait for the longest match of every step (measured: a
+// quarter of the kernel), and the table keeps older, equally useful
+// positions instead (slightly better ratio on record streams).
+//
+// Per position the candidate positions are loaded together and their first
+// four bytes compared together (one LDS round trip each), so a literal costs
+// three round trips; only candidates that match >= 4 bytes are extended, in
+// candidate order, skipping any that cannot beat the best so far.
 template <class V>
 DFL_HD inline void parse(Shared &s, uint32_t n, int lane, uint32_t lo, uint32_t hi, V &v) {
     uint16_t *t = s.lt[lane];
@@ -214,39 +281,45 @@ DFL_HD inline void parse(Shared &s, uint32_t n, int lane, uint32_t lo, uint32_t 
         if (q + 4 <= n) lt_insert(t, hash4(ld32(s, q)), q);
     uint32_t p = lo;
     while (p < hi) {
-        uint32_t best = 0, bd = 0;
         const uint32_t lim = (hi - p) < 258 ? (hi - p) : 258;
-        uint32_t h = 0;
         const bool hashed = p + 4 <= n;
-        if (hashed) h = hash4(ld32(s, p));
+        const uint32_t vp = ld32(s, p);
+        const uint32_t h = hashed ? hash4(vp) : 0;
+        const uint32_t set = (h & (kLS - 1)) * 2;
+        uint32_t best = 0, bd = 0;
+        const uint32_t t0 = t[set], t1 = t[set + 1];
         if (lim >= 4) {
-            auto tryc = [&](uint32_t c) {
-                if (c == kNone || c >= p || p - c > 32768) return;
-                const uint32_t l = match_len(s, c, p, lim);
-                if (l > best) { best = l; bd = p - c; }
-            };
-            const uint32_t set = (h & (kLS - 1)) * 2;
-            tryc(t[set] ? (uint32_t)t[set] - 1 : kNone);
-            tryc(t[set + 1] ? (uint32_t)t[set + 1] - 1 : kNone);
+            uint32_t c[8];
+            c[0] = t0 ? t0 - 1 : kNone;
+            c[1] = t1 ? t1 - 1 : kNone;
             if (p >= 32768) {
-                tryc(s.b_min[h]);
+                c[2] = s.b_min[h];
                 const uint32_t am = s.a_max[h];
-                tryc(am ? am - 1 : kNone);
+                c[3] = am ? am - 1 : kNone;
             } else {
-                tryc(s.a_min[h]);
+                c[2] = s.a_min[h];
+                c[3] = kNone;
             }
-            if (best < 258) {
-                tryc(p >= 1 ? p - 1 : kNone);
-                tryc(p >= 2 ? p - 2 : kNone);
-                tryc(p >= 3 ? p - 3 : kNone);
-                tryc(p >= 4 ? p - 4 : kNone);
+DFL_UNROLL
+            for (int k = 1; k <= 4; ++k) c[3 + k] = p >= (uint32_t)k ? p - (uint32_t)k : kNone;
+            uint32_t ok = 0;
+DFL_UNROLL
+            for (int i = 0; i < 8; ++i)
+                if (c[i] != kNone && c[i] < p && p - c[i] <= 32768 && ld32(s, c[i]) == vp) ok |= 1u << i;
+DFL_UNROLL
+            for (int i = 0; i < 8; ++i) {
+                if (!((ok >> i) & 1) || best >= lim) continue;
+                if (best && s.in[c[i] + best] != s.in[p + best]) continue;   // not longer than best
+                const uint32_t l = 4 + match_len(s, c[i] + 4, p + 4, lim - 4);
+                if (l > best) { best = l; bd = p - c[i]; }
             }
         }
-        if (hashed) lt_insert(t, h, p);
+        if (hashed) {                                       // lt_insert(t, h, p)
+            t[set + 1] = (uint16_t)t0;
+            t[set] = (uint16_t)(p + 1);
+        }
         if (best >= 4) {
             v.match(best, bd);
-            for (uint32_t q = p + 1; q < p + best; ++q)
-                if (q + 4 <= n) lt_insert(t, hash4(ld32(s, q)), q);
             p += best;
         } else {
             v.lit(s.in[p]);
@@ -267,6 +340,42 @@ struct CountV {            // P2: symbol histogram, extra bits
     }
 };
 
+struct TokV {              // P2: the lane's tokens (kTokE layout)
+    uint32_t *t;
+    int lane;
+    uint32_t e = 0, run = 0;
+    DFL_HD void lit(uint8_t) { ++run; }
+    DFL_HD void match(uint32_t len, uint32_t d) {
+        t[e * kT + lane] = (run << 23) | ((len - 4) << 15) | (d - 1);
+        ++e;
+        run = 0;
+    }
+    DFL_HD void finish() { t[e * kT + lane] = (1u << 31) | (run << 23); }
+};
+
+struct CountTokV {         // P2: both
+    CountV c;
+    TokV t;
+    DFL_HD void lit(uint8_t b) { c.lit(b); t.lit(b); }
+    DFL_HD void match(uint32_t len, uint32_t d) { c.match(len, d); t.match(len, d); }
+};
+
+// the tokens of a lane again, from the token buffer
+template <class V>
+DFL_HD inline void replay(const Shared &s, const uint32_t *t, int lane, uint32_t lo, V &v) {
+    uint32_t p = lo;
+    for (int e = 0; e < kTokE; ++e) {
+        const uint32_t x = t[e * kT + lane];
+        const uint32_t run = (x >> 23) & 255;
+        for (uint32_t q = 0; q < run; ++q) v.lit(s.in[p + q]);
+        p += run;
+        if (x >> 31) break;
+        const uint32_t len = ((x >> 15) & 255) + 4;
+        v.match(len, (x & 0x7fff) + 1);
+        p += len;
+    }
+}
+
 struct BitsV {             // P4: bits of a lane's tokens
     const Shared &s;
     uint32_t bits = 0;
@@ -277,27 +386,37 @@ struct BitsV {             // P4: bits of a lane's tokens
     }
 };
 
-// LSB-first bit writer over a zeroed word array; words that may be shared
-// with a neighbour are or-ed atomically
+// LSB-first bit writer over a word array.  A word shared with the previous
+// writer (first word, start not word-aligned) or the next one (last word,
+// unless own_last) is or-ed atomically into a word zeroed beforehand; the
+// words in between belong to this writer alone and are stored.
 struct BitOut {
     uint32_t *w;
     uint64_t acc = 0;
-    uint32_t nacc = 0;      // bits in acc
+    uint32_t nacc;          // bits in acc
     uint32_t word;          // index of acc's first word
-    DFL_HD BitOut(uint32_t *words, uint32_t bitpos) : w(words), word(bitpos >> 5) { nacc = bitpos & 31; }
+    bool first = true, shared_first, own_last;
+    DFL_HD BitOut(uint32_t *words, uint32_t bitpos, bool own_last_word)
+        : w(words), nacc(bitpos & 31), word(bitpos >> 5), shared_first((bitpos & 31) != 0), own_last(own_last_word) {}
+    DFL_HD uint32_t pos() const { return word * 32 + nacc; }
     DFL_HD void put(uint32_t v, uint32_t nb) {
         if (!nb) return;
         acc |= (uint64_t)v << nacc;
         nacc += nb;
         if (nacc >= 32) {
-            aor(&w[word], (uint32_t)acc);
+            if (first && shared_first) aor(&w[word], (uint32_t)acc);
+            else w[word] = (uint32_t)acc;
+            first = false;
             ++word;
             acc >>= 32;
             nacc -= 32;
         }
     }
     DFL_HD void flush() {
-        if (nacc) aor(&w[word], (uint32_t)acc);
+        if (nacc) {
+            if ((first && shared_first) || !own_last) aor(&w[word], (uint32_t)acc);
+            else w[word] = (uint32_t)acc;
+        }
         acc = 0;
         nacc = 0;
     }
@@ -367,6 +486,31 @@ DFL_HD inline void limit_assign(uint32_t *a, const uint32_t *keys, int m, int ma
         for (uint32_t c = 0; c < num[l]; ++c) len[keys[k++] & 511] = (uint8_t)l;
 }
 
+// The counting half of limit_assign: codes per length, limited to max_len
+// with the Kraft sum restored (num[0..32]).
+DFL_HD inline void limit_counts(const uint32_t *a, int m, int max_len, uint32_t *num) {
+    for (int i = 0; i <= 32; ++i) num[i] = 0;
+    for (int i = 0; i < m; ++i) num[a[i] > 32 ? 32 : a[i]]++;
+    for (int i = max_len + 1; i <= 32; ++i) { num[max_len] += num[i]; num[i] = 0; }
+    uint32_t total = 0;
+    for (int i = max_len; i > 0; --i) total += num[i] << (max_len - i);
+    while (total != (1u << max_len)) {
+        num[max_len]--;
+        for (int i = max_len - 1; i > 0; --i)
+            if (num[i]) { num[i]--; num[i + 1] += 2; break; }
+        total--;
+    }
+}
+// ... and the assigning half for one rank (0 = rarest symbol)
+DFL_HD inline uint8_t len_of_rank(const uint32_t *num, int max_len, uint32_t r) {
+    uint32_t k = 0;
+    for (int l = max_len; l >= 1; --l) {
+        k += num[l];
+        if (r < k) return (uint8_t)l;
+    }
+    return 0;
+}
+
 // Code lengths <= max_len for freq[0..n) (n <= 32) into len[0..n) on one
 // thread; scratch holds 2n words.  At least `min_used` symbols get a code.
 DFL_HD inline void build_lengths_small(const uint32_t *freq, int n, int max_len, uint8_t *len, uint32_t *scratch,
@@ -423,14 +567,16 @@ DFL_HD inline uint16_t code_of(const uint8_t *len, int i, const uint32_t *next) 
 
 // P3a (all lanes): symbol keys and their ranks (sorted ascending by (freq, symbol))
 DFL_HD inline void p3a_keys(Shared &s, int lane) {
-    if (lane == 0) { s.lit_freq[256] = 1; s.m_lit = 0; s.m_dist = 0; }   // end of block
+    if (lane == 0) { s.lit_freq[256] = 1; s.m_lit = 0; s.m_dist = 0; s.last_lit = 0; s.last_dist = 0; }   // end of block
     for (int i = lane; i < 288; i += kT) {
         const uint32_t f = (i < 286) ? (i == 256 ? 1u : s.lit_freq[i]) : 0u;
         s.key_lit[i] = f ? ((f << 9) | (uint32_t)i) : 0u;
+        s.lit_len[i] = 0;
     }
     if (lane < 32) {
         const uint32_t f = lane < 30 ? s.dist_freq[lane] : 0u;
         s.key_dist[lane] = f ? ((f << 9) | (uint32_t)lane) : 0u;
+        s.dist_len[lane] = 0;
     }
 }
 DFL_HD inline void p3b_rank(Shared &s, int lane) {
@@ -440,6 +586,7 @@ DFL_HD inline void p3b_rank(Shared &s, int lane) {
         uint32_t r = 0;
         for (int j = 0; j < 288; ++j) { const uint32_t o = s.key_lit[j]; r += (o != 0) & (o < k); }
         s.srt_lit[r] = k;
+        s.sort_a[r] = k >> 9;
         aadd(&s.m_lit, 1);
     }
     if (lane < 32) {
@@ -448,34 +595,61 @@ DFL_HD inline void p3b_rank(Shared &s, int lane) {
             uint32_t r = 0;
             for (int j = 0; j < 32; ++j) { const uint32_t o = s.key_dist[j]; r += (o != 0) & (o < k); }
             s.srt_dist[r] = k;
+            s.sort_d[r] = k >> 9;
             aadd(&s.m_dist, 1);
         }
     }
 }
 
-// P3c (thread 0): code lengths, first codes, the run-length-coded header
-DFL_HD inline void p3c_lengths(Shared &s) {
-    for (int i = 0; i < 288; ++i) s.lit_len[i] = 0;
-    for (int i = 0; i < 32; ++i) s.dist_len[i] = 0;
-    const int ml = (int)s.m_lit;
-    uint32_t *f = s.sort_a;
-    for (int i = 0; i < ml; ++i) f[i] = s.srt_lit[i] >> 9;
-    mr_lengths(f, ml);                               // >= 2 symbols: a literal and end of block
-    limit_assign(f, s.srt_lit, ml, 15, s.lit_len, s.t0_num);
-    const int md = (int)s.m_dist;
-    if (md == 0) s.dist_len[0] = 1;                  // no match: one unused code of length 1
-    else if (md == 1) s.dist_len[s.srt_dist[0] & 511] = 1;
-    else {
-        for (int i = 0; i < md; ++i) f[i] = s.srt_dist[i] >> 9;
-        mr_lengths(f, md);
-        limit_assign(f, s.srt_dist, md, 15, s.dist_len, s.t0_num);
+// P3c1: the two trees at once, literal/length on lane 0 and distance on the
+// first lane of the second wave: code lengths by rank, codes per length
+constexpr int kDistLane = kT > 64 ? 64 : 0;
+DFL_HD inline void p3c_trees(Shared &s, int lane) {
+    if (lane == 0) {
+        const int ml = (int)s.m_lit;                 // >= 2: a literal and end of block
+        mr_lengths(s.sort_a, ml);
+        limit_counts(s.sort_a, ml, 15, s.num_lit);
     }
-    first_codes(s.lit_len, 286, s.next_code[0], s.t0_cnt);
-    first_codes(s.dist_len, 30, s.next_code[1], s.t0_cnt);
-    int nlit = 286;
-    while (nlit > 257 && !s.lit_len[nlit - 1]) --nlit;
-    int ndist = 30;
-    while (ndist > 1 && !s.dist_len[ndist - 1]) --ndist;
+    if (lane == kDistLane) {
+        const int md = (int)s.m_dist;
+        if (md <= 1) {                               // one code of length 1 (unused when md == 0)
+            for (int i = 0; i <= 32; ++i) s.num_dist[i] = 0;
+            s.num_dist[1] = 1;
+        } else {
+            mr_lengths(s.sort_d, md);
+            limit_counts(s.sort_d, md, 15, s.num_dist);
+        }
+    }
+}
+// P3c2 (all lanes): every symbol's length from its rank (the rarest take the
+// longest codes), the highest coded symbols
+DFL_HD inline void p3c_assign(Shared &s, int lane) {
+    const uint32_t ml = s.m_lit, md = s.m_dist;
+    for (uint32_t r = (uint32_t)lane; r < ml; r += kT) {
+        const uint32_t sym = s.srt_lit[r] & 511;
+        s.lit_len[sym] = len_of_rank(s.num_lit, 15, r);
+        amax(&s.last_lit, sym);
+    }
+    if (lane == 0 && md == 0) s.dist_len[0] = 1;
+    if ((uint32_t)lane < md) {
+        const uint32_t sym = s.srt_dist[lane] & 511;
+        s.dist_len[sym] = len_of_rank(s.num_dist, 15, (uint32_t)lane);
+        amax(&s.last_dist, sym);
+    }
+}
+
+DFL_HD inline void first_codes_from_counts(const uint32_t *num, uint32_t *next) {
+    uint32_t c = 0;
+    next[0] = 0;
+    for (int l = 1; l < 16; ++l) { c = (c + (l > 1 ? num[l - 1] : 0)) << 1; next[l] = c; }
+}
+
+// P3c3 (thread 0): first codes, the run-length-coded header and its code
+DFL_HD inline void p3c_header(Shared &s) {
+    first_codes_from_counts(s.num_lit, s.next_code[0]);
+    first_codes_from_counts(s.num_dist, s.next_code[1]);
+    const int nlit = s.last_lit + 1 > 257 ? (int)s.last_lit + 1 : 257;
+    const int ndist = (int)s.last_dist + 1;
     s.hlit = (uint32_t)(nlit - 257);
     s.hdist = (uint32_t)(ndist - 1);
     // run-length code the lengths (symbols 16 / 17 / 18)
@@ -536,15 +710,32 @@ DFL_HD inline void write_header(const Shared &s, BitOut &o) {
     }
 }
 
-// or `nb` (<= 4) little-endian bytes of v at byte offset `at` of a zeroed word array
-DFL_HD inline void or_bytes(uint32_t *w, uint32_t at, uint32_t v, int nb) {
-    for (int i = 0; i < nb; ++i) {
-        const uint32_t b = (v >> (8 * i)) & 0xff, a = at + (uint32_t)i;
-        aor(&w[a >> 2], b << (8 * (a & 3)));
-    }
+// `nb` (<= 4) little-endian bytes of v at byte offset `at` (byte stores)
+DFL_HD inline void put_bytes(uint32_t *w, uint32_t at, uint32_t v, int nb) {
+    uint8_t *o = reinterpret_cast<uint8_t *>(w);
+    for (int i = 0; i < nb; ++i) o[at + (uint32_t)i] = (uint8_t)(v >> (8 * i));
+}
+
+// gzip member header with the BGZF extra field: 1f 8b 08 04 | mtime 0 |
+// xfl 0 | os ff | xlen 6 | 'B' 'C' 2 0 | BSIZE (member bytes - 1)
+DFL_HD inline void put_gzip_header(BitOut &o, uint32_t bsize) {
+    o.put(0x04088b1fu, 32);
+    o.put(0, 32);
+    o.put(0xff00u, 16);
+    o.put(6, 16);
+    o.put(0x00024342u, 32);
+    o.put(bsize, 16);
 }
 
 // ---- the phases (lane = thread index) -----------------------------------------
+// stored-or-compressed decision once the bits are known (any one lane)
+DFL_HD inline void decide(Shared &s, uint32_t n, uint32_t end_bits) {
+    s.body_bits = end_bits - 144 + s.lit_len[256];
+    const uint32_t dbytes = (s.body_bits + 7) / 8;
+    s.stored = (dbytes > kMaxDeflate || dbytes > n + 5) ? 1u : 0u;
+    s.use_stage = (!s.stored && dbytes + 26 <= sizeof(s.stage)) ? 1u : 0u;
+}
+
 DFL_HD inline void p0_clear(Shared &s, int lane) {
     for (int i = lane; i < kHN; i += kT) { s.a_min[i] = kNone; s.b_min[i] = kNone; s.a_max[i] = 0; }
     for (int i = lane; i < 288; i += kT) s.lit_freq[i] = 0;
@@ -560,73 +751,93 @@ DFL_HD inline void p1_hash(Shared &s, uint32_t n, int lane) {
         else amin(&s.b_min[h], p);
     }
 }
-DFL_HD inline void p2_count(Shared &s, uint32_t n, int lane) {
+DFL_HD inline void p2_count(Shared &s, uint32_t n, int lane, uint32_t *tok) {
     uint32_t lo, hi;
     lane_range(n, lane, lo, hi);
-    CountV v{s};
+    CountTokV v{CountV{s}, TokV{tok, lane}};
     parse(s, n, lane, lo, hi, v);
-    if (v.extra) aadd(&s.extra_bits, v.extra);
+    v.t.finish();
+    if (v.c.extra) aadd(&s.extra_bits, v.c.extra);
     // CRC32 register of the sub-block (no init / final xor), shifted past the rest
     uint32_t c = 0;
     for (uint32_t p = lo; p < hi; ++p) c = crc_byte((c ^ s.in[p]) & 0xff) ^ (c >> 8);
     s.lane_crc[lane] = (hi > lo) ? multmodp(x8nmodp(n - hi), c) : 0;
 }
-DFL_HD inline void p4_bits(Shared &s, uint32_t n, int lane) {
+DFL_HD inline void p4_bits(Shared &s, uint32_t n, int lane, const uint32_t *tok) {
     uint32_t lo, hi;
     lane_range(n, lane, lo, hi);
     BitsV v{s};
-    parse(s, n, lane, lo, hi, v);
+    replay(s, tok, lane, lo, v);
     s.lane_bits[lane] = v.bits;
 }
-// thread 0 between P4 and P5: offsets, stored decision, CRC
-DFL_HD inline void p4_scan(Shared &s, uint32_t n) {
-    uint32_t acc = 3 * 8 * 6 + s.hdr_bits;    // deflate data begins at byte 18 of the slot
-    for (int l = 0; l < kT; ++l) { s.lane_off[l] = acc; acc += s.lane_bits[l]; }
-    s.body_bits = acc - 144 + s.lit_len[256];
-    const uint32_t dbytes = (s.body_bits + 7) / 8;
-    s.stored = (dbytes > kMaxDeflate || dbytes > n + 5) ? 1u : 0u;
+// between P4 and P5, sequential form (the host emulation; the kernel runs
+// the same scan across the workgroup): bit offsets (deflate data begins at
+// byte 18 of the member), stored decision, CRC; zeroes the words two lanes
+// share, in both possible destinations (stage[] and the global slot)
+DFL_HD inline void p4_scan(Shared &s, uint32_t n, uint32_t *out) {
+    uint32_t acc = 3 * 8 * 6 + s.hdr_bits;
+    for (int l = 0; l < kT; ++l) {
+        s.lane_off[l] = acc;
+        if (l && (acc & 31)) {
+            out[acc >> 5] = 0;
+            if ((acc >> 5) < sizeof(s.stage) / 4) s.stage[acc >> 5] = 0;
+        }
+        acc += s.lane_bits[l];
+    }
+    decide(s, n, acc);
     uint32_t c = multmodp(x8nmodp(n), 0xffffffffu);
     for (int l = 0; l < kT; ++l) c ^= s.lane_crc[l];
     s.crc = ~c;
 }
-DFL_HD inline void p5_emit(Shared &s, uint32_t n, int lane, uint32_t *out) {
-    if (s.stored) {
-        // stored block: BFINAL=1 BTYPE=00, LEN, NLEN, raw bytes (byte-aligned after the 3 bits)
-        uint32_t lo, hi;
-        lane_range(n, lane, lo, hi);
-        for (uint32_t p = lo; p < hi; ++p) or_bytes(out, 18 + 5 + p, s.in[p], 1);
-        return;
-    }
+// P5: into stage[] when use_stage (copied out by p6_copy), else into out
+DFL_HD inline void p5_emit(Shared &s, uint32_t n, int lane, const uint32_t *tok, uint32_t *out) {
     uint32_t lo, hi;
     lane_range(n, lane, lo, hi);
-    BitOut o(out, s.lane_off[lane]);
+    if (s.use_stage) out = s.stage;
+    if (s.stored) {
+        // stored block: BFINAL=1 BTYPE=00, LEN, NLEN, raw bytes (byte-aligned after the 3 bits)
+        uint8_t *o = reinterpret_cast<uint8_t *>(out) + 18 + 5;
+        for (uint32_t p = lo; p < hi; ++p) o[p] = s.in[p];
+        return;
+    }
+    BitOut o(out, lane == 0 ? 0 : s.lane_off[lane], lane == kT - 1);
+    if (lane == 0) {
+        put_gzip_header(o, (s.body_bits + 7) / 8 + 25);
+        write_header(s, o);
+    }
     EmitV v{s, o};
-    parse(s, n, lane, lo, hi, v);
-    if (lane == kT - 1) o.put(s.lit_code[256], s.lit_len[256]);
+    replay(s, tok, lane, lo, v);
+    if (lane == kT - 1) {
+        o.put(s.lit_code[256], s.lit_len[256]);
+        o.put(0, (8 - (o.pos() & 7)) & 7);
+        o.put(s.crc, 32);
+        o.put(n, 32);
+    }
     o.flush();
 }
-// thread 0 after P5: header bits and the BGZF framing
+// after P5 (all lanes): a member assembled in stage[] to the slot, one
+// coalesced word per lane per step
+DFL_HD inline void p6_copy(const Shared &s, int lane, uint32_t *out) {
+    if (!s.use_stage) return;
+    const uint32_t words = ((s.body_bits + 7) / 8 + 26 + 3) / 4;
+    for (uint32_t i = (uint32_t)lane; i < words; i += kT) out[i] = s.stage[i];
+}
+
+// thread 0 after P5: the member size; a stored block's framing
 DFL_HD inline uint32_t p6_frame(const Shared &s, uint32_t n, uint32_t *out) {
-    uint32_t dbytes;
-    if (s.stored) {
-        dbytes = 5 + n;
-        or_bytes(out, 18, 1, 1);
-        or_bytes(out, 19, n, 2);
-        or_bytes(out, 21, ~n & 0xffff, 2);
-    } else {
-        BitOut o(out, 144);
-        write_header(s, o);
-        o.flush();
-        dbytes = (s.body_bits + 7) / 8;
-    }
-    // 1f 8b 08 04 | mtime 0 | xfl 0 | os ff | xlen 6 | 'B' 'C' 2 0 | BSIZE
-    or_bytes(out, 0, 0x04088b1fu, 4);
-    or_bytes(out, 8, 0xff00u, 2);
-    or_bytes(out, 10, 6, 2);
-    or_bytes(out, 12, 0x00024342u, 4);
-    or_bytes(out, 16, dbytes + 25, 2);
-    or_bytes(out, 18 + dbytes, s.crc, 4);
-    or_bytes(out, 22 + dbytes, n, 4);
+    if (!s.stored) return (s.body_bits + 7) / 8 + 26;
+    const uint32_t dbytes = 5 + n;
+    put_bytes(out, 0, 0x04088b1fu, 4);
+    put_bytes(out, 4, 0, 4);
+    put_bytes(out, 8, 0xff00u, 2);
+    put_bytes(out, 10, 6, 2);
+    put_bytes(out, 12, 0x00024342u, 4);
+    put_bytes(out, 16, dbytes + 25, 2);
+    put_bytes(out, 18, 1, 1);
+    put_bytes(out, 19, n, 2);
+    put_bytes(out, 21, ~n & 0xffff, 2);
+    put_bytes(out, 18 + dbytes, s.crc, 4);
+    put_bytes(out, 22 + dbytes, n, 4);
     return dbytes + 26;
 }
 

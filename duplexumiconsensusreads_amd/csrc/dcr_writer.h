@@ -30,6 +30,8 @@ struct DflArgs {
     const int64_t *stream_bytes;    // device scalar (rec_off[2F])
     uint8_t *slots;                 // 64 KiB per block
     int64_t *sizes;                 // per block (0 past the last block)
+    uint32_t *tok;                  // dfl::kTokWords per workgroup of the grid
+    unsigned long long *stamps;     // diagnostic (dcr_deflate_probe): s_memtime cycles per phase, or null
 };
 
 struct CompactArgs {

@@ -327,6 +327,34 @@ __global__ __launch_bounds__(256) void k_famfail(FmtArgs A) {
     A.ds_len_out[2 * f + 1] = A.ds.len[2 * f + 1];
 }
 
+// dfl::p4_scan across the workgroup: wave scans of the lanes' bit counts,
+// xor of their CRC registers; zeroes the words two lanes share
+__device__ __forceinline__ void p4_scan_wg(dfl::Shared &s, uint32_t n, int lane, uint32_t *slot) {
+    const uint32_t b = s.lane_bits[lane];
+    const uint32_t inc = wave_incl_scan(b);
+    uint32_t cx = s.lane_crc[lane];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) cx ^= __shfl_xor(cx, d, kW);
+    const int w = lane >> 6;
+    if ((lane & (kW - 1)) == kW - 1) s.wave_sum[w] = inc;
+    if ((lane & (kW - 1)) == 0) s.wave_crc[w] = cx;
+    __syncthreads();
+    uint32_t base = 3 * 8 * 6 + s.hdr_bits;
+    for (int k = 0; k < w; ++k) base += s.wave_sum[k];
+    const uint32_t off = base + inc - b;
+    s.lane_off[lane] = off;
+    if (lane && (off & 31)) {
+        slot[off >> 5] = 0;
+        if ((off >> 5) < sizeof(s.stage) / 4) s.stage[off >> 5] = 0;
+    }
+    if (lane == dfl::kT - 1) {
+        dfl::decide(s, n, off + b);
+        uint32_t c = dfl::multmodp(dfl::x8nmodp(n), 0xffffffffu);
+        for (int k = 0; k < dfl::kT / kW; ++k) c ^= s.wave_crc[k];
+        s.crc = ~c;
+    }
+}
+
 // one workgroup (256 lanes) per BGZF block of the record stream
 __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
     extern __shared__ __align__(16) uint8_t smem[];
@@ -334,35 +362,77 @@ __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
     const int lane = threadIdx.x;
     const int64_t total = *D.stream_bytes;
     const int64_t nb = (total + dfl::kMaxIn - 1) / dfl::kMaxIn;
+    const bool st = D.stamps != nullptr;
+    uint32_t *tok = D.tok + (size_t)blockIdx.x * dfl::kTokWords;
+    uint64_t t[12] = {0}, t0 = 0;
+    auto stamp = [&](int k) {
+        if (st && lane == 0) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            t[k] += now - t0;
+            t0 = now;
+        }
+    };
     for (int64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        if (st && lane == 0) t0 = __builtin_amdgcn_s_memtime();
         const int64_t off = b * (int64_t)dfl::kMaxIn;
         const uint32_t n = (uint32_t)((total - off) < (int64_t)dfl::kMaxIn ? (total - off) : dfl::kMaxIn);
         uint32_t *slot = reinterpret_cast<uint32_t *>(D.slots + b * (int64_t)dfl::kSlot);
-        for (uint32_t i = lane; i < n + 16; i += dfl::kT) s.in[i] = i < n ? D.stream[off + i] : 0;
-        for (uint32_t i = lane; i < dfl::kSlot / 16; i += dfl::kT) reinterpret_cast<uint4 *>(slot)[i] = uint4{0, 0, 0, 0};
+        // stage the block as dwords (block starts are dword-aligned; the
+        // record stream's allocation is padded), zero bytes past n
+        {
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(D.stream + off);
+            uint32_t *dst = reinterpret_cast<uint32_t *>(s.in);
+            const uint32_t nw = (n + 3) / 4, pw = (uint32_t)sizeof(s.in) / 4;
+            for (uint32_t i = lane; i < pw; i += dfl::kT) {
+                uint32_t v = 0;
+                if (i < nw) {
+                    v = src[i];
+                    const uint32_t rem = n - 4 * i;
+                    if (rem < 4) v &= (1u << (8 * rem)) - 1;
+                }
+                dst[i] = v;
+            }
+        }
         dfl::p0_clear(s, lane);
         __syncthreads();
+        stamp(0);
         dfl::p1_hash(s, n, lane);
         __syncthreads();
-        dfl::p2_count(s, n, lane);
+        stamp(1);
+        dfl::p2_count(s, n, lane, tok);
         __syncthreads();
+        stamp(2);
         dfl::p3a_keys(s, lane);
         __syncthreads();
         dfl::p3b_rank(s, lane);
         __syncthreads();
-        if (lane == 0) dfl::p3c_lengths(s);
+        stamp(3);
+        dfl::p3c_trees(s, lane);
         __syncthreads();
+        dfl::p3c_assign(s, lane);
+        __syncthreads();
+        if (lane == 0) dfl::p3c_header(s);
+        __syncthreads();
+        stamp(4);
         dfl::p3d_codes(s, lane);
         __syncthreads();
-        dfl::p4_bits(s, n, lane);
+        stamp(5);
+        dfl::p4_bits(s, n, lane, tok);
         __syncthreads();
-        if (lane == 0) dfl::p4_scan(s, n);
+        stamp(6);
+        p4_scan_wg(s, n, lane, slot);
         __syncthreads();
-        dfl::p5_emit(s, n, lane, slot);
+        stamp(7);
+        dfl::p5_emit(s, n, lane, tok, slot);
         __syncthreads();
+        dfl::p6_copy(s, lane, slot);
+        stamp(8);
         if (lane == 0) D.sizes[b] = dfl::p6_frame(s, n, slot);
         __syncthreads();
+        stamp(9);
     }
+    if (st && lane == 0)
+        for (int k = 0; k < 10; ++k) atomicAdd(&D.stamps[k], (unsigned long long)t[k]);
 }
 
 // compressed blocks into one contiguous buffer (offsets from an exclusive scan)

@@ -1,0 +1,48 @@
+"""GPU deflate phase probe: k_deflate over a formatted consensus stream with
+s_memtime phase stamps (dcr_deflate_probe, diagnostic entry of libdcr.so)."""
+import ctypes
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, ".")
+from duplexumiconsensusreads_amd import _lib, native_io, synth  # noqa: E402
+from duplexumiconsensusreads_amd.params import ConsensusParams  # noqa: E402
+from duplexumiconsensusreads_amd.stream import DeviceStream  # noqa: E402
+
+PHASES = ["load+clear", "hash", "count+crc", "keys+rank", "lengths(t0)", "codes", "bits", "scan(t0)", "emit",
+          "frame(t0)"]
+
+
+def main():
+    path = "/tmp/probe.bam"
+    synth.write_packed_bam(path, synth.packed_fixed_size(16_384, seed=5), seed=5)
+    ctx = _lib.Context(ConsensusParams(), device=0)
+    ds = DeviceStream(ctx, device_writer=True)
+    ing = native_io.Ingest(path)
+    hb = native_io.HostBatch(reads=1 << 20)
+    ing.next(hb)
+    res = ds.result(ds.submit(hb))
+    raw = res.record_bytes_of(hb.n_fam)
+    lib = _lib.load()
+    fn = lib.dcr_deflate_probe
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                   ctypes.c_void_p]
+    for dbg in [0]:
+        st = np.zeros(10, np.uint64)
+        ms = ctypes.c_float()
+        cb = ctypes.c_int64()
+        for rep in range(3):
+            st[:] = 0
+            _lib._check(fn(ctx._ctx, raw.ctypes.data, raw.nbytes, st.ctypes.data, ctypes.byref(ms),
+                           ctypes.byref(cb)))
+        tot = st.sum()
+        print(f"dbg={dbg}: {raw.nbytes / 1e6:.1f} MB -> {cb.value / 1e6:.1f} MB ({raw.nbytes / cb.value:.2f}x) in "
+              f"{ms.value:.2f} ms = {raw.nbytes / ms.value / 1e6:.2f} GB/s")
+        print("  " + "  ".join(f"{name} {100.0 * v / tot:.1f}%" for name, v in zip(PHASES, st)))
+
+
+if __name__ == "__main__":
+    main()
