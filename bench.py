@@ -167,10 +167,15 @@ def e2e_passes(path, params_args, device, steps, warmup, workdir):
     stats = {}
     t0 = time.perf_counter()
     for _ in range(steps):
-        stats = {}
+        stats = {"trace": []}
+        t_pass = time.perf_counter()
         with contextlib.redirect_stdout(io.StringIO()):
             cli.main(argv, stats=stats)
-    return time.perf_counter() - t0, stats
+    dt = time.perf_counter() - t0
+    trace = stats.pop("trace")
+    log("last pass timeline (ms from CLI start): " +
+        " ".join(f"{k}[{(a - t_pass) * 1e3:.0f},{(b - t_pass) * 1e3:.0f}]" for k, a, b in trace))
+    return dt, stats
 
 
 def main():

@@ -103,6 +103,7 @@ class Context:
         self._ctx = lib.dcr_create(device, ctypes.byref(self._p))
         if not self._ctx:
             raise DcrError(f"dcr_create failed: {lib.dcr_last_error().decode()}")
+        self.want_info = want_info
         if want_info:
             _check(lib.dcr_set_options(self._ctx, 1))
 
@@ -127,12 +128,14 @@ class Context:
         return load().dcr_stream(self._ctx)
 
     # -- host-pointer path ------------------------------------------------
-    def run_host(self, packed: PackedBatch, want_info=True):
+    def run_host(self, packed: PackedBatch, want_info=None):
         ss = OutArrays(4 * packed.n_fam, packed.ss_cols)
         ds = OutArrays(2 * packed.n_fam, packed.ds_cols)
         b = packed.as_struct()
         so, do = ss.as_struct(), ds.as_struct()
         _check(load().dcr_run_batch_host(self._ctx, ctypes.byref(b), ctypes.byref(so), ctypes.byref(do)))
+        if want_info is None:
+            want_info = self.want_info
         info = self.read_info(packed.n_reads) if want_info else None
         return ss, ds, info
 

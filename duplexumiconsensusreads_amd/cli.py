@@ -173,8 +173,9 @@ class _Driver:
         self.ing, self.cons, self.excl, self.unproc = ing, cons, excl, unproc
         self.verbose = args.verbose
         # per-stage busy seconds and totals (bench.py --e2e reports them)
+        self.trace = None          # optional [(stage, t0, t1)] (bench.py)
         self.stats = {"batches": 0, "consensus_records": 0, "consensus_bases": 0, "ingest_s": 0.0,
-                      "submit_s": 0.0, "wait_s": 0.0, "write_s": 0.0}
+                      "submit_s": 0.0, "wait_s": 0.0, "write_s": 0.0, "idle_s": 0.0}
 
     # -- stdout of one batch, in the reference's order --------------------------
     def _prints(self, hb, fail_f, kind, which, last_batch):
@@ -288,6 +289,8 @@ class _Driver:
         t0 = time.perf_counter()
         res = self.backend.result(handle)
         t1 = time.perf_counter()
+        if self.trace is not None:
+            self.trace.append(("wait", t0, t1))
         F = hb.n_fam
         st = self.stats
         if getattr(self.backend, "device_writer", False):
@@ -323,6 +326,8 @@ class _Driver:
         self.excl.write(hb.a["side_exc"][:exc_cut])
         self.unproc.write(hb.a["side_filt"][:filt_cut])
         st["write_s"] += time.perf_counter() - t1
+        if self.trace is not None:
+            self.trace.append(("write", t1, time.perf_counter()))
         if fail_f < F:
             if kind == "exit":
                 col = badchar_column(hb, fail_f, which, self.params.min_base_quality) if which < 4 else None
@@ -340,8 +345,10 @@ class _Driver:
         """Ingest thread -> device -> writer, in input order."""
         n_buf = 3
         free = queue.Queue()
+        t0 = time.perf_counter()
         for _ in range(n_buf):
             free.put(self.backend.host_batch(batch_reads))
+        self.stats["alloc_s"] = time.perf_counter() - t0
         ready = queue.Queue()
         stop = threading.Event()
 
@@ -353,7 +360,10 @@ class _Driver:
                         return
                     t0 = time.perf_counter()
                     self.ing.next(hb)
-                    self.stats["ingest_s"] += time.perf_counter() - t0
+                    t1 = time.perf_counter()
+                    self.stats["ingest_s"] += t1 - t0
+                    if self.trace is not None:
+                        self.trace.append(("ingest", t0, t1))
                     ready.put(hb)
                     if hb.end_kind != native_io.END_FULL:
                         return
@@ -365,12 +375,17 @@ class _Driver:
         pending = None
         try:
             while True:
+                t0 = time.perf_counter()
                 hb = ready.get()
+                self.stats["idle_s"] += time.perf_counter() - t0
                 if isinstance(hb, BaseException):
                     raise hb
                 t0 = time.perf_counter()
                 handle = self.backend.submit(hb)
-                self.stats["submit_s"] += time.perf_counter() - t0
+                t1 = time.perf_counter()
+                self.stats["submit_s"] += t1 - t0
+                if self.trace is not None:
+                    self.trace.append(("submit", t0, t1))
                 if pending is not None:
                     self.finish(*pending, last_batch=False)
                     free.put(pending[0])
@@ -383,12 +398,15 @@ class _Driver:
             stop.set()
             free.put(None)
             th.join()
+            t0 = time.perf_counter()
             self.backend.close()
+            self.stats["backend_close_s"] = time.perf_counter() - t0
 
 
 def main(argv: Optional[list] = None, backend=None, rng=random, stats: Optional[dict] = None) -> int:
     """``main`` (:1426-1650).  ``backend`` defaults to the HIP library;
     ``stats`` (optional) receives per-stage times and output totals."""
+    t_start = time.perf_counter()
     args = parse_args(sys.argv[1:] if argv is None else argv)
     params = ConsensusParams.from_args(args)
     try:
@@ -414,13 +432,18 @@ def main(argv: Optional[list] = None, backend=None, rng=random, stats: Optional[
     excl = native_io.BgzfWriter("%s_filteredreads.bam" % consensus_filename[:-4], ing.header, lvl, nt)
     unproc = native_io.BgzfWriter("%s_filteredfamilies.bam" % consensus_filename[:-4], ing.header, lvl, nt)
     ing.set_rng_state(rng.getstate())
+    t_open = time.perf_counter()
     try:
         drv = _Driver(args, params, be, ing, cons, excl, unproc)
+        if stats is not None and "trace" in stats:
+            drv.trace = stats["trace"]
         try:
             drv.run(max(args.batch_reads, 1))
         finally:
             if stats is not None:
                 stats.update(drv.stats)
+                stats["open_s"] = t_open - t_start
+                stats["run_s"] = time.perf_counter() - t_open
         c = ing.counters()
         if stats is not None:
             stats.update(c)
@@ -437,11 +460,14 @@ def main(argv: Optional[list] = None, backend=None, rng=random, stats: Optional[
         print("\n A total of %d families (%.2f %%) were filtered out due to not enough reads to generate a "
               "consensus read." % (excluded, excluded / tot_f * 100))
     finally:
+        t_close = time.perf_counter()
         rng.setstate(ing.rng_state(rng.getstate()))
         excl.close()
         unproc.close()
         cons.close()
         ing.close()
+        if stats is not None:
+            stats["close_s"] = time.perf_counter() - t_close
     return 0
 
 

@@ -67,6 +67,10 @@ struct dcr_ctx {
     DevBuf io;          // staging for the host-pointer entry point
     // streaming (dcr_submit / dcr_wait): copy streams and per-slot device buffers
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+    // dcr_wait_write's copy of the compressed blocks: a stream of its own, so
+    // that it does not queue behind the next batch's downloads on s_d2h
+    // (which wait for that batch's kernels)
+    hipStream_t s_fetch = nullptr;
     struct Slot {
         DevBuf buf;
         DevBuf wbuf;              // device record writer: metadata, record stream, BGZF blocks
@@ -272,6 +276,7 @@ void dcr_destroy(dcr_ctx *c) {
     }
     if (c->s_h2d) (void)hipStreamDestroy(c->s_h2d);
     if (c->s_d2h) (void)hipStreamDestroy(c->s_d2h);
+    if (c->s_fetch) (void)hipStreamDestroy(c->s_fetch);
     if (c->d_params) (void)hipFree(c->d_params);
     if (c->d_llr16) (void)hipFree(c->d_llr16);
     if (c->d_wtab) (void)hipFree(c->d_wtab);
@@ -659,6 +664,7 @@ int dcr_submit(dcr_ctx *c, int slot, const dcr_batch *h, dcr_out *hss, dcr_out *
     if (!c->s_h2d) {
         HIP_TRY(hipStreamCreateWithFlags(&c->s_h2d, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&c->s_d2h, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&c->s_fetch, hipStreamNonBlocking));
     }
     dcr_ctx::Slot &S = c->slots[slot];
     if (!S.ev_h2d) {
@@ -737,6 +743,7 @@ int dcr_submit_write(dcr_ctx *c, int slot, const dcr_batch *h, const dcr_wmeta *
     if (!c->s_h2d) {
         HIP_TRY(hipStreamCreateWithFlags(&c->s_h2d, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&c->s_d2h, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&c->s_fetch, hipStreamNonBlocking));
     }
     dcr_ctx::Slot &S = c->slots[slot];
     if (!S.ev_h2d) {
@@ -866,8 +873,8 @@ int dcr_wait_write(dcr_ctx *c, int slot, dcr_wres *res) {
     const int64_t n = res->totals[0];
     if (n > res->cap_bgzf) return fail(DCR_ECAPACITY, "BGZF output larger than cap_bgzf (see totals[0])");
     if (n > 0) {
-        HIP_TRY(hipMemcpyAsync(res->bgzf, S.d_comp, (size_t)n, hipMemcpyDeviceToHost, c->s_d2h));
-        HIP_TRY(hipStreamSynchronize(c->s_d2h));
+        HIP_TRY(hipMemcpyAsync(res->bgzf, S.d_comp, (size_t)n, hipMemcpyDeviceToHost, c->s_fetch));
+        HIP_TRY(hipStreamSynchronize(c->s_fetch));
     }
     return DCR_OK;
 }

@@ -10,8 +10,11 @@
 #include <cstddef>
 #include <cstdint>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <new>
+#include <sys/mman.h>
 #include <thread>
 #include <vector>
 
@@ -42,6 +45,42 @@ inline void wr32(uint8_t *p, uint32_t v) {
     p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
 }
 
+// Large host buffer on transparent huge pages (2 MiB) where the kernel
+// allows it: the record walk reads inflated data at irregular strides, and
+// with 4 KiB pages every few records cost a TLB miss.  resize() keeps the
+// contents only when the capacity suffices.
+class HugeBuf {
+  public:
+    HugeBuf() = default;
+    HugeBuf(const HugeBuf &) = delete;
+    HugeBuf &operator=(const HugeBuf &) = delete;
+    ~HugeBuf() { release(); }
+    void resize(size_t n) {
+        if (n <= cap_) { n_ = n; return; }
+        release();
+        constexpr size_t kHP = (size_t)2 << 20;
+        const size_t cap = (n + kHP - 1) & ~(kHP - 1);
+        void *p = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p == MAP_FAILED) throw std::bad_alloc();
+        (void)madvise(p, cap, MADV_HUGEPAGE);
+        p_ = (uint8_t *)p;
+        cap_ = cap;
+        n_ = n;
+    }
+    uint8_t *data() { return p_; }
+    const uint8_t *data() const { return p_; }
+    size_t size() const { return n_; }
+
+  private:
+    void release() {
+        if (p_) munmap(p_, cap_);
+        p_ = nullptr;
+        cap_ = n_ = 0;
+    }
+    uint8_t *p_ = nullptr;
+    size_t cap_ = 0, n_ = 0;
+};
+
 inline int pick_threads(int n) {
     if (n > 0) return std::min(n, 64);
     unsigned hc = std::thread::hardware_concurrency();
@@ -49,7 +88,12 @@ inline int pick_threads(int n) {
 }
 
 // Persistent workers; run(n, fn) calls fn(i) for i in [0, n) on the workers
-// and the calling thread, returns false if any call returned false.
+// and the calling thread, returns false if any call returned false (the
+// remaining calls are then skipped).  run() returns once every call has
+// finished; it does not wait for workers that have not woken up yet (with
+// more threads than cores, e.g. the inflater's pool beside this one, a late
+// worker would otherwise hold every run for a scheduler time slice): a late
+// worker finds the job's indices used up and goes back to sleep.
 class Pool {
   public:
     explicit Pool(int n_threads) : nt_(std::max(1, n_threads)) {
@@ -71,54 +115,61 @@ class Pool {
                 if (!fn(i)) return false;
             return true;
         }
+        auto job = std::make_shared<Job>();
+        job->fn = &fn;
+        job->n = n;
         {
             std::lock_guard<std::mutex> g(mu_);
-            fn_ = &fn;
-            n_ = n;
-            next_ = 0;
-            ok_ = true;
-            active_ = (int)th_.size();
+            job_ = job;
             ++gen_;
         }
         cv_.notify_all();
-        work();
-        std::unique_lock<std::mutex> lk(mu_);
-        done_cv_.wait(lk, [this] { return active_ == 0; });
-        fn_ = nullptr;
-        return ok_;
+        work(*job);
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            done_cv_.wait(lk, [&] { return job->done.load() == n; });
+            if (job_ == job) job_.reset();
+        }
+        return job->ok.load();
     }
 
   private:
-    void work() {
-        const std::function<bool(size_t)> *fn = fn_;
-        for (size_t i; ok_.load(std::memory_order_relaxed) && (i = next_.fetch_add(1)) < n_;)
-            if (!(*fn)(i)) ok_ = false;
+    struct Job {
+        const std::function<bool(size_t)> *fn = nullptr;
+        size_t n = 0;
+        std::atomic<size_t> next{0}, done{0};
+        std::atomic<bool> ok{true};
+    };
+    void work(Job &j) {
+        for (;;) {
+            const size_t i = j.next.fetch_add(1);
+            if (i >= j.n) return;
+            if (j.ok.load(std::memory_order_relaxed) && !(*j.fn)(i)) j.ok = false;
+            if (j.done.fetch_add(1) + 1 == j.n) {
+                std::lock_guard<std::mutex> g(mu_);
+                done_cv_.notify_all();
+            }
+        }
     }
     void loop() {
         uint64_t seen = 0;
         for (;;) {
+            std::shared_ptr<Job> j;
             {
                 std::unique_lock<std::mutex> lk(mu_);
                 cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
                 if (stop_) return;
                 seen = gen_;
+                j = job_;
             }
-            work();
-            {
-                std::lock_guard<std::mutex> g(mu_);
-                if (--active_ == 0) done_cv_.notify_all();
-            }
+            if (j) work(*j);
         }
     }
     int nt_;
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
-    const std::function<bool(size_t)> *fn_ = nullptr;
-    size_t n_ = 0;
-    std::atomic<size_t> next_{0};
-    std::atomic<bool> ok_{true};
-    int active_ = 0;
+    std::shared_ptr<Job> job_;
     uint64_t gen_ = 0;
     bool stop_ = false;
 };

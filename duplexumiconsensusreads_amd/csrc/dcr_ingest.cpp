@@ -13,6 +13,7 @@
 #include <zlib.h>
 
 #include <cmath>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -178,7 +179,7 @@ struct Job {
 // can put the bytes it still needs (the open family, a partial record)
 // right before the new data without moving the new data.
 struct Chunk {
-    std::vector<uint8_t> buf;       // [kHead headroom][len inflated bytes]
+    HugeBuf buf;                    // [kHead headroom][len inflated bytes]
     size_t len = 0;
     bool eof = false;               // nothing follows this chunk
     std::string err;
@@ -314,7 +315,7 @@ class Inflater {
 
     FILE *f_;
     Pool pool_;
-    std::vector<uint8_t> cbuf_;
+    HugeBuf cbuf_;
     size_t cbeg_ = 0, cend_ = 0;
     bool file_eof_ = false;
     Chunk chunks_[3];
@@ -325,8 +326,18 @@ class Inflater {
     std::thread th_;
 };
 
+// DCR_INGEST_PROF=1: seconds per ingest stage, printed to stderr at close
+struct IngestProf {
+    bool on = std::getenv("DCR_INGEST_PROF") != nullptr;
+    double wait_chunk = 0, scan = 0, parse = 0, flush = 0, walk_total = 0;
+    static double now() {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+};
+
 struct dcr_ingest {
     FILE *f = nullptr;
+    IngestProf prof;
     dcr_ingest_cfg cfg{};
     std::unique_ptr<Pool> pool;          // pack jobs
     std::unique_ptr<Inflater> infl;
@@ -334,7 +345,7 @@ struct dcr_ingest {
     const uint8_t *wb = nullptr;
     size_t wpos = 0, wend = 0;
     Chunk *cur = nullptr;
-    std::vector<uint8_t> big[2];
+    HugeBuf big[2];
     int big_i = 0;
     bool data_eof = false;
     std::vector<uint8_t> header;
@@ -351,6 +362,9 @@ struct dcr_ingest {
     std::vector<int> idx_tmp;
 
     ~dcr_ingest() {
+        if (prof.on)
+            std::fprintf(stderr, "[ingest] walk %.3f s: chunk wait %.3f, record scan %.3f, parse %.3f, pack copy %.3f\n",
+                         prof.walk_total, prof.wait_chunk, prof.scan, prof.parse, prof.flush);
         infl.reset();             // stops the inflate thread before the file closes
         if (f) std::fclose(f);
     }
@@ -361,7 +375,9 @@ struct dcr_ingest {
         while (wend - wpos < n) {
             if (data_eof) return 0;
             flush_jobs();                           // the jobs point into the current window
+            const double tw = prof.on ? IngestProf::now() : 0;
             Chunk *nx = infl->next();
+            if (prof.on) prof.wait_chunk += IngestProf::now() - tw;
             if (!nx->err.empty()) {
                 g_err = nx->err;
                 data_eof = true;
@@ -376,7 +392,7 @@ struct dcr_ingest {
                 if (left) std::memcpy(nx->buf.data() + base, wb + keep, left);
                 nbuf = nx->buf.data();
             } else {                                 // a leftover larger than the headroom
-                std::vector<uint8_t> &bg = big[big_i];
+                HugeBuf &bg = big[big_i];
                 big_i ^= 1;
                 bg.resize(left + nx->len + 16);
                 std::memcpy(bg.data(), wb + keep, left);
@@ -400,6 +416,12 @@ struct dcr_ingest {
     dcr_host_batch *hb = nullptr;
     void flush_jobs() {
         if (jobs.empty()) return;
+        const double tf = prof.on ? IngestProf::now() : 0;
+        struct Acc {
+            double &d, t;
+            bool on;
+            ~Acc() { if (on) d += IngestProf::now() - t; }
+        } acc{prof.flush, tf, prof.on};
         const size_t chunk = 2048;
         const size_t nchunks = (jobs.size() + chunk - 1) / chunk;
         const uint8_t *w = wb;
@@ -515,6 +537,7 @@ struct dcr_ingest {
         if (rq.size() < kRQ) { rq.resize(kRQ); rq_off.resize(kRQ); }
         rq_pos = rq_n = 0;
         size_t n = 0;
+        double ts = prof.on ? IngestProf::now() : 0;
         for (;;) {
             size_t p = wpos;
             while (n < kRQ && wend - p >= 4) {
@@ -547,11 +570,14 @@ struct dcr_ingest {
             }
         }
         const size_t chunk = 512;
+        const double tp = prof.on ? IngestProf::now() : 0;
+        if (prof.on) prof.scan += tp - ts;
         pool->run((n + chunk - 1) / chunk, [&](size_t c) {
             const size_t e = std::min(n, (c + 1) * chunk);
             for (size_t i = c * chunk; i < e; ++i) rq[i].perr = (uint8_t)parse_at(rq_off[i], rq[i]);
             return true;
         });
+        if (prof.on) prof.parse += IngestProf::now() - tp;
         rq_n = n;
         return 1;
     }
@@ -838,8 +864,10 @@ struct dcr_ingest {
             b->end_kind = errored ? DCR_END_ERROR : DCR_END_EOF;
             return fail(DCR_IO_EARG, "the input has already ended");
         }
+        const double tw = prof.on ? IngestProf::now() : 0;
         int rc = walk();
         flush_jobs();
+        if (prof.on) prof.walk_total += IngestProf::now() - tw;
         hb = nullptr;
         if (rc < 0) {
             if (cap_err) return DCR_IO_ECAPACITY;

@@ -2331,9 +2331,22 @@ __device__ __forceinline__ void send_to_general_(int rec, int g0, int R, uint32_
     }
 }
 template <bool DUPLEX>
-__device__ __forceinline__ void send_to_general(const FastArgs &, const RecMeta &m, uint2 rm, const uint8_t *lds,
+__device__ __forceinline__ void send_to_general(const FastArgs &a, const RecMeta &m, uint2 rm, const uint8_t *lds,
                                                 int lane) {
-    send_to_general_<DUPLEX>(m.rec, m.g0, (int)(m.w & 127u), rm.x, lds, lane);
+    const int R = (int)(m.w & 127u);
+    if (!DUPLEX && !a.want_info && lane < R) {
+        // trim_record left the read info out (nobody asked for it), but the
+        // general kernel reads it: the same values trim_record writes
+        const int tl = ((int)rm.x >> 8) & 255;
+        dcr_read_info inf;
+        inf.seq_start = m.base_al + (int64_t)rm.y;
+        inf.len = tl;
+        inf.n_cig = tl > 0 ? 1 : 0;
+        inf.status = tl > 0 ? DCR_ST_OK : DCR_ST_INDEX_ERROR;
+        inf.has_ins = 0;
+        a.info[m.g0 + lane] = inf;
+    }
+    send_to_general_<DUPLEX>(m.rec, m.g0, R, rm.x, lds, lane);
 }
 
 struct Staged {

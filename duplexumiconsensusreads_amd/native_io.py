@@ -131,6 +131,8 @@ class HostBatch:
                 "c": 8 * reads, "b": avg_len * reads, "n": 96 * t + (1 << 16), "s": side_bytes}
         lay, off = [], 0
         for name, dt, ln in _HB_ARRAYS:
+            if ln == "s":
+                continue
             nb = np.dtype(dt).itemsize * caps[ln]
             off = (off + 255) & ~255
             lay.append((name, dt, off, caps[ln]))
@@ -144,6 +146,11 @@ class HostBatch:
         for name, dt, o, n in lay:
             self.a[name] = self.mem[o:o + n * np.dtype(dt).itemsize].view(dt)
             setattr(s, name, base + o)
+        # the side-file records never cross PCIe: ordinary (lazily paged) memory
+        for name, dt, ln in _HB_ARRAYS:
+            if ln == "s":
+                self.a[name] = np.empty(caps[ln], dt)
+                setattr(s, name, self.a[name].ctypes.data)
         self.s = s
 
     # -- filled fields ---------------------------------------------------------

@@ -47,29 +47,31 @@ def test_gpu_matches_reference_goldens(ctx, pname):
     assert n_ok > 0 or pname == "pre1"
 
 
+def random_cfg(kind, seed):
+    if kind == "C1":
+        return synth.SynthConfig("t", 300, sub_size="poisson5", seed=seed)
+    if kind == "indel":
+        return synth.SynthConfig("t", 300, sub_size="zipf", zipf_max=40, indel_frac=0.3, seed=seed)
+    if kind == "clip":
+        return synth.SynthConfig("t", 300, sub_size="poisson5", indel_frac=0.1, softclip_frac=0.5, seed=seed)
+    if kind == "big":
+        return synth.SynthConfig("t", 6, sub_size="loguniform", logu_lo=60, logu_hi=300, indel_frac=0.05,
+                                 n_loci=2, seed=seed)
+    if kind == "len250":     # T around the 240/256 pairwise and LDS-scratch boundaries
+        return synth.SynthConfig("t", 120, read_len=248, sub_size="poisson5", indel_frac=0.1, seed=seed)
+    if kind == "len600":     # T > 256: global column scratch, deeper pairwise recursion
+        return synth.SynthConfig("t", 30, read_len=600, sub_size="poisson5", indel_frac=0.2, seed=seed)
+    if kind == "len90":
+        return synth.SynthConfig("t", 300, read_len=90, sub_size="fixed8", seed=seed)
+    if kind == "deep":       # > 64 reads per subfamily without insertions
+        return synth.SynthConfig("t", 4, sub_size="loguniform", logu_lo=65, logu_hi=200, n_loci=1, seed=seed)
+    return synth.SynthConfig("t", 200, sub_size="poisson5", indel_frac=0.5, softclip_frac=0.3, seed=seed)
+
+
 @pytest.mark.parametrize("seed,kind", [(1, "C1"), (2, "indel"), (3, "clip"), (4, "big"), (5, "wild"),
                                        (6, "len250"), (7, "len600"), (8, "len90"), (9, "deep")])
 def test_gpu_matches_oracle_random(ctx, seed, kind):
-    if kind == "C1":
-        cfg = synth.SynthConfig("t", 300, sub_size="poisson5", seed=seed)
-    elif kind == "indel":
-        cfg = synth.SynthConfig("t", 300, sub_size="zipf", zipf_max=40, indel_frac=0.3, seed=seed)
-    elif kind == "clip":
-        cfg = synth.SynthConfig("t", 300, sub_size="poisson5", indel_frac=0.1, softclip_frac=0.5, seed=seed)
-    elif kind == "big":
-        cfg = synth.SynthConfig("t", 6, sub_size="loguniform", logu_lo=60, logu_hi=300, indel_frac=0.05,
-                                n_loci=2, seed=seed)
-    elif kind == "len250":   # T around the 240/256 pairwise and LDS-scratch boundaries
-        cfg = synth.SynthConfig("t", 120, read_len=248, sub_size="poisson5", indel_frac=0.1, seed=seed)
-    elif kind == "len600":   # T > 256: global column scratch, deeper pairwise recursion
-        cfg = synth.SynthConfig("t", 30, read_len=600, sub_size="poisson5", indel_frac=0.2, seed=seed)
-    elif kind == "len90":
-        cfg = synth.SynthConfig("t", 300, read_len=90, sub_size="fixed8", seed=seed)
-    elif kind == "deep":     # > 64 reads per subfamily without insertions
-        cfg = synth.SynthConfig("t", 4, sub_size="loguniform", logu_lo=65, logu_hi=200, n_loci=1, seed=seed)
-    else:
-        cfg = synth.SynthConfig("t", 200, sub_size="poisson5", indel_frac=0.5, softclip_frac=0.3, seed=seed)
-    packed = synth.packed_from_records(cfg)
+    packed = synth.packed_from_records(random_cfg(kind, seed))
     params = ConsensusParams(max_reads=10_000)
     ctx.set_params(params)
     got = ctx.run_host(packed)
@@ -77,6 +79,34 @@ def test_gpu_matches_oracle_random(ctx, seed, kind):
     assert_same(packed, got, want)
     for k in ("seq_start", "len", "status", "has_ins"):
         assert np.array_equal(got[2][k], want[2][k]), k
+
+
+# The CLI runs without per-read info (DCR_OPT_READ_INFO off): records the
+# fast kernel hands to the general kernel (invalid letters, '+' / '-' calls)
+# must still see their reads' preprocessing.
+@pytest.fixture(scope="module")
+def ctx_noinfo():
+    c = _lib.Context(ConsensusParams(), device=0, want_info=False)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("pname", sorted(FAM["params"]))
+def test_gpu_goldens_without_read_info(ctx_noinfo, pname):
+    cases = [c for c in FAM["cases"] if c["params"] == pname]
+    results, expects = run_cases_with_backend(cases, pname, _lib.backend(ctx_noinfo))
+    n_ok = check_results(results, expects, cases)
+    assert n_ok > 0 or pname == "pre1"
+
+
+@pytest.mark.parametrize("seed,kind", [(2, "indel"), (3, "clip"), (5, "wild"), (9, "deep")])
+def test_gpu_random_without_read_info(ctx_noinfo, seed, kind):
+    packed = synth.packed_from_records(random_cfg(kind, seed))
+    params = ConsensusParams(max_reads=10_000)
+    ctx_noinfo.set_params(params)
+    got = ctx_noinfo.run_host(packed, want_info=False)
+    want = dcr_oracle_c.run(packed, params)
+    assert_same(packed, got, want)
 
 
 def test_gpu_device_path_matches_host_path(ctx):
