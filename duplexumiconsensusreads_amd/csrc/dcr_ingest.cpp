@@ -147,6 +147,7 @@ struct Rec {
     uint8_t fmsg;                    // which stop (kFilterMsg)
     uint8_t perr;                    // malformed record (kParseErr), 0 ok
     uint8_t eqx;                     // CIGAR still holds '=' / 'X' after the trim (:374-375)
+    int8_t subk;                     // split_family subfamily (:132-154): A1 B1 A2 B2 = 0..3, -1 none
     int64_t end_kept;                // pos + length after clip removal (the T bound)
     char code[24];                   // the MI prefix, when l_code <= 24 (else read from the window)
     char rx[32];                     // RX, when l_rx <= 32
@@ -173,16 +174,204 @@ struct Job {
 
 }  // namespace
 
-// Background BGZF inflate: a thread reads the file and inflates ~32 MiB runs
-// of whole blocks (on its own worker pool) into chunks, two ahead of the
-// record walk; each chunk keeps headroom in front of its data so the walk
-// can put the bytes it still needs (the open family, a partial record)
-// right before the new data without moving the new data.
+// The per-record parse (fields, aux MI / RX, the reference's filters, clip
+// bound, '=' / 'X' outcome, subfamily): runs on the scanner's pool ahead of
+// the walk, or on the ingest pool for records the scanner did not index.
+struct RecParser {
+    int min_map_quality = 0, min_base_quality = 0;
+    const uint8_t *at(const uint8_t *wb, const Rec &r, uint32_t o) const { return wb + r.off + o; }
+
+    // -- record parse ------------------------------------------------------------
+    // the fields of the whole record at window offset off (0 ok, else kParseErr)
+    int parse_at(const uint8_t *wb, size_t off, Rec &rc) const {
+        const uint8_t *base = wb + off;
+        const uint8_t *r = base + 4;
+        rc.off = off;
+        rc.len = 4u + (uint32_t)rdi32(base);
+        rc.tid = rdi32(r);
+        rc.pos = rdi32(r + 4);
+        const uint32_t l_rn = r[8];
+        rc.mapq = r[9];
+        rc.n_cig = rd16(r + 12);
+        rc.flag = rd16(r + 14);
+        rc.l_seq = rdi32(r + 16);
+        rc.perr = 0;
+        if (rc.l_seq < 0) return 1;
+        rc.o_cig = 4 + 32 + l_rn;
+        rc.o_seq = rc.o_cig + 4u * rc.n_cig;
+        rc.o_qual = rc.o_seq + (uint32_t)((rc.l_seq + 1) >> 1);
+        size_t p = rc.o_qual + (size_t)rc.l_seq;
+        if (p > rc.len) return 2;
+        rc.o_mi = rc.o_rx = 0;
+        rc.l_mi = rc.l_rx = 0;
+        rc.mi_type = rc.rx_type = 0;
+        // aux fields
+        while (p + 3 <= rc.len) {
+            const uint8_t t0 = base[p], t1 = base[p + 1], ty = base[p + 2];
+            size_t v = p + 3, e;
+            switch (ty) {
+                case 'A': case 'c': case 'C': e = v + 1; break;
+                case 's': case 'S': e = v + 2; break;
+                case 'i': case 'I': case 'f': e = v + 4; break;
+                case 'd': e = v + 8; break;
+                case 'Z': case 'H': {
+                    const void *z = std::memchr(base + v, 0, rc.len - v);
+                    if (!z) return 3;
+                    e = (size_t)((const uint8_t *)z - base) + 1;
+                    break;
+                }
+                case 'B': {
+                    if (v + 5 > rc.len) return 4;
+                    const uint8_t sub = base[v];
+                    const uint32_t n = rd32(base + v + 1);
+                    size_t es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
+                    e = v + 5 + es * (size_t)n;
+                    break;
+                }
+                default: return 5;
+            }
+            if (e > rc.len) return 6;
+            // the first occurrence, as pysam's get_tag (bam_aux_get)
+            if (t0 == 'M' && t1 == 'I' && !rc.mi_type) {
+                rc.mi_type = ty;
+                rc.o_mi = (uint32_t)v;
+                rc.l_mi = (uint16_t)(ty == 'Z' ? e - v - 1 : 0);
+            } else if (t0 == 'R' && t1 == 'X' && !rc.rx_type) {
+                rc.rx_type = ty;
+                rc.o_rx = (uint32_t)v;
+                rc.l_rx = (uint16_t)(ty == 'Z' ? e - v - 1 : 0);
+            }
+            p = e;
+        }
+        rc.l_code = rc.l_mi;
+        if (rc.mi_type == 'Z') {
+            const void *sl = std::memchr(base + rc.o_mi, '/', rc.l_mi);
+            if (sl) rc.l_code = (uint16_t)((const uint8_t *)sl - (base + rc.o_mi));
+        }
+        if (rc.mi_type == 'Z' && rc.l_code <= sizeof rc.code) std::memcpy(rc.code, base + rc.o_mi, rc.l_code);
+        if (rc.rx_type == 'Z' && rc.l_rx <= sizeof rc.rx) std::memcpy(rc.rx, base + rc.o_rx, rc.l_rx);
+        int msg = 0;
+        rc.pf = (int8_t)filters(wb, rc, msg);
+        rc.fmsg = (uint8_t)msg;
+        rc.end_kept = (int64_t)rc.pos + rc.l_seq - clip_total(wb, rc);
+        {
+            const bool rev = rc.flag & 16, r1 = rc.flag & 64, r2 = rc.flag & 128;
+            rc.subk = (int8_t)((!rev && r1) ? 0 : (!rev && r2) ? 1 : (rev && r1) ? 2 : (rev && r2) ? 3 : -1);
+        }
+        rc.eqx = rc.pf == 1 && eqx_after_trim(wb, rc);
+        return 0;
+    }
+
+    // pass_filters (:1135-1181): 1 pass, 0 excluded, -1 the reference stops (err set)
+    int filters(const uint8_t *wb, const Rec &r, int &msg) const {
+        if (!r.mi_type) { msg = 1; return -1; }
+        if (!r.rx_type) { msg = 2; return -1; }
+        if (r.n_cig == 0) { msg = 3; return -1; }
+        const uint8_t *c = at(wb, r, r.o_cig);
+        for (uint32_t i = 0; i < r.n_cig; ++i) {
+            const uint32_t op = rd32(c + 4 * i) & 15;
+            if (op == 3 || op == 6 || op >= 9) { msg = 4; return -1; }
+        }
+        for (uint32_t i = 1; i + 1 < r.n_cig; ++i)
+            if ((rd32(c + 4 * i) & 15) == 4) { msg = 5; return -1; }
+        const uint16_t fl = r.flag;
+        return (fl & 1) && (fl & 2) && !(fl & 4) && !(fl & 8) && !(fl & 2048) && !(fl & 512) &&
+               (int)r.mapq >= min_map_quality;
+    }
+
+    // end soft clips of a read (batch.py _end_soft_clips; remove_clipping :214-226)
+    int32_t clip_total(const uint8_t *wb, const Rec &r) const {
+        const uint8_t *c = at(wb, r, r.o_cig);
+        const int n = r.n_cig;
+        if (n == 0) return 0;
+        auto op = [&](int i) { return (int)(rd32(c + 4 * i) & 15); };
+        auto ln = [&](int i) { return (int32_t)(rd32(c + 4 * i) >> 4); };
+        const int first = 0, last = n - 1;
+        int32_t c5 = 0;
+        if (op(first) == 4) c5 = ln(first);
+        else if (op(first) == 5 && n > 1 && op(first + 1) == 4) c5 = ln(first + 1);
+        const int i5 = op(first) == 4 ? first : first + 1;
+        int c3i = -1;
+        if (op(last) == 4) c3i = last;
+        else if (op(last) == 5 && n > 1) c3i = last - 1;
+        int32_t c3 = 0;
+        if (c3i >= first && op(c3i) == 4 && !(c5 > 0 && c3i == i5)) c3 = ln(c3i);
+        return c5 + c3;
+    }
+
+    // does the read's CIGAR, after remove_clipping and trim_3prime_N, still
+    // hold a '=' / 'X' op (change_match_mismatch_operations prints, :374-375)?
+    bool eqx_after_trim(const uint8_t *wb, const Rec &r) const {
+        const uint8_t *c = at(wb, r, r.o_cig);
+        bool any = false;
+        for (uint32_t i = 0; i < r.n_cig; ++i) {
+            const uint32_t op = rd32(c + 4 * i) & 15;
+            any |= (op == 7 || op == 8);
+        }
+        if (!any || r.l_seq == 0) return false;
+        // remove_clipping: S bases leave the sequence (:214-251)
+        int32_t s5 = 0, s3 = 0;
+        bool inseq = false, modified = false;
+        int64_t expanded = 0;
+        for (uint32_t i = 0; i < r.n_cig; ++i) {
+            const uint32_t w = rd32(c + 4 * i), op = w & 15, ln = w >> 4;
+            if (op == 5) modified = true;
+            else if (op == 4) {
+                modified = true;
+                if (!inseq) s5 = (int32_t)ln; else s3 = (int32_t)ln;
+            } else {
+                inseq = true;
+                expanded += ln;
+            }
+        }
+        (void)modified;
+        int32_t b = s5, e = r.l_seq - s3;       // seq[s5 : -s3] (s3 > 0) or seq[s5:]
+        if (s3 == 0) e = r.l_seq;
+        if (e < b) e = b;
+        // mask (:279-283) then count the trailing 'N' (:306-312)
+        const uint8_t *sq = at(wb, r, r.o_seq), *ql = at(wb, r, r.o_qual);
+        int32_t tn = 0;
+        for (int32_t i = e - 1; i >= b; --i) {
+            const int code = (sq[i >> 1] >> ((i & 1) ? 0 : 4)) & 15;
+            if (code == 15 || (int)ql[i] < min_base_quality) ++tn;
+            else break;
+        }
+        // original_cigar[:len - tn] with Python slice semantics (:320-322)
+        int64_t keep = expanded - tn;
+        if (keep < 0) keep = std::max<int64_t>(0, expanded + keep);
+        int64_t pos = 0;
+        for (uint32_t i = 0; i < r.n_cig && pos < keep; ++i) {
+            const uint32_t w = rd32(c + 4 * i), op = w & 15, ln = w >> 4;
+            if (op == 4 || op == 5) continue;
+            if (op == 7 || op == 8) return true;
+            pos += ln;
+        }
+        return false;
+    }
+
+};
+
+// Background BGZF inflate and record index, two pipeline stages ahead of the
+// record walk:
+//   inflate thread  reads the file and inflates ~32 MiB runs of whole blocks
+//                   (on its own worker pool) into a chunk;
+//   scanner thread  follows the block_size chain through the chunk (the BAM
+//                   header first) and parses every record that starts and
+//                   ends inside it (on a second pool), so the walk gets
+//                   parsed records and does no pointer chasing of its own.
+// Each chunk keeps headroom in front of its data so the walk can put the
+// bytes it still needs (the open family, a record straddling the chunk
+// boundary) right before the new data without moving it: record offsets are
+// then the same in the chunk buffer and in the walk's window.  On anything
+// unexpected the scanner stops indexing and the walk's own serial scan (with
+// its error messages) takes over.
 struct Chunk {
     HugeBuf buf;                    // [kHead headroom][len inflated bytes]
     size_t len = 0;
     bool eof = false;               // nothing follows this chunk
     std::string err;
+    bool indexed = false;           // recs holds every record starting after the first
+    std::vector<Rec> recs;          // boundary in this chunk and ending in it (off from buf start)
 };
 
 class Inflater {
@@ -190,13 +379,14 @@ class Inflater {
     static constexpr size_t kHead = (size_t)8 << 20;
     static constexpr size_t kWant = (size_t)32 << 20;
 
-    Inflater(FILE *f, int n_threads) : f_(f), pool_(n_threads) {
+    Inflater(FILE *f, int n_threads, const RecParser &rp) : f_(f), pool_(n_threads), spool_(n_threads), rp_(rp) {
         cbuf_.resize((size_t)48 << 20);
         for (auto &c : chunks_) {
             c.buf.resize(kHead + kWant + 0x10000);
             empty_.push_back(&c);
         }
         th_ = std::thread([this] { loop(); });
+        sth_ = std::thread([this] { scan_loop(); });
     }
     ~Inflater() {
         {
@@ -205,6 +395,7 @@ class Inflater {
         }
         cv_.notify_all();
         th_.join();
+        sth_.join();
     }
     Chunk *next() {
         std::unique_lock<std::mutex> lk(mu_);
@@ -220,6 +411,7 @@ class Inflater {
         }
         cv_.notify_all();
     }
+    double scan_s = 0, index_parse_s = 0;   // DCR_INGEST_PROF
 
   private:
     void loop() {
@@ -236,12 +428,128 @@ class Inflater {
             const bool last = c->eof || !c->err.empty();
             {
                 std::lock_guard<std::mutex> g(mu_);
+                inflated_.push_back(c);
+            }
+            cv_.notify_all();
+            if (last) return;
+        }
+    }
+    void scan_loop() {
+        for (;;) {
+            Chunk *c;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || !inflated_.empty(); });
+                if (stop_) return;
+                c = inflated_.front();
+                inflated_.pop_front();
+            }
+            scan(*c);
+            const bool last = c->eof || !c->err.empty();
+            {
+                std::lock_guard<std::mutex> g(mu_);
                 full_.push_back(c);
             }
             cv_.notify_all();
             if (last) return;
         }
     }
+
+    // the block_size chain through c, continuing the stream state of the
+    // previous chunk (a field or a skip may straddle the boundary)
+    void scan(Chunk &c) {
+        c.recs.clear();
+        c.indexed = false;
+        if (dead_ || !c.err.empty()) { dead_ = true; return; }
+        const double t0 = prof_ ? now() : 0;
+        const uint8_t *d = c.buf.data() + kHead;
+        const size_t n = c.len;
+        size_t pos = 0;
+        offs_.clear();
+        auto field = [&](uint32_t &v) -> bool {      // a 4-byte field, possibly across chunks
+            while (nfld_ < 4 && pos < n) fld_[nfld_++] = d[pos++];
+            if (nfld_ < 4) return false;
+            v = rd32(fld_);
+            nfld_ = 0;
+            return true;
+        };
+        for (;;) {
+            if (skip_) {
+                const size_t a = (size_t)std::min<uint64_t>(skip_, n - pos);
+                pos += a;
+                skip_ -= a;
+                if (skip_) break;
+            }
+            uint32_t v;
+            if (st_ == kRec) {
+                if (nfld_ == 0) {
+                    while (pos + 4 <= n) {                  // whole records inside the chunk
+                        // the chain is a pointer chase through data other cores just wrote
+                        __builtin_prefetch(d + pos + 16384);
+                        __builtin_prefetch(d + pos + 16384 + 64);
+                        __builtin_prefetch(d + pos + 16384 + 128);
+                        __builtin_prefetch(d + pos + 16384 + 192);
+                        const int32_t bs = rdi32(d + pos);
+                        if (bs < 32) { dead_ = true; return; }
+                        if (pos + 4 + (size_t)bs > n) break;
+                        offs_.push_back(pos);
+                        pos += 4 + (size_t)bs;
+                    }
+                    if (pos + 4 <= n) {                     // one that runs into the next chunk
+                        skip_ = pos + 4 + (uint64_t)(uint32_t)rdi32(d + pos) - n;
+                        pos = n;
+                        break;
+                    }
+                }
+                if (!field(v)) break;                       // its block_size straddles the boundary
+                if ((int32_t)v < 32) { dead_ = true; return; }
+                skip_ = v;
+                continue;
+            }
+            if (!field(v)) break;
+            const int32_t iv = (int32_t)v;
+            switch (st_) {
+                case kMagic:
+                    if (v != 0x014d4142u) { dead_ = true; return; }   // "BAM\1"
+                    st_ = kLText;
+                    break;
+                case kLText:
+                    if (iv < 0) { dead_ = true; return; }
+                    skip_ = v;
+                    st_ = kNRef;
+                    break;
+                case kNRef:
+                    if (iv < 0) { dead_ = true; return; }
+                    nref_left_ = iv;
+                    st_ = nref_left_ ? kLName : kRec;
+                    break;
+                default:                                    // kLName: name and l_ref
+                    if (iv < 0) { dead_ = true; return; }
+                    skip_ = (uint64_t)v + 4;
+                    st_ = --nref_left_ ? kLName : kRec;
+                    break;
+            }
+        }
+        const double t1 = prof_ ? now() : 0;
+        c.recs.resize(offs_.size());
+        const uint8_t *base = c.buf.data();
+        const size_t chunk = 512;
+        spool_.run((offs_.size() + chunk - 1) / chunk, [&](size_t k) {
+            const size_t e = std::min(offs_.size(), (k + 1) * chunk);
+            for (size_t i = k * chunk; i < e; ++i)
+                c.recs[i].perr = (uint8_t)rp_.parse_at(base, kHead + offs_[i], c.recs[i]);
+            return true;
+        });
+        c.indexed = true;
+        if (prof_) {
+            scan_s += t1 - t0;
+            index_parse_s += now() - t1;
+        }
+    }
+    static double now() {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+
     void top_up() {
         std::memmove(cbuf_.data(), cbuf_.data() + cbeg_, cend_ - cbeg_);
         cend_ -= cbeg_;
@@ -314,22 +622,33 @@ class Inflater {
     }
 
     FILE *f_;
-    Pool pool_;
+    Pool pool_, spool_;
+    RecParser rp_;
     HugeBuf cbuf_;
     size_t cbeg_ = 0, cend_ = 0;
     bool file_eof_ = false;
-    Chunk chunks_[3];
-    std::deque<Chunk *> empty_, full_;
+    Chunk chunks_[4];
+    std::deque<Chunk *> empty_, inflated_, full_;
     std::mutex mu_;
     std::condition_variable cv_;
     bool stop_ = false;
-    std::thread th_;
+    std::thread th_, sth_;
+    // scanner stream state
+    enum { kMagic, kLText, kNRef, kLName, kRec } st_ = kMagic;
+    uint8_t fld_[4] = {0, 0, 0, 0};
+    int nfld_ = 0;
+    uint64_t skip_ = 0;
+    int32_t nref_left_ = 0;
+    bool dead_ = false;
+    std::vector<size_t> offs_;
+    const bool prof_ = std::getenv("DCR_INGEST_PROF") != nullptr;
 };
 
 // DCR_INGEST_PROF=1: seconds per ingest stage, printed to stderr at close
 struct IngestProf {
     bool on = std::getenv("DCR_INGEST_PROF") != nullptr;
     double wait_chunk = 0, scan = 0, parse = 0, flush = 0, walk_total = 0;
+    int64_t indexed = 0;
     static double now() {
         return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
     }
@@ -341,16 +660,21 @@ struct dcr_ingest {
     dcr_ingest_cfg cfg{};
     std::unique_ptr<Pool> pool;          // pack jobs
     std::unique_ptr<Inflater> infl;
+    RecParser rp;
     // decompressed window: wb[wpos, wend) (a chunk's buffer, or big[] for huge leftovers)
     const uint8_t *wb = nullptr;
     size_t wpos = 0, wend = 0;
-    Chunk *cur = nullptr;
+    Chunk *cur = nullptr;               // the chunk whose buffer is the window (null: big[])
+    size_t ci = 0;                      // next unserved record of cur->recs
     HugeBuf big[2];
     int big_i = 0;
     bool data_eof = false;
     std::vector<uint8_t> header;
-    // the open family (passing reads, input order)
-    std::vector<Rec> fam;
+    // the open family (passing reads, input order): pointers into the served
+    // records, or into fam_store once those are replaced (materialize_family)
+    std::vector<const Rec *> fam;
+    std::vector<Rec> fam_store;
+    std::string umi2_;                   // check_family_UMIs scratch
     bool started = false;     // any passing read seen
     bool finished = false;    // EOF processed
     bool errored = false;
@@ -363,8 +687,11 @@ struct dcr_ingest {
 
     ~dcr_ingest() {
         if (prof.on)
-            std::fprintf(stderr, "[ingest] walk %.3f s: chunk wait %.3f, record scan %.3f, parse %.3f, pack copy %.3f\n",
-                         prof.walk_total, prof.wait_chunk, prof.scan, prof.parse, prof.flush);
+            std::fprintf(stderr,
+                         "[ingest] walk %.3f s: chunk wait %.3f, serial scan %.3f, parse %.3f, pack copy %.3f; "
+                         "scanner stage: chain %.3f, parse %.3f; indexed records %lld of %lld\n",
+                         prof.walk_total, prof.wait_chunk, prof.scan, prof.parse, prof.flush, infl ? infl->scan_s : 0.0,
+                         infl ? infl->index_parse_s : 0.0, (long long)prof.indexed, (long long)records);
         infl.reset();             // stops the inflate thread before the file closes
         if (f) std::fclose(f);
     }
@@ -383,7 +710,7 @@ struct dcr_ingest {
                 data_eof = true;
                 return -1;
             }
-            const size_t keep = fam.empty() ? wpos : std::min(wpos, fam.front().off);
+            const size_t keep = fam.empty() ? wpos : std::min(wpos, fam.front()->off);
             const size_t left = wend - keep;
             size_t base;
             const uint8_t *nbuf;
@@ -400,12 +727,13 @@ struct dcr_ingest {
                 base = 0;
                 nbuf = bg.data();
             }
-            for (auto &r : fam) r.off = r.off - keep + base;
+            for (auto &r : fam_store) r.off = r.off - keep + base;   // fam points into fam_store here
             wpos = wpos - keep + base;
             wend = base + left + nx->len;
             wb = nbuf;
             if (cur) infl->give_back(cur);
-            if (nbuf == nx->buf.data()) cur = nx;
+            ci = 0;
+            if (nbuf == nx->buf.data()) cur = nx;       // the chunk's record offsets hold in the window
             else { cur = nullptr; infl->give_back(nx); }
             if (nx->eof) data_eof = true;
         }
@@ -448,103 +776,54 @@ struct dcr_ingest {
         jobs.clear();
     }
 
-    // -- record parse ------------------------------------------------------------
-    // the fields of the whole record at window offset off (0 ok, else kParseErr)
-    int parse_at(size_t off, Rec &rc) const {
-        const uint8_t *base = wb + off;
-        const uint8_t *r = base + 4;
-        rc.off = off;
-        rc.len = 4u + (uint32_t)rdi32(base);
-        rc.tid = rdi32(r);
-        rc.pos = rdi32(r + 4);
-        const uint32_t l_rn = r[8];
-        rc.mapq = r[9];
-        rc.n_cig = rd16(r + 12);
-        rc.flag = rd16(r + 14);
-        rc.l_seq = rdi32(r + 16);
-        rc.perr = 0;
-        if (rc.l_seq < 0) return 1;
-        rc.o_cig = 4 + 32 + l_rn;
-        rc.o_seq = rc.o_cig + 4u * rc.n_cig;
-        rc.o_qual = rc.o_seq + (uint32_t)((rc.l_seq + 1) >> 1);
-        size_t p = rc.o_qual + (size_t)rc.l_seq;
-        if (p > rc.len) return 2;
-        rc.o_mi = rc.o_rx = 0;
-        rc.l_mi = rc.l_rx = 0;
-        rc.mi_type = rc.rx_type = 0;
-        // aux fields
-        while (p + 3 <= rc.len) {
-            const uint8_t t0 = base[p], t1 = base[p + 1], ty = base[p + 2];
-            size_t v = p + 3, e;
-            switch (ty) {
-                case 'A': case 'c': case 'C': e = v + 1; break;
-                case 's': case 'S': e = v + 2; break;
-                case 'i': case 'I': case 'f': e = v + 4; break;
-                case 'd': e = v + 8; break;
-                case 'Z': case 'H': {
-                    const void *z = std::memchr(base + v, 0, rc.len - v);
-                    if (!z) return 3;
-                    e = (size_t)((const uint8_t *)z - base) + 1;
-                    break;
-                }
-                case 'B': {
-                    if (v + 5 > rc.len) return 4;
-                    const uint8_t sub = base[v];
-                    const uint32_t n = rd32(base + v + 1);
-                    size_t es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
-                    e = v + 5 + es * (size_t)n;
-                    break;
-                }
-                default: return 5;
-            }
-            if (e > rc.len) return 6;
-            // the first occurrence, as pysam's get_tag (bam_aux_get)
-            if (t0 == 'M' && t1 == 'I' && !rc.mi_type) {
-                rc.mi_type = ty;
-                rc.o_mi = (uint32_t)v;
-                rc.l_mi = (uint16_t)(ty == 'Z' ? e - v - 1 : 0);
-            } else if (t0 == 'R' && t1 == 'X' && !rc.rx_type) {
-                rc.rx_type = ty;
-                rc.o_rx = (uint32_t)v;
-                rc.l_rx = (uint16_t)(ty == 'Z' ? e - v - 1 : 0);
-            }
-            p = e;
-        }
-        rc.l_code = rc.l_mi;
-        if (rc.mi_type == 'Z') {
-            const void *sl = std::memchr(base + rc.o_mi, '/', rc.l_mi);
-            if (sl) rc.l_code = (uint16_t)((const uint8_t *)sl - (base + rc.o_mi));
-        }
-        if (rc.mi_type == 'Z' && rc.l_code <= sizeof rc.code) std::memcpy(rc.code, base + rc.o_mi, rc.l_code);
-        if (rc.rx_type == 'Z' && rc.l_rx <= sizeof rc.rx) std::memcpy(rc.rx, base + rc.o_rx, rc.l_rx);
-        int msg = 0;
-        rc.pf = (int8_t)filters(rc, msg);
-        rc.fmsg = (uint8_t)msg;
-        rc.end_kept = (int64_t)rc.pos + rc.l_seq - clip_total(rc);
-        rc.eqx = rc.pf == 1 && eqx_after_trim(rc);
-        return 0;
-    }
-
-    // parsed records ahead of the walk: rq[rq_pos, rq_n)
+    // parsed records ahead of the walk: rqp[rq_pos, rq_n) (the scanner's
+    // index of the current chunk, or rq from the serial scan)
+    const Rec *rqp = nullptr;
     std::vector<Rec> rq;
     std::vector<size_t> rq_off;
     size_t rq_pos = 0, rq_n = 0;
 
     // scan the next complete records of the window (block_size chain) and
     // parse them on the pool; 1 some, 0 end of data, -1 error (g_err)
+    // the open family's records out of rq before rq is refilled
+    void materialize_family() {
+        if (fam.empty()) return;
+        std::vector<Rec> tmp;
+        tmp.reserve(fam.size());
+        for (const Rec *r : fam) tmp.push_back(*r);
+        fam_store.swap(tmp);
+        for (size_t i = 0; i < fam.size(); ++i) fam[i] = &fam_store[i];
+    }
+
     int prefetch_records() {
         constexpr size_t kRQ = 16384;
+        materialize_family();
         if (rq.size() < kRQ) { rq.resize(kRQ); rq_off.resize(kRQ); }
         rq_pos = rq_n = 0;
         size_t n = 0;
         double ts = prof.on ? IngestProf::now() : 0;
+        size_t stop_at = SIZE_MAX;
         for (;;) {
+            // the scanner's records of the current chunk, from wpos on
+            if (cur && cur->indexed && ci < cur->recs.size()) {
+                const std::vector<Rec> &R = cur->recs;
+                while (ci < R.size() && R[ci].off < wpos) ++ci;
+                if (ci < R.size() && R[ci].off == wpos) {
+                    rqp = R.data() + ci;
+                    rq_n = R.size() - ci;
+                    ci = R.size();
+                    prof.indexed += (int64_t)rq_n;
+                    return 1;
+                }
+            }
+            // serial scan: records straddling a chunk boundary, unindexed chunks
+            stop_at = (cur && cur->indexed && ci < cur->recs.size()) ? cur->recs[ci].off : SIZE_MAX;
             size_t p = wpos;
-            while (n < kRQ && wend - p >= 4) {
-                __builtin_prefetch(wb + p + 4096);
-                __builtin_prefetch(wb + p + 4096 + 64);
-                __builtin_prefetch(wb + p + 4096 + 128);
-                __builtin_prefetch(wb + p + 4096 + 192);
+            while (n < kRQ && wend - p >= 4 && p < stop_at) {
+                __builtin_prefetch(wb + p + 16384);
+                __builtin_prefetch(wb + p + 16384 + 64);
+                __builtin_prefetch(wb + p + 16384 + 128);
+                __builtin_prefetch(wb + p + 16384 + 192);
                 const int32_t bs = rdi32(wb + p);
                 if (bs < 32) {
                     if (n == 0) { g_err = "malformed BAM record (block_size < 32)"; return -1; }
@@ -569,37 +848,23 @@ struct dcr_ingest {
                 return 0;
             }
         }
+        // a serial record running past the index's next record: the index is off
+        if (stop_at != SIZE_MAX && rq_off[n - 1] + 4 + (size_t)rdi32(wb + rq_off[n - 1]) > stop_at) cur->indexed = false;
         const size_t chunk = 512;
         const double tp = prof.on ? IngestProf::now() : 0;
         if (prof.on) prof.scan += tp - ts;
         pool->run((n + chunk - 1) / chunk, [&](size_t c) {
             const size_t e = std::min(n, (c + 1) * chunk);
-            for (size_t i = c * chunk; i < e; ++i) rq[i].perr = (uint8_t)parse_at(rq_off[i], rq[i]);
+            for (size_t i = c * chunk; i < e; ++i) rq[i].perr = (uint8_t)rp.parse_at(wb, rq_off[i], rq[i]);
             return true;
         });
         if (prof.on) prof.parse += IngestProf::now() - tp;
+        rqp = rq.data();
         rq_n = n;
         return 1;
     }
 
     const uint8_t *at(const Rec &r, uint32_t o) const { return wb + r.off + o; }
-
-    // pass_filters (:1135-1181): 1 pass, 0 excluded, -1 the reference stops (err set)
-    int filters(const Rec &r, int &msg) const {
-        if (!r.mi_type) { msg = 1; return -1; }
-        if (!r.rx_type) { msg = 2; return -1; }
-        if (r.n_cig == 0) { msg = 3; return -1; }
-        const uint8_t *c = at(r, r.o_cig);
-        for (uint32_t i = 0; i < r.n_cig; ++i) {
-            const uint32_t op = rd32(c + 4 * i) & 15;
-            if (op == 3 || op == 6 || op >= 9) { msg = 4; return -1; }
-        }
-        for (uint32_t i = 1; i + 1 < r.n_cig; ++i)
-            if ((rd32(c + 4 * i) & 15) == 4) { msg = 5; return -1; }
-        const uint16_t fl = r.flag;
-        return (fl & 1) && (fl & 2) && !(fl & 4) && !(fl & 8) && !(fl & 2048) && !(fl & 512) &&
-               (int)r.mapq >= cfg.min_map_quality;
-    }
 
     const char *code_of(const Rec &r) const {
         return r.l_code <= sizeof r.code ? r.code : (const char *)at(r, r.o_mi);
@@ -609,93 +874,21 @@ struct dcr_ingest {
         return a.l_code == b.l_code && std::memcmp(code_of(a), code_of(b), a.l_code) == 0;
     }
 
-    // -- the family -------------------------------------------------------------
-    // end soft clips of a read (batch.py _end_soft_clips; remove_clipping :214-226)
-    int32_t clip_total(const Rec &r) const {
-        const uint8_t *c = at(r, r.o_cig);
-        const int n = r.n_cig;
-        if (n == 0) return 0;
-        auto op = [&](int i) { return (int)(rd32(c + 4 * i) & 15); };
-        auto ln = [&](int i) { return (int32_t)(rd32(c + 4 * i) >> 4); };
-        const int first = 0, last = n - 1;
-        int32_t c5 = 0;
-        if (op(first) == 4) c5 = ln(first);
-        else if (op(first) == 5 && n > 1 && op(first + 1) == 4) c5 = ln(first + 1);
-        const int i5 = op(first) == 4 ? first : first + 1;
-        int c3i = -1;
-        if (op(last) == 4) c3i = last;
-        else if (op(last) == 5 && n > 1) c3i = last - 1;
-        int32_t c3 = 0;
-        if (c3i >= first && op(c3i) == 4 && !(c5 > 0 && c3i == i5)) c3 = ln(c3i);
-        return c5 + c3;
-    }
-
-    // does the read's CIGAR, after remove_clipping and trim_3prime_N, still
-    // hold a '=' / 'X' op (change_match_mismatch_operations prints, :374-375)?
-    bool eqx_after_trim(const Rec &r) const {
-        const uint8_t *c = at(r, r.o_cig);
-        bool any = false;
-        for (uint32_t i = 0; i < r.n_cig; ++i) {
-            const uint32_t op = rd32(c + 4 * i) & 15;
-            any |= (op == 7 || op == 8);
-        }
-        if (!any || r.l_seq == 0) return false;
-        // remove_clipping: S bases leave the sequence (:214-251)
-        int32_t s5 = 0, s3 = 0;
-        bool inseq = false, modified = false;
-        int64_t expanded = 0;
-        for (uint32_t i = 0; i < r.n_cig; ++i) {
-            const uint32_t w = rd32(c + 4 * i), op = w & 15, ln = w >> 4;
-            if (op == 5) modified = true;
-            else if (op == 4) {
-                modified = true;
-                if (!inseq) s5 = (int32_t)ln; else s3 = (int32_t)ln;
-            } else {
-                inseq = true;
-                expanded += ln;
-            }
-        }
-        (void)modified;
-        int32_t b = s5, e = r.l_seq - s3;       // seq[s5 : -s3] (s3 > 0) or seq[s5:]
-        if (s3 == 0) e = r.l_seq;
-        if (e < b) e = b;
-        // mask (:279-283) then count the trailing 'N' (:306-312)
-        const uint8_t *sq = at(r, r.o_seq), *ql = at(r, r.o_qual);
-        int32_t tn = 0;
-        for (int32_t i = e - 1; i >= b; --i) {
-            const int code = (sq[i >> 1] >> ((i & 1) ? 0 : 4)) & 15;
-            if (code == 15 || (int)ql[i] < cfg.min_base_quality) ++tn;
-            else break;
-        }
-        // original_cigar[:len - tn] with Python slice semantics (:320-322)
-        int64_t keep = expanded - tn;
-        if (keep < 0) keep = std::max<int64_t>(0, expanded + keep);
-        int64_t pos = 0;
-        for (uint32_t i = 0; i < r.n_cig && pos < keep; ++i) {
-            const uint32_t w = rd32(c + 4 * i), op = w & 15, ln = w >> 4;
-            if (op == 4 || op == 5) continue;
-            if (op == 7 || op == 8) return true;
-            pos += ln;
-        }
-        return false;
-    }
-
-    std::vector<Rec> sub[4];
+    std::vector<const Rec *> sub[4];
 
     // preprocess_family up to the read loop (:1248-1264), then pack or file
     // the family.  Returns 1 done, 0 no room in this batch (nothing changed),
     // -1 the reference stops at this family (batch error set).
     int complete_family() {
         dcr_host_batch *b = hb;
-        const Rec &r0 = fam.front();
-        const std::string code(code_of(r0), r0.l_code);
+        const Rec &r0 = *fam.front();
+        const char *code = code_of(r0);
+        const size_t l_code = r0.l_code;
         // capacity check first, with the unsampled family as the bound
-        int64_t nb = 0, nc = 0;
-        for (const Rec &r : fam) { nb += r.l_seq; nc += r.n_cig; }
+        int64_t nb = 0, nc = 0, filt_bytes = 0;
+        for (const Rec *r : fam) { nb += r->l_seq; nc += r->n_cig; filt_bytes += r->len; }
         const int64_t nfam_reads = (int64_t)fam.size();
-        const int64_t names_need = (int64_t)code.size() + 1 + 2 * (int64_t)(r0.l_rx + 1) + 64 * 2;
-        int64_t filt_bytes = 0;
-        for (const Rec &r : fam) filt_bytes += r.len;
+        const int64_t names_need = (int64_t)l_code + 1 + 2 * (int64_t)(r0.l_rx + 1) + 64 * 2;
         const bool fits = b->n_tab < b->cap_tab && b->n_fam < b->cap_fam &&
                           b->n_reads + nfam_reads <= b->cap_reads && b->n_bases + nb <= b->cap_bases &&
                           b->n_cigar + nc <= b->cap_cigar && b->n_names + names_need <= b->cap_names &&
@@ -705,41 +898,39 @@ struct dcr_ingest {
                 return fail_capacity("one family exceeds the batch capacities");
             return 0;
         }
-        // check_family_UMIs (:100-113)
+        // check_family_UMIs (:100-113): every RX is umi1 or its swapped halves
         if (r0.rx_type != 'Z') return stop(DCR_ERR_ATTRIBUTE, "'int' object has no attribute 'split'");
-        const char *rx0 = rx_of(r0);
-        const std::string umi1(rx0, r0.l_rx);
-        const size_t d1 = umi1.find('-');
-        if (d1 == std::string::npos) return stop(DCR_ERR_INDEX, "list index out of range");
-        const size_t d2 = umi1.find('-', d1 + 1);
-        const std::string umi2 = umi1.substr(d1 + 1, d2 == std::string::npos ? std::string::npos : d2 - d1 - 1) +
-                                 "-" + umi1.substr(0, d1);
-        for (const Rec &r : fam) {
-            if (r.rx_type != 'Z') return stop(DCR_ERR_ATTRIBUTE, "RX tag is not a string");
-            const char *x = rx_of(r);
-            const bool eq1 = r.l_rx == umi1.size() && std::memcmp(x, umi1.data(), r.l_rx) == 0;
-            const bool eq2 = r.l_rx == umi2.size() && std::memcmp(x, umi2.data(), r.l_rx) == 0;
+        const char *umi1 = rx_of(r0);
+        const size_t l1 = r0.l_rx;
+        const char *d1p = (const char *)std::memchr(umi1, '-', l1);
+        if (!d1p) return stop(DCR_ERR_INDEX, "list index out of range");
+        const size_t d1 = (size_t)(d1p - umi1);
+        const char *d2p = (const char *)std::memchr(umi1 + d1 + 1, '-', l1 - d1 - 1);
+        const size_t e2 = d2p ? (size_t)(d2p - umi1) : l1;
+        umi2_.assign(umi1 + d1 + 1, e2 - d1 - 1);
+        umi2_ += '-';
+        umi2_.append(umi1, d1);
+        for (const Rec *r : fam) {
+            if (r->rx_type != 'Z') return stop(DCR_ERR_ATTRIBUTE, "RX tag is not a string");
+            const char *x = rx_of(*r);
+            const bool eq1 = r->l_rx == l1 && std::memcmp(x, umi1, l1) == 0;
+            const bool eq2 = !eq1 && r->l_rx == umi2_.size() && std::memcmp(x, umi2_.data(), r->l_rx) == 0;
             if (!eq1 && !eq2)
-                return stop(DCR_ERR_EXIT, "ERROR: family " + code +
+                return stop(DCR_ERR_EXIT, "ERROR: family " + std::string(code, l_code) +
                                               " has different UMI tags. \n Please check output file of previous "
                                               "step of the pipeline (fgbio GroupReadsByUmi)");
         }
         // check_family_rnames (:116-128)
         for (size_t i = 1; i < fam.size(); ++i)
-            if (fam[i].tid != r0.tid)
-                return stop(DCR_ERR_EXIT, "ERROR: family " + code +
+            if (fam[i]->tid != r0.tid)
+                return stop(DCR_ERR_EXIT, "ERROR: family " + std::string(code, l_code) +
                                               " has difference rnames (e.g. chromosome numbers). \n Please check "
                                               "output file of previous step of the pipeline (fgbio "
                                               "GroupReadsByUmi)");
-        // split_family (:132-154)
-        for (auto &s : sub) s.clear();
-        for (const Rec &r : fam) {
-            const bool rev = r.flag & 16, r1 = r.flag & 64, r2 = r.flag & 128;
-            if (!rev && r1) sub[0].push_back(r);
-            else if (!rev && r2) sub[1].push_back(r);
-            else if (rev && r1) sub[2].push_back(r);
-            else if (rev && r2) sub[3].push_back(r);
-        }
+        // split_family (:132-154), the subfamily of each read from parse_at
+        for (auto &sv : sub) sv.clear();
+        for (const Rec *r : fam)
+            if (r->subk >= 0) sub[r->subk].push_back(r);
         // check_number_reads (:157-188)
         int sampled = 0;
         bool enough = true;
@@ -749,7 +940,7 @@ struct dcr_ingest {
             if (n > cfg.max_reads) {
                 if (cfg.max_reads < 0) return stop(DCR_ERR_VALUE, "Sample larger than population or is negative");
                 rng.sample(n, cfg.max_reads, idx_tmp);
-                std::vector<Rec> pick;
+                std::vector<const Rec *> pick;
                 pick.reserve(idx_tmp.size());
                 for (int j : idx_tmp) pick.push_back(sub[k][(size_t)j]);
                 sub[k].swap(pick);
@@ -760,15 +951,15 @@ struct dcr_ingest {
         b->tab_sampled[t] = sampled;
         b->tab_exc_cut[t] = b->n_side_exc;
         b->tab_filt_cut[t] = b->n_side_filt;
-        b->tab_code[t] = put_name(code.data(), code.size());
+        b->tab_code[t] = put_name(code, l_code);
         const int64_t code_off = b->tab_code[t];
         if (!enough) {
             // filtered family: its reads to _filteredfamilies.bam in input order (:1550-1551)
             b->tab_kind[t] = DCR_FAM_FILTERED;
             b->tab_proc[t] = -1;
-            for (const Rec &r : fam) {
-                std::memcpy(b->side_filt + b->n_side_filt, at(r, 0), r.len);
-                b->n_side_filt += r.len;
+            for (const Rec *r : fam) {
+                std::memcpy(b->side_filt + b->n_side_filt, at(*r, 0), r->len);
+                b->n_side_filt += r->len;
             }
             ++filtered;
             return 1;
@@ -784,7 +975,8 @@ struct dcr_ingest {
             int16_t eqx = 0;
             mn[k] = mx[k] = 0;
             bool first = true;
-            for (const Rec &r : sub[k]) {
+            for (const Rec *rp : sub[k]) {
+                const Rec &r = *rp;
                 const int32_t i = b->n_reads++;
                 b->read_pos[i] = r.pos;
                 b->read_mapq[i] = r.mapq;
@@ -816,9 +1008,9 @@ struct dcr_ingest {
         b->ds_cols = b->ds_col_off[2 * f + 2];
         // writer metadata: RX of the read0 of A1 and of B1 (:1367 via add_tags)
         for (int j = 0; j < 2; ++j) {
-            const std::vector<Rec> &s = sub[2 * j];
-            if (s.empty()) b->fam_rx[2 * f + j] = put_name("", 0);
-            else b->fam_rx[2 * f + j] = put_name((const char *)at(s[0], s[0].o_rx), s[0].l_rx);
+            const std::vector<const Rec *> &sv = sub[2 * j];
+            if (sv.empty()) b->fam_rx[2 * f + j] = put_name("", 0);
+            else b->fam_rx[2 * f + j] = put_name((const char *)at(*sv[0], sv[0]->o_rx), sv[0]->l_rx);
         }
         ++processed;
         return 1;
@@ -895,7 +1087,7 @@ struct dcr_ingest {
                     return 1;
                 }
             }
-            const Rec &r = rq[rq_pos];
+            const Rec &r = rqp[rq_pos];
             if (r.perr) { g_err = kParseErr[r.perr]; return -1; }
             if (r.pf < 0) return stop(kFilterMsg[r.fmsg].kind, kFilterMsg[r.fmsg].msg);
             if (r.pf == 0) {
@@ -913,7 +1105,7 @@ struct dcr_ingest {
                 continue;
             }
             if (r.mi_type != 'Z') return stop(DCR_ERR_ATTRIBUTE, "'int' object has no attribute 'split'");
-            if (!fam.empty() && !same_code(r, fam.front())) {
+            if (!fam.empty() && !same_code(r, *fam.front())) {
                 const int c = complete_family();
                 if (c <= 0) return c;      // 0: batch full, the read stays unconsumed
                 fam.clear();
@@ -921,7 +1113,7 @@ struct dcr_ingest {
             ++passed;
             ++records;
             started = true;
-            fam.push_back(r);
+            fam.push_back(&r);
             wpos = r.off + r.len;
             ++rq_pos;
         }
@@ -941,7 +1133,9 @@ dcr_ingest *dcr_ingest_open(const char *path, const dcr_ingest_cfg *cfg) {
     ing->f = f;
     ing->cfg = *cfg;
     ing->pool.reset(new Pool(pick_threads(cfg->n_threads)));
-    ing->infl.reset(new Inflater(f, pick_threads(cfg->n_threads)));
+    ing->rp.min_map_quality = cfg->min_map_quality;
+    ing->rp.min_base_quality = cfg->min_base_quality;
+    ing->infl.reset(new Inflater(f, pick_threads(cfg->n_threads), ing->rp));
     // seed like an unseeded random.Random is not reproducible; callers pass
     // their state with dcr_ingest_set_rng.  Default: random.seed(0).
     for (int i = 0; i < 624; ++i) ing->rng.mt[i] = 0;
