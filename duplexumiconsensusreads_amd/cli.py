@@ -25,9 +25,15 @@ exception, or its message and ``sys.exit(1)``, is raised at that family.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import ctypes
+import io
+import os
 import queue
 import random
+import shutil
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -68,6 +74,8 @@ def parse_args(argv):
     ap.add_argument("--threads", required=False, default=0, type=int, help=argparse.SUPPRESS)
     ap.add_argument("--compression_level", required=False, default=6, type=int, help=argparse.SUPPRESS)
     ap.add_argument("--device", required=False, default=0, type=int, help=argparse.SUPPRESS)
+    # one process per GPU over ranges of whole families (sharded mode below)
+    ap.add_argument("--gpus", required=False, default=1, type=int, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
@@ -174,6 +182,7 @@ class _Driver:
         self.verbose = args.verbose
         # per-stage busy seconds and totals (bench.py --e2e reports them)
         self.trace = None          # optional [(stage, t0, t1)] (bench.py)
+        self.ends_at_eof = True    # False for a sharded range that stops before the end
         self.stats = {"batches": 0, "consensus_records": 0, "consensus_bases": 0, "ingest_s": 0.0,
                       "submit_s": 0.0, "wait_s": 0.0, "write_s": 0.0, "idle_s": 0.0}
 
@@ -234,7 +243,9 @@ class _Driver:
                     print(line)
                 if failing and which == 4 + j:
                     return
-            is_last = last_batch and t == n_tab - 1
+            # the family the input's end completes (a range that ends early
+            # completes its last family on the next family's first read)
+            is_last = last_batch and t == n_tab - 1 and self.ends_at_eof
             print("Consensus reads for family", code,
                   "have been sucessfully writen \n" if is_last else "have been sucessfully written \n")  # :1597, :1631
 
@@ -407,8 +418,14 @@ def main(argv: Optional[list] = None, backend=None, rng=random, stats: Optional[
     """``main`` (:1426-1650).  ``backend`` defaults to the HIP library;
     ``stats`` (optional) receives per-stage times and output totals."""
     t_start = time.perf_counter()
-    args = parse_args(sys.argv[1:] if argv is None else argv)
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse_args(argv)
     params = ConsensusParams.from_args(args)
+    group = _shard_group()
+    if group is not None:
+        return _main_sharded(args, params, backend, rng, stats, group)
+    if args.gpus > 1:
+        return _launch_ranks(argv, args.gpus)
     try:
         ing = native_io.Ingest(args.input_file, params.min_map_quality, params.min_reads, params.max_reads,
                                params.min_base_quality, args.threads)
@@ -449,16 +466,7 @@ def main(argv: Optional[list] = None, backend=None, rng=random, stats: Optional[
             stats.update(c)
         if args.verbose:
             print("\n Input file has been completely read \n")
-        passed_reads, excluded_reads = c["passed"], c["excluded"]
-        processed, excluded = c["processed"], c["filtered"]
-        tot_r, tot_f = passed_reads + excluded_reads, processed + excluded
-        print("\n A total of %d reads (%.2f %%) passed the initial quality filters." %
-              (passed_reads, passed_reads / tot_r * 100))
-        print("\n A total of %d reads (%.2f %%) were filtered out." % (excluded_reads, excluded_reads / tot_r * 100))
-        print("\n A total of %d families (%.2f %%) were successfully processed to generate a consensus read." %
-              (processed, processed / tot_f * 100))
-        print("\n A total of %d families (%.2f %%) were filtered out due to not enough reads to generate a "
-              "consensus read." % (excluded, excluded / tot_f * 100))
+        _print_summary(c)
     finally:
         t_close = time.perf_counter()
         rng.setstate(ing.rng_state(rng.getstate()))
@@ -469,6 +477,262 @@ def main(argv: Optional[list] = None, backend=None, rng=random, stats: Optional[
         if stats is not None:
             stats["close_s"] = time.perf_counter() - t_close
     return 0
+
+
+def _print_summary(c):
+    """The closing counts (:1642-1649)."""
+    passed_reads, excluded_reads = c["passed"], c["excluded"]
+    processed, excluded = c["processed"], c["filtered"]
+    tot_r, tot_f = passed_reads + excluded_reads, processed + excluded
+    print("\n A total of %d reads (%.2f %%) passed the initial quality filters." %
+          (passed_reads, passed_reads / tot_r * 100))
+    print("\n A total of %d reads (%.2f %%) were filtered out." % (excluded_reads, excluded_reads / tot_r * 100))
+    print("\n A total of %d families (%.2f %%) were successfully processed to generate a consensus read." %
+          (processed, processed / tot_f * 100))
+    print("\n A total of %d families (%.2f %%) were filtered out due to not enough reads to generate a "
+          "consensus read." % (excluded, excluded / tot_f * 100))
+
+
+# -- sharded mode: one process per GPU over ranges of whole families ---------------
+#
+# ``--gpus N`` relaunches the CLI as N ranks (torch.distributed.run, gloo for
+# the small control messages; no data-path collective).  Rank 0 finds N-1
+# split points, each the first read of a family (native_io.split_points);
+# every rank runs the ordinary pipeline over its range into part files, and
+# rank 0 concatenates the parts in order under the header, prints the ranks'
+# stdout in order and the summary.  The result is the single-process result:
+#   * a family never straddles two ranks, and a range that ends early
+#     completes its last family there, as the reference does when the next
+#     family's first read arrives;
+#   * random.sample draws: the (population, size) of every call depends only
+#     on the data, so each rank's exact starting state is the state after
+#     the calls of the ranks before it; ranks that ran from another state run
+#     again (none when nothing is downsampled);
+#   * the first failing rank ends the output exactly as the reference stops:
+#     its parts are already cut where the reference stops writing, later
+#     ranks are dropped and its exception is raised.
+
+_EXC = {c.__name__: c for c in (IndexError, TypeError, ValueError, OverflowError, AttributeError, KeyError,
+                                 ZeroDivisionError, UnicodeEncodeError)}
+_BGZF_EOF = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+
+
+def _shard_group():
+    """(dist, rank, world) when this process is a rank of the sharded CLI
+    (DCR_SHARD=1, set by _launch_ranks, in a torch.distributed group of more
+    than one process), else None.  torch is only imported in that case."""
+    if os.environ.get("DCR_SHARD") != "1":
+        return None
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+            return None
+        # gloo announces its connections on file descriptor 1: keep them out
+        # of the CLI's stdout
+        sys.stdout.flush()
+        saved, null = os.dup(1), os.open(os.devnull, os.O_WRONLY)
+        os.dup2(null, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
+            os.close(null)
+    if dist.get_world_size() <= 1:
+        return None
+    return dist, dist.get_rank(), dist.get_world_size()
+
+
+def _rank_device(args, local):
+    """--device + the local rank, wrapped over the visible GPUs (counting them
+    does not initialise the GPU on this stack)."""
+    try:
+        import torch
+        n = torch.cuda.device_count()
+    except Exception:
+        n = 0
+    return args.device + (local % n if n else local)
+
+
+def _launch_ranks(argv, n):
+    """N ranks of this CLI, one per GPU, started before anything here touches a GPU."""
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    rest = []
+    skip = False
+    for a in argv:                       # drop --gpus N / --gpus=N
+        if skip:
+            skip = False
+            continue
+        if a == "--gpus":
+            skip = True
+            continue
+        if a.startswith("--gpus="):
+            continue
+        rest.append(a)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "duplexumiconsensusreads_amd.cli", *rest]
+    env = dict(os.environ, DCR_SHARD="1")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
+def _run_range(args, params, backend, path, rng, rng_state, rng_range, parts, device):
+    """The ordinary pipeline over one range of families into part files;
+    stdout, outcome, counters and random.sample calls in a dict."""
+    res = {"status": "ok", "exc_args": (), "calls": [], "counters": None, "stdout": "", "stats": {}}
+    lvl, nt = args.compression_level, args.threads
+    out = io.StringIO()
+    ing = native_io.Ingest(path, params.min_map_quality, params.min_reads, params.max_reads,
+                           params.min_base_quality, args.threads, rng_range[0], rng_range[1])
+    be = _as_backend(backend, params, device)
+    cons = native_io.BgzfWriter(parts[0], b"", lvl, nt)
+    excl = native_io.BgzfWriter(parts[1], b"", lvl, nt)
+    unproc = native_io.BgzfWriter(parts[2], b"", lvl, nt)
+    ing.set_rng_state(rng_state)
+    drv = _Driver(args, params, be, ing, cons, excl, unproc)
+    drv.ends_at_eof = rng_range[1] == -1
+    try:
+        with contextlib.redirect_stdout(out):
+            drv.run(max(args.batch_reads, 1))
+    except ReferenceExit as e:
+        res["status"], res["exc_args"] = "exit", (e.code,)
+    except tuple(_EXC.values()) as e:
+        res["status"], res["exc_args"] = type(e).__name__, e.args
+    except Exception as e:                  # not a reference outcome: reported as is
+        res["status"], res["exc_args"] = "error", (repr(e),)
+    finally:
+        res["calls"] = ing.sample_calls()
+        res["counters"] = ing.counters()
+        res["stats"] = dict(drv.stats)
+        excl.close()
+        unproc.close()
+        cons.close()
+        ing.close()
+        res["stdout"] = out.getvalue()
+    return res
+
+
+def _merge_parts(final, header, parts, lvl, nt):
+    """header + the parts' blocks (each without its end-of-file block) + EOF."""
+    w = native_io.BgzfWriter(final, header, lvl, nt)
+    w.close()
+    with open(final, "r+b") as f:
+        f.seek(-len(_BGZF_EOF), 2)
+        f.truncate()
+        for p in parts:
+            n = os.path.getsize(p) - len(_BGZF_EOF)
+            with open(p, "rb") as src:
+                left = n
+                while left > 0:
+                    chunk = src.read(min(left, 64 << 20))
+                    if not chunk:
+                        break
+                    f.write(chunk)
+                    left -= len(chunk)
+        f.write(_BGZF_EOF)
+
+
+def _main_sharded(args, params, backend, rng, stats, group):
+    dist, rank, world = group
+    path = args.input_file
+    try:
+        header = native_io.bam_header(path)
+        in_ok = True
+    except Exception:
+        in_ok = False
+    if not in_ok:
+        if rank == 0:
+            print("ERROR: input file not found. \n Please specify file name of a valid .bam file. "
+                  "Include the format in the file name.")
+        raise ReferenceExit(1)
+    if rank == 0 and args.verbose:
+        print(path, "has been read.")
+    if args.output_file is None:
+        consensus_filename = "%s_cons.bam" % path[:-4]
+    elif args.output_file.endswith(".bam"):
+        consensus_filename = args.output_file
+    else:
+        if rank == 0:
+            print("ERROR: output file is not specified in the right format. \n Please specify the file name of a "
+                  "valid .bam file. Include the format in the file name.")
+        raise ReferenceExit(1)
+    finals = [consensus_filename, "%s_filteredreads.bam" % consensus_filename[:-4],
+              "%s_filteredfamilies.bam" % consensus_filename[:-4]]
+    obj = [native_io.split_points(path, world, params) if rank == 0 else None,
+           rng.getstate() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    splits, s0 = obj
+    pts = [0] + [v for v in splits if v != -1]
+    ranges = [(pts[i], pts[i + 1] if i + 1 < len(pts) else -1) for i in range(len(pts))]
+    mine = ranges[rank] if rank < len(ranges) else None
+    parts = ["%s.part%d" % (f, rank) for f in finals]
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    device = _rank_device(args, local) if backend is None else args.device
+    empty = {"status": "ok", "exc_args": (), "calls": [], "counters": None, "stdout": "", "stats": {}}
+    result, used, rounds = empty, None, 0
+    if mine is not None:
+        result = _run_range(args, params, backend, path, rng, s0, mine, parts, device)
+        used, rounds = s0, 1
+    while True:
+        results = [None] * world
+        dist.all_gather_object(results, result)
+        # this rank's exact starting state: the calls of the (ok) ranks before it
+        state, target = s0, None
+        for r in range(rank):
+            if results[r]["status"] != "ok":
+                break
+            state = native_io.py_replay(state, results[r]["calls"])
+        else:
+            target = state
+        again = bool(mine is not None and target is not None and target != used)
+        flags = [None] * world
+        dist.all_gather_object(flags, again)
+        if not any(flags):
+            break
+        if again:
+            result = _run_range(args, params, backend, path, rng, target, mine, parts, device)
+            used = target
+            rounds += 1
+    if stats is not None:
+        stats.update(result["stats"])
+        stats["shard_rounds"] = rounds
+    if rank == 0:
+        fail = next((r for r in range(world) if results[r]["status"] != "ok"), None)
+        upto = (fail + 1) if fail is not None else world
+        lvl, nt = args.compression_level, args.threads
+        for k in range(3):
+            _merge_parts(finals[k], header, ["%s.part%d" % (finals[k], r) for r in range(min(upto, len(ranges)))],
+                         lvl, nt)
+        sys.stdout.write("".join(results[r]["stdout"] for r in range(upto)))
+        state = s0
+        for r in range(upto):
+            state = native_io.py_replay(state, results[r]["calls"])
+        if stats is not None:
+            stats["ranks"] = [results[r]["stats"] for r in range(world)]
+    dist.barrier()
+    for p in parts:
+        if os.path.exists(p):
+            os.remove(p)
+    if rank != 0:
+        return 0
+    rng.setstate(state)
+    if fail is None:
+        tot = {}
+        for r in range(min(world, len(ranges))):
+            for k, v in (results[r]["counters"] or {}).items():
+                tot[k] = tot.get(k, 0) + v
+        if args.verbose:
+            print("\n Input file has been completely read \n")
+        _print_summary(tot)
+        return 0
+    st, ea = results[fail]["status"], results[fail]["exc_args"]
+    if st == "exit":
+        raise ReferenceExit(*ea)
+    if st in _EXC:
+        raise _EXC[st](*ea)
+    raise RuntimeError(f"rank {fail}: {ea[0] if ea else st}")
 
 
 if __name__ == "__main__":

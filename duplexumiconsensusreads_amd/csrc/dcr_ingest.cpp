@@ -12,6 +12,7 @@
 // Reference: /root/reference/DuplexUMIConsensusReads.py (":line" below).
 #include <zlib.h>
 
+#include <cctype>
 #include <cmath>
 #include <chrono>
 #include <condition_variable>
@@ -379,7 +380,18 @@ class Inflater {
     static constexpr size_t kHead = (size_t)8 << 20;
     static constexpr size_t kWant = (size_t)32 << 20;
 
-    Inflater(FILE *f, int n_threads, const RecParser &rp) : f_(f), pool_(n_threads), spool_(n_threads), rp_(rp) {
+    // ranged: start at the BGZF block at file offset start_coff, start_uoff
+    // bytes into its data, on a record boundary (no header); end_coff >= 0:
+    // stop end_uoff bytes into the data of the block at end_coff
+    Inflater(FILE *f, int n_threads, const RecParser &rp, bool ranged = false, uint64_t start_coff = 0,
+             uint32_t start_uoff = 0, int64_t end_coff = -1, uint32_t end_uoff = 0)
+        : f_(f), pool_(n_threads), spool_(n_threads), rp_(rp), end_coff_(end_coff), end_uoff_(end_uoff) {
+        if (ranged) {
+            std::fseek(f_, (long)start_coff, SEEK_SET);
+            cpos_ = start_coff;
+            st_ = kRec;
+            skip_ = start_uoff;
+        }
         cbuf_.resize((size_t)48 << 20);
         for (auto &c : chunks_) {
             c.buf.resize(kHead + kWant + 0x10000);
@@ -551,6 +563,7 @@ class Inflater {
     }
 
     void top_up() {
+        cpos_ += cbeg_;
         std::memmove(cbuf_.data(), cbuf_.data() + cbeg_, cend_ - cbeg_);
         cend_ -= cbeg_;
         cbeg_ = 0;
@@ -567,11 +580,18 @@ class Inflater {
         c.err.clear();
         struct Blk { size_t coff, clen, doff; uint32_t isize, crc; };
         std::vector<Blk> blks;
-        size_t total = 0;
+        size_t total = 0, cut = SIZE_MAX;
+        if (range_done_) { c.eof = true; return; }
         // compressed bytes are only moved while no parsed block points into them
         if (!file_eof_ && cend_ - cbeg_ < cbuf_.size() / 2) top_up();
         for (;;) {
-            while (cend_ - cbeg_ >= 18 && total + 0x10000 <= kWant) {
+            while (!range_done_ && cend_ - cbeg_ >= 18 && total + 0x10000 <= kWant) {
+                if (end_coff_ >= 0 && cpos_ + cbeg_ >= (uint64_t)end_coff_) {
+                    // the range's last block: only its first end_uoff bytes
+                    range_done_ = true;
+                    if (cpos_ + cbeg_ != (uint64_t)end_coff_ || end_uoff_ == 0) break;
+                    cut = total + end_uoff_;
+                }
                 const uint8_t *h = cbuf_.data() + cbeg_;
                 if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) { c.err = "not a BGZF file"; return; }
                 const size_t xlen = rd16(h + 10);
@@ -598,7 +618,7 @@ class Inflater {
                 blks.push_back(b);
                 cbeg_ += blen;
             }
-            if (!blks.empty()) break;
+            if (!blks.empty() || range_done_) break;
             if (file_eof_) {
                 if (cend_ > cbeg_) { c.err = "truncated BGZF block at the end of the file"; return; }
                 break;
@@ -619,11 +639,22 @@ class Inflater {
         if (!ok) { c.err = "BGZF block failed to inflate or CRC mismatch"; return; }
         c.len = total;
         if (blks.empty() && file_eof_ && cend_ == cbeg_) c.eof = true;
+        if (range_done_) {
+            if (cut != SIZE_MAX) {
+                if (cut > total) { c.err = "range end past the end of its BGZF block"; return; }
+                c.len = cut;
+            }
+            c.eof = true;
+        }
     }
 
     FILE *f_;
     Pool pool_, spool_;
     RecParser rp_;
+    int64_t end_coff_;
+    uint32_t end_uoff_;
+    uint64_t cpos_ = 0;             // file offset of cbuf_[0]
+    bool range_done_ = false;
     HugeBuf cbuf_;
     size_t cbeg_ = 0, cend_ = 0;
     bool file_eof_ = false;
@@ -675,6 +706,8 @@ struct dcr_ingest {
     std::vector<const Rec *> fam;
     std::vector<Rec> fam_store;
     std::string umi2_;                   // check_family_UMIs scratch
+    bool mid_end = false;     // the range stops before the end of the file
+    std::vector<int32_t> sample_calls;   // (n, k) of every random.sample call
     bool started = false;     // any passing read seen
     bool finished = false;    // EOF processed
     bool errored = false;
@@ -940,6 +973,8 @@ struct dcr_ingest {
             if (n > cfg.max_reads) {
                 if (cfg.max_reads < 0) return stop(DCR_ERR_VALUE, "Sample larger than population or is negative");
                 rng.sample(n, cfg.max_reads, idx_tmp);
+                sample_calls.push_back(n);
+                sample_calls.push_back(cfg.max_reads);
                 std::vector<const Rec *> pick;
                 pick.reserve(idx_tmp.size());
                 for (int j : idx_tmp) pick.push_back(sub[k][(size_t)j]);
@@ -1076,7 +1111,7 @@ struct dcr_ingest {
                 if (st < 0) return -1;
                 if (st == 0) {
                     // end of input: the last family (:1610-1631)
-                    if (!started) return stop(DCR_ERR_TYPE, "'NoneType' object is not subscriptable");
+                    if (!started && !mid_end) return stop(DCR_ERR_TYPE, "'NoneType' object is not subscriptable");
                     if (!fam.empty()) {
                         const int c = complete_family();
                         if (c <= 0) return c;
@@ -1120,12 +1155,142 @@ struct dcr_ingest {
     }
 };
 
+// ---------------------------------------------------------------------------
+// Split points for family-range sharding (dcr_split_points).
+namespace {
+
+// a BGZF block header at h (avail bytes): 1f 8b 08 04, XLEN 6, "BC" 2 BSIZE
+bool bgzf_header(const uint8_t *h, size_t avail, size_t &blen) {
+    if (avail < 18 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || h[3] != 4) return false;
+    if (rd16(h + 10) != 6 || h[12] != 'B' || h[13] != 'C' || rd16(h + 14) != 2) return false;
+    blen = (size_t)rd16(h + 16) + 1;
+    return blen >= 26;
+}
+
+struct SplitReader {
+    FILE *f = nullptr;
+    uint64_t fsize = 0;
+    libdeflate_decompressor *dec = libdeflate_alloc_decompressor();
+    std::vector<uint8_t> data;                         // inflated bytes of consecutive blocks
+    std::vector<std::pair<uint64_t, size_t>> blocks;   // (file offset, start in data)
+    uint64_t next = 0;                                 // file offset of the next block to read
+    ~SplitReader() { libdeflate_free_decompressor(dec); }
+
+    bool read_at(uint64_t off, uint8_t *dst, size_t n) {
+        if (std::fseek(f, (long)off, SEEK_SET) != 0) return false;
+        return std::fread(dst, 1, n, f) == n;
+    }
+    // first block start at or after target: a header followed by another one
+    // (or the end of the file) at its BSIZE
+    bool find_block(uint64_t target, uint64_t &out) {
+        std::vector<uint8_t> w(1 << 18);
+        for (uint64_t base = target; base < fsize; base += w.size() - 32) {
+            const size_t n = (size_t)std::min<uint64_t>(w.size(), fsize - base);
+            if (!read_at(base, w.data(), n)) return false;
+            for (size_t j = 0; j + 18 <= n; ++j) {
+                size_t blen;
+                if (!bgzf_header(w.data() + j, n - j, blen)) continue;
+                const uint64_t nx = base + j + blen;
+                if (nx == fsize) { out = base + j; return true; }
+                uint8_t h2[18];
+                size_t b2;
+                if (nx + 18 <= fsize && read_at(nx, h2, 18) && bgzf_header(h2, 18, b2)) { out = base + j; return true; }
+            }
+            if (n < w.size()) break;
+        }
+        return false;
+    }
+    // append the next block's data; false at the end of the file or on error
+    bool more() {
+        if (next >= fsize) return false;
+        uint8_t h[18];
+        size_t blen;
+        if (!read_at(next, h, 18) || !bgzf_header(h, 18, blen) || next + blen > fsize) return false;
+        std::vector<uint8_t> cb(blen);
+        if (!read_at(next, cb.data(), blen)) return false;
+        const uint32_t isize = rd32(cb.data() + blen - 4);
+        if (isize > 0x10000) return false;
+        const size_t at = data.size();
+        data.resize(at + isize);
+        size_t got = 0;
+        if (isize && (libdeflate_deflate_decompress(dec, cb.data() + 18, blen - 26, data.data() + at, isize, &got) != 0 ||
+                      got != isize))
+            return false;
+        blocks.emplace_back(next, at);
+        next += blen;
+        return true;
+    }
+    bool have(size_t n) {
+        while (data.size() < n)
+            if (!more()) return false;
+        return true;
+    }
+    int64_t voff(size_t pos) const {
+        for (size_t k = blocks.size(); k-- > 0;) {
+            const size_t end = k + 1 < blocks.size() ? blocks[k + 1].second : data.size();
+            if (blocks[k].second <= pos && pos < end) return (int64_t)((blocks[k].first << 16) | (pos - blocks[k].second));
+        }
+        return -1;
+    }
+};
+
+// a plausible BAM record at o (every field, the read name and the aux
+// fields up to exactly block_size); next = the following record
+bool record_ok(SplitReader &rd, size_t o, int32_t n_ref, size_t &next) {
+    if (!rd.have(o + 36)) return false;
+    const int32_t bs = rdi32(rd.data.data() + o);
+    if (bs < 32 || bs > (1 << 24) || !rd.have(o + 4 + (size_t)bs)) return false;
+    const uint8_t *r = rd.data.data() + o + 4;
+    const int32_t tid = rdi32(r), pos = rdi32(r + 4), l_seq = rdi32(r + 16), ntid = rdi32(r + 20), npos = rdi32(r + 24);
+    const uint32_t l_rn = r[8], n_cig = rd16(r + 12);
+    if (tid < -1 || tid >= n_ref || ntid < -1 || ntid >= n_ref || pos < -1 || npos < -1 || l_rn < 1 || l_seq < 0)
+        return false;
+    size_t p = 32 + l_rn + 4 * (size_t)n_cig + (size_t)((l_seq + 1) / 2) + (size_t)l_seq;
+    if (p > (size_t)bs || r[32 + l_rn - 1] != 0) return false;
+    for (uint32_t i = 0; i + 1 < l_rn; ++i)
+        if (r[32 + i] < 33 || r[32 + i] > 126) return false;
+    while (p < (size_t)bs) {
+        if (p + 3 > (size_t)bs) return false;
+        const uint8_t t0 = r[p], t1 = r[p + 1], ty = r[p + 2];
+        if (!std::isalpha(t0) || !std::isalnum(t1)) return false;
+        size_t v = p + 3, e;
+        switch (ty) {
+            case 'A': case 'c': case 'C': e = v + 1; break;
+            case 's': case 'S': e = v + 2; break;
+            case 'i': case 'I': case 'f': e = v + 4; break;
+            case 'Z': case 'H': {
+                const void *z = std::memchr(r + v, 0, (size_t)bs - v);
+                if (!z) return false;
+                e = (size_t)((const uint8_t *)z - r) + 1;
+                break;
+            }
+            case 'B': {
+                if (v + 5 > (size_t)bs) return false;
+                const uint8_t sub = r[v];
+                const size_t es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 :
+                                  (sub == 'i' || sub == 'I' || sub == 'f') ? 4 : 0;
+                if (!es) return false;
+                e = v + 5 + es * (size_t)rd32(r + v + 1);
+                break;
+            }
+            default: return false;
+        }
+        if (e > (size_t)bs) return false;
+        p = e;
+    }
+    next = o + 4 + (size_t)bs;
+    return true;
+}
+
+}  // namespace
+
 extern "C" {
 
 int dcr_io_abi_version(void) { return DCR_IO_ABI_VERSION; }
 const char *dcr_io_last_error(void) { return g_err.c_str(); }
 
-dcr_ingest *dcr_ingest_open(const char *path, const dcr_ingest_cfg *cfg) {
+static dcr_ingest *open_impl(const char *path, const dcr_ingest_cfg *cfg, bool ranged, int64_t start_voff,
+                             int64_t end_voff) {
     if (!path || !cfg) { g_err = "NULL argument"; return nullptr; }
     FILE *f = std::fopen(path, "rb");
     if (!f) { g_err = std::string("cannot open ") + path; return nullptr; }
@@ -1135,11 +1300,24 @@ dcr_ingest *dcr_ingest_open(const char *path, const dcr_ingest_cfg *cfg) {
     ing->pool.reset(new Pool(pick_threads(cfg->n_threads)));
     ing->rp.min_map_quality = cfg->min_map_quality;
     ing->rp.min_base_quality = cfg->min_base_quality;
-    ing->infl.reset(new Inflater(f, pick_threads(cfg->n_threads), ing->rp));
+    const int64_t end_coff = end_voff >= 0 ? (end_voff >> 16) : -1;
+    const uint32_t end_uoff = end_voff >= 0 ? (uint32_t)(end_voff & 0xffff) : 0;
+    ing->mid_end = end_voff >= 0;
+    ing->infl.reset(new Inflater(f, pick_threads(cfg->n_threads), ing->rp, ranged, (uint64_t)start_voff >> 16,
+                                 (uint32_t)(start_voff & 0xffff), end_coff, end_uoff));
     // seed like an unseeded random.Random is not reproducible; callers pass
     // their state with dcr_ingest_set_rng.  Default: random.seed(0).
     for (int i = 0; i < 624; ++i) ing->rng.mt[i] = 0;
     ing->rng.index = 624;
+    if (ranged) {
+        // the range starts on a record boundary start_uoff bytes into its first block
+        const size_t skip = (size_t)(start_voff & 0xffff);
+        const int st = ing->need(skip + 4);
+        if (st < 0) return nullptr;
+        if (st > 0) ing->wpos += skip;
+        else ing->wpos = ing->wend;       // an empty range
+        return ing.release();
+    }
     // header: magic, l_text, text, n_ref, refs
     int st = ing->need(12);
     if (st <= 0) { if (st == 0) g_err = "empty BAM"; return nullptr; }
@@ -1159,6 +1337,130 @@ dcr_ingest *dcr_ingest_open(const char *path, const dcr_ingest_cfg *cfg) {
     ing->header.assign(ing->wb + ing->wpos, ing->wb + ing->wpos + p);
     ing->wpos += p;
     return ing.release();
+}
+
+dcr_ingest *dcr_ingest_open(const char *path, const dcr_ingest_cfg *cfg) { return open_impl(path, cfg, false, 0, -1); }
+
+dcr_ingest *dcr_ingest_open_range(const char *path, const dcr_ingest_cfg *cfg, int64_t start_voff, int64_t end_voff) {
+    return open_impl(path, cfg, start_voff != 0, start_voff, end_voff);
+}
+
+int dcr_split_points(const char *path, int32_t n_parts, const dcr_ingest_cfg *cfg, int64_t *voff) {
+    if (!path || !cfg || n_parts < 1 || (n_parts > 1 && !voff)) return fail(DCR_IO_EARG, "bad arguments");
+    for (int32_t i = 0; i + 1 < n_parts; ++i) voff[i] = -1;
+    if (n_parts == 1) return DCR_IO_OK;
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return fail(DCR_IO_EARG, std::string("cannot open ") + path);
+    struct Closer { FILE *f; ~Closer() { std::fclose(f); } } closer{f};
+    std::fseek(f, 0, SEEK_END);
+    const uint64_t fsize = (uint64_t)std::ftell(f);
+    // n_ref from the header
+    int32_t n_ref = 0;
+    {
+        SplitReader rd;
+        rd.f = f;
+        rd.fsize = fsize;
+        if (!rd.have(12) || std::memcmp(rd.data.data(), "BAM\1", 4) != 0) return fail(DCR_IO_EFORMAT, "not a BAM file");
+        const size_t l_text = (size_t)rdi32(rd.data.data() + 4);
+        if (!rd.have(12 + l_text)) return fail(DCR_IO_EFORMAT, "truncated BAM header");
+        n_ref = rdi32(rd.data.data() + 8 + l_text);
+    }
+    RecParser rp;
+    rp.min_map_quality = cfg->min_map_quality;
+    rp.min_base_quality = cfg->min_base_quality;
+    int64_t last = 0;
+    for (int32_t part = 1; part < n_parts; ++part) {
+        SplitReader rd;
+        rd.f = f;
+        rd.fsize = fsize;
+        uint64_t b0;
+        if (!rd.find_block(fsize * (uint64_t)part / (uint64_t)n_parts, b0) || b0 == 0) continue;
+        rd.next = b0;
+        // a record boundary: eight consecutive plausible records
+        size_t c = SIZE_MAX;
+        for (size_t o = 0; o < 0x20000 && rd.have(o + 36); ++o) {
+            size_t q = o, nx;
+            int k = 0;
+            while (k < 8 && record_ok(rd, q, n_ref, nx)) { q = nx; ++k; }
+            if (k == 8) { c = o; break; }
+        }
+        if (c == SIZE_MAX) continue;
+        // then the first passing read whose code differs from the passing read before it
+        std::string prev;
+        bool have_prev = false;
+        size_t found = SIZE_MAX;
+        for (size_t o = c, nx; o < ((size_t)64 << 20); o = nx) {
+            if (!record_ok(rd, o, n_ref, nx)) break;
+            Rec r;
+            if (rp.parse_at(rd.data.data(), o, r) != 0 || r.pf < 0) break;   // the reference stops here: no split
+            if (r.pf == 0) continue;
+            if (r.mi_type != 'Z') break;
+            const char *cp = r.l_code <= sizeof r.code ? r.code : (const char *)rd.data.data() + o + r.o_mi;
+            const std::string code(cp, r.l_code);
+            if (have_prev && code != prev) { found = o; break; }
+            prev = code;
+            have_prev = true;
+        }
+        if (found == SIZE_MAX) continue;
+        const int64_t v = rd.voff(found);
+        if (v > last) {
+            voff[part - 1] = v;
+            last = v;
+        }
+    }
+    return DCR_IO_OK;
+}
+
+int64_t dcr_bam_header(const char *path, uint8_t *out, int64_t cap) {
+    if (!path) { g_err = "NULL argument"; return -1; }
+    FILE *f = std::fopen(path, "rb");
+    if (!f) { g_err = std::string("cannot open ") + path; return -1; }
+    struct Closer { FILE *f; ~Closer() { std::fclose(f); } } closer{f};
+    SplitReader rd;
+    rd.f = f;
+    std::fseek(f, 0, SEEK_END);
+    rd.fsize = (uint64_t)std::ftell(f);
+    if (!rd.have(12) || std::memcmp(rd.data.data(), "BAM\1", 4) != 0) { g_err = "not a BAM file"; return -1; }
+    const int32_t l_text = rdi32(rd.data.data() + 4);
+    if (l_text < 0 || !rd.have(12 + (size_t)l_text)) { g_err = "truncated BAM header"; return -1; }
+    size_t p = 8 + (size_t)l_text;
+    const int32_t n_ref = rdi32(rd.data.data() + p);
+    p += 4;
+    for (int32_t i = 0; i < n_ref; ++i) {
+        if (!rd.have(p + 4)) { g_err = "truncated BAM header"; return -1; }
+        const int32_t ln = rdi32(rd.data.data() + p);
+        if (ln < 0 || !rd.have(p + 8 + (size_t)ln)) { g_err = "truncated BAM header"; return -1; }
+        p += 8 + (size_t)ln;
+    }
+    if (out && (int64_t)p <= cap) std::memcpy(out, rd.data.data(), p);
+    return (int64_t)p;
+}
+
+int64_t dcr_ingest_sample_calls(dcr_ingest *ing, int32_t *out, int64_t cap) {
+    if (!ing) return -1;
+    const int64_t n = (int64_t)ing->sample_calls.size() / 2;
+    if (out)
+        for (int64_t i = 0; i < std::min(n, cap); ++i) {
+            out[2 * i] = ing->sample_calls[(size_t)(2 * i)];
+            out[2 * i + 1] = ing->sample_calls[(size_t)(2 * i + 1)];
+        }
+    return n;
+}
+
+int dcr_py_replay(uint32_t *mt, int32_t *index, const int32_t *calls, int64_t n_calls) {
+    if (!mt || !index || (n_calls > 0 && !calls) || *index < 0 || *index > 624) return fail(DCR_IO_EARG, "bad arguments");
+    PyRandom r;
+    std::memcpy(r.mt, mt, sizeof r.mt);
+    r.index = *index;
+    std::vector<int> v;
+    for (int64_t i = 0; i < n_calls; ++i) {
+        const int n = calls[2 * i], k = calls[2 * i + 1];
+        if (n < 0 || k < 0 || k > n) return fail(DCR_IO_EARG, "bad sample call");
+        r.sample(n, k, v);
+    }
+    std::memcpy(mt, r.mt, sizeof r.mt);
+    *index = r.index;
+    return DCR_IO_OK;
 }
 
 void dcr_ingest_close(dcr_ingest *ing) { delete ing; }

@@ -100,6 +100,11 @@ def load():
             "dcr_fmt_write": (_i32, [_vp, _vp, _vp, _vp, _i32]),
             "dcr_synth_write": (_i32, [_vp, _vp, _i32]),
             "dcr_deflate_emulate": (_i64, [_vp, _i64, _vp]),
+            "dcr_split_points": (_i32, [ctypes.c_char_p, _i32, _vp, _vp]),
+            "dcr_ingest_open_range": (_vp, [ctypes.c_char_p, _vp, _i64, _i64]),
+            "dcr_ingest_sample_calls": (_i64, [_vp, _vp, _i64]),
+            "dcr_py_replay": (_i32, [_vp, _vp, _vp, _i64]),
+            "dcr_bam_header": (_i64, [ctypes.c_char_p, _vp, _i64]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -208,15 +213,29 @@ class HostBatch:
 class Ingest:
     """dcr_ingest: a BAM opened for batched reading."""
 
-    def __init__(self, path, min_map_quality=20, min_reads=1, max_reads=100, min_base_quality=20, n_threads=0):
+    def __init__(self, path, min_map_quality=20, min_reads=1, max_reads=100, min_base_quality=20, n_threads=0,
+                 start_voff=0, end_voff=-1):
+        """``start_voff`` / ``end_voff``: a range of whole families
+        (split_points); the header is then empty."""
         lib = load()
         cfg = IngestCfg(min_map_quality, min_reads, max_reads, min_base_quality, n_threads, 0)
-        self._h = lib.dcr_ingest_open(os.fsencode(path), ctypes.byref(cfg))
+        if start_voff == 0 and end_voff == -1:
+            self._h = lib.dcr_ingest_open(os.fsencode(path), ctypes.byref(cfg))
+        else:
+            self._h = lib.dcr_ingest_open_range(os.fsencode(path), ctypes.byref(cfg), int(start_voff), int(end_voff))
         if not self._h:
             raise _err(f"cannot read {path}")
         p = _vp()
         n = lib.dcr_ingest_header(self._h, ctypes.byref(p))
-        self.header = ctypes.string_at(p.value, n)
+        self.header = ctypes.string_at(p.value, n) if n > 0 else b""
+
+    def sample_calls(self):
+        """(population, sample size) of every random.sample call so far."""
+        lib = load()
+        n = lib.dcr_ingest_sample_calls(self._h, None, 0)
+        out = np.zeros(2 * max(n, 1), np.int32)
+        lib.dcr_ingest_sample_calls(self._h, out.ctypes.data, n)
+        return [(int(out[2 * i]), int(out[2 * i + 1])) for i in range(n)]
 
     def set_rng_state(self, state):
         """``random.getstate()`` of a CPython generator."""
@@ -336,6 +355,38 @@ def deflate_emulate(data: bytes) -> bytes:
     if n < 0:
         raise IOError_("deflate_emulate: bad input size")
     return out.raw[:n]
+
+
+def split_points(path, n_parts, params):
+    """dcr_split_points: BGZF virtual offsets where parts 1..n-1 of the input
+    start (each a family start), -1 where none was found."""
+    cfg = IngestCfg(params.min_map_quality, params.min_reads, params.max_reads, params.min_base_quality, 0, 0)
+    out = np.full(max(n_parts - 1, 1), -1, np.int64)
+    if load().dcr_split_points(os.fsencode(path), n_parts, ctypes.byref(cfg), out.ctypes.data) != 0:
+        raise _err("split_points")
+    return [int(v) for v in out[:n_parts - 1]]
+
+
+def bam_header(path):
+    """The BAM header as stored (dcr_bam_header)."""
+    lib = load()
+    n = lib.dcr_bam_header(os.fsencode(path), None, 0)
+    if n < 0:
+        raise _err(f"cannot read {path}")
+    buf = ctypes.create_string_buffer(n)
+    lib.dcr_bam_header(os.fsencode(path), buf, n)
+    return buf.raw[:n]
+
+
+def py_replay(state, calls):
+    """A CPython random state after random.sample(range(n), k) for each (n, k)."""
+    words = np.asarray(state[1][:624], np.uint32).copy()
+    index = ctypes.c_int32(int(state[1][624]))
+    c = np.asarray(calls, np.int32).reshape(-1)
+    if load().dcr_py_replay(words.ctypes.data, ctypes.byref(index), c.ctypes.data if c.size else None,
+                            len(calls)) != 0:
+        raise _err("py_replay")
+    return (state[0], tuple(int(w) for w in words) + (int(index.value),), state[2])
 
 
 def py_sample(state, n, k):

@@ -145,6 +145,32 @@ int dcr_ingest_next(dcr_ingest *ing, dcr_host_batch *hb);
    families, [3] filtered families, [4] records read */
 int dcr_ingest_counters(dcr_ingest *ing, int64_t *out5);
 
+/* ---- family-range sharding (cli --gpus N: one process per GPU) ----------
+ * Split points for n_parts ranges of whole families: part p (p >= 1) starts
+ * at voff[p-1], the BGZF virtual offset (block file offset << 16 | offset in
+ * the block's data) of a passing read whose MI code differs from that of the
+ * passing read before it: a family start in the reference's grouping
+ * (:1185-1217), found near p/n of the file.  A record boundary near the
+ * target is found by checking a run of consecutive records field by field;
+ * the rank before checks that its own record chain arrives exactly there.
+ * -1 where no point was found near the target (the part is then empty).
+ * Returns 0 or an error code (dcr_io_last_error). */
+int dcr_split_points(const char *path, int32_t n_parts, const dcr_ingest_cfg *cfg, int64_t *voff);
+/* open the records of [start_voff, end_voff): start 0 = the file start
+ * (header parsed), end -1 = the end of the file.  A range that stops before
+ * the end of the file completes its last family at the range end, as the
+ * reference does when the next family's first read arrives. */
+dcr_ingest *dcr_ingest_open_range(const char *path, const dcr_ingest_cfg *cfg, int64_t start_voff, int64_t end_voff);
+/* the (population, sample size) pair of every random.sample call so far, in
+ * order (check_number_reads :157-188): returns the count, copies up to cap
+ * pairs into out */
+int64_t dcr_ingest_sample_calls(dcr_ingest *ing, int32_t *out, int64_t cap);
+/* random.sample(range(n_i), k_i) for each pair: the state after those calls */
+int dcr_py_replay(uint32_t *mt624, int32_t *index, const int32_t *calls, int64_t n_calls);
+/* the BAM header as stored (magic .. references) without opening an ingest:
+ * returns its length (copied when <= cap), or -1 */
+int64_t dcr_bam_header(const char *path, uint8_t *out, int64_t cap);
+
 /* CPython random.sample(range(n), k) on the given state (tests) */
 int dcr_py_sample(uint32_t *mt624, int32_t *index, int32_t n, int32_t k, int32_t *out);
 
