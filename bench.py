@@ -241,6 +241,14 @@ def main():
 
     e2e_bases = stats.get("consensus_bases", 0) * args.steps
     in_bases = int(packed.seq_len.astype(np.int64).sum()) * args.steps
+    # per-rank busy time of the last CLI pass (whole pass, ingest thread, waits on the device)
+    mine = {"rank": rank, "e2e_s_per_pass": (e2e_s or 0.0) / max(args.steps, 1),
+            "device_resident_ms": dev_step * 1e3,
+            **{k: round(v, 4) for k, v in stats.items() if k in ("ingest_s", "wait_s", "idle_s", "write_s")}}
+    per_rank = [mine]
+    if dist:
+        per_rank = [None] * world
+        tdist.all_gather_object(per_rank, mine)
     if dist:
         slowest = shard.max_over_ranks(e2e_s or 0.0, device=dev)
         dev_slowest = shard.max_over_ranks(dev_step, device=dev)
@@ -280,7 +288,8 @@ def main():
                                            "ms_per_step": dev_slowest * 1e3, "kernel_ms": kavg,
                                            "records_not_ok": n_bad},
                        "single_strand_stage_GBps": alg / (sum(kavg[k] for k in _lib.KERNELS[1:5]) / 1e3) / 1e9,
-                       "parallelism": f"family-sharded x{world}, one process per GPU, no data-path collective"},
+                       "parallelism": f"family-sharded x{world}, one process per GPU, no data-path collective",
+                       "per_rank": per_rank},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": dom_label,
