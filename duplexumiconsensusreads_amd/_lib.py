@@ -72,9 +72,10 @@ def load():
             import torch  # noqa: F401
         except ImportError:
             pass
-        if not os.path.exists(LIB_PATH):
-            raise DcrError(f"{LIB_PATH} not built — run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
-        lib = ctypes.CDLL(LIB_PATH)
+        path = os.environ.get("DCR_LIB_PATH", LIB_PATH)     # diagnostic builds (tools/)
+        if not os.path.exists(path):
+            raise DcrError(f"{path} not built — run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+        lib = ctypes.CDLL(path)
         for name, (res, args) in EXPORTS.items():
             fn = getattr(lib, name)
             fn.restype = res

@@ -317,7 +317,7 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     const size_t o_et = o;   o = align_up(o + sizeof(double) * (size_t)std::max<int64_t>(cols, 1));
     const size_t o_ins = o;  o = align_up(o + (size_t)std::max<int64_t>(s->ss_cols, 1));
     const size_t o_st = o;   o = align_up(o + sizeof(int4) * (size_t)std::max<int64_t>(s->n_reads, 1));
-    const size_t o_err = o;  o = align_up(o + 32);
+    const size_t o_err = o;  o = align_up(o + 64);
     const size_t o_stamp = o; o = align_up(o + 32 * sizeof(unsigned long long));
     const size_t n_rec = (size_t)std::max<int64_t>(4LL * s->n_fam, 1);
     const size_t o_ovf = o;  o = align_up(o + sizeof(int) * n_rec);
@@ -336,9 +336,10 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     c->w.insflag = (uint8_t *)(b + o_ins);
     c->w.state = (int4 *)(b + o_st);
     c->w.err = (int *)(b + o_err);
-    c->w.ovf_count = (int *)(b + o_err) + 1;     // err, ovf_count[2], fast_count[2], xcount[2]: one 32-byte block
+    c->w.ovf_count = (int *)(b + o_err) + 1;     // err, ovf_count[2], fast_count[2], xcount[2], gen_next[2]: one block
     c->w.fast_count = (int *)(b + o_err) + 3;
     c->w.xcount = (int *)(b + o_err) + 5;
+    c->w.gen_next = (int *)(b + o_err) + 7;      // [2], in the same block: reset with it per batch
     c->w.xlist = (int *)(b + o_xl);
     c->w.stamps = (unsigned long long *)(b + o_stamp);
     c->w.ovf = (int *)(b + o_ovf);
@@ -353,7 +354,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     int rc = dcr_reserve(c, in);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMemsetAsync(c->w.err, 0, 32, c->stream));
+    HIP_TRY(hipMemsetAsync(c->w.err, 0, 64, c->stream));
     c->last_reads = in->n_reads;
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     // per-read preprocessing (:191-325) is fused: k_recmeta<ss> analyses the

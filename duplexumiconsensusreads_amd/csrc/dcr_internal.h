@@ -39,6 +39,7 @@ struct Workspace {
     int *ovf_count;         // [2] single-strand / duplex general-list lengths
     int *fast_count;        // [2] single-strand / duplex fast-list lengths
     int *xcount;            // [2] single-strand / duplex exact-queue lengths
+    int *gen_next;          // [2] next general-list entry to claim (k_consensus_general)
     int *xlist;             // [n_rec] exact queue: fast-list indices (k_consensus_fast<., true>)
     unsigned long long *stamps;   // [32] diagnostic phase cycles (DCR_STAMP builds only)
     RecMeta *meta;          // [n_rec] fast list

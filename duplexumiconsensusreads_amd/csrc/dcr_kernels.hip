@@ -2826,7 +2826,15 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
         for (int k = 0; k < 10; ++k) atomicAdd(&a.stamps[k + (DUPLEX ? 16 : 0)], (unsigned long long)sp.acc[k]);
 }
 
-// persistent: drains the general list written by k_recmeta
+// persistent: drains the general list written by k_recmeta.  A wave takes
+// the record at its grid position, then claims the next ones from a counter
+// (reset with the batch's other counters), so a wave that drew deep records
+// does not hold the kernel's tail while others idle.  The claim is made by
+// the wave's first active lane, not by a fixed lane: with a claim gated on
+// lane 0 the compiler lowered this loop as a divergent loop (a per-lane exit
+// mask at the latch); once lane 0 dropped out of exec no claim was made
+// again and the wave re-read its last index forever (the
+// round-1 hang).
 template <bool DUPLEX>
 #ifndef DCR_GEN_OCC
 #define DCR_GEN_OCC 2
@@ -2843,11 +2851,60 @@ __global__ __launch_bounds__(kBlock, DCR_GEN_OCC) void k_consensus_general(Args 
     for (int i = threadIdx.x; i < DCR_MAX_QTHRESH; i += kBlock) s_qthr[i] = P->qthresh[i];
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
     const int n = a.ws.ovf_count[DUPLEX ? 1 : 0];
+    int *next = a.ws.gen_next + (DUPLEX ? 1 : 0);
+#if defined(DCR_GEN_VARIANT) && DCR_GEN_VARIANT == 1     // diagnostic: claim, at most one record per wave
+    {
+        int i = 0;
+        if (lane == 0) i = atomicAdd(next, 1);
+        i = __builtin_amdgcn_readfirstlane(__shfl(i, 0, kWave));
+        if (i < n) {
+            const int v = a.ws.ovf[i];
+            process_record<DUPLEX, false>(a, v & 0x7fffffff, s_wave[wave], s_lut, s_qthr, s_wtab, v < 0, lane);
+        }
+        return;
+    }
+#endif
+#if defined(DCR_GEN_VARIANT) && DCR_GEN_VARIANT == 2     // diagnostic: static stride, reversed order
+    for (int k = blockIdx.x * kWavesPerBlock + wave; k < n; k += gridDim.x * kWavesPerBlock) {
+        const int v = a.ws.ovf[n - 1 - k];
+        process_record<DUPLEX, false>(a, v & 0x7fffffff, s_wave[wave], s_lut, s_qthr, s_wtab, v < 0, lane);
+    }
+    (void)next;
+    return;
+#endif
+#if defined(DCR_GEN_VARIANT) && DCR_GEN_VARIANT == 3     // diagnostic: static stride over block 0's waves only
+    if (blockIdx.x == 0)
+        for (int k = wave; k < n; k += kWavesPerBlock) {
+            const int v = a.ws.ovf[k];
+            process_record<DUPLEX, false>(a, v & 0x7fffffff, s_wave[wave], s_lut, s_qthr, s_wtab, v < 0, lane);
+        }
+    (void)next;
+    return;
+#endif
+#ifdef DCR_GEN_STATIC     // diagnostic (tools/ablate.py): the round-1 static stride
+    for (int i = blockIdx.x * kWavesPerBlock + wave; i < n; i += gridDim.x * kWavesPerBlock) {
+        const int v = a.ws.ovf[i];
+        process_record<DUPLEX, false>(a, v & 0x7fffffff, s_wave[wave], s_lut, s_qthr, s_wtab, v < 0, lane);
+    }
+    (void)next;
+    return;
+#endif
+    // the first record of each wave by position (no atomic on the way in: most
+    // general lists are shorter than the grid), then claims past the grid
     const int nw = gridDim.x * kWavesPerBlock;
-    for (int i = blockIdx.x * kWavesPerBlock + wave; i < n; i += nw) {
+    for (int i = blockIdx.x * kWavesPerBlock + wave;;) {
+        if (i >= n) break;
         const int v = a.ws.ovf[i];                  // bit 31: k_decide decided every column
-        process_record<DUPLEX, false>(a, v & 0x7fffffff, s_wave[wave], s_lut, s_qthr, s_wtab, v < 0, threadIdx.x & 63);
+        process_record<DUPLEX, false>(a, v & 0x7fffffff, s_wave[wave], s_lut, s_qthr, s_wtab, v < 0, lane);
+        if (nw >= n) break;
+        // one claim per wave, by its first active lane (any lane may carry it)
+        const uint64_t act = __ballot(1);
+        const int leader = __ffsll((long long)act) - 1;
+        int t = 0;
+        if (lane == leader) t = atomicAdd(next, 1);
+        i = nw + __builtin_amdgcn_readfirstlane(__shfl(t, leader, kWave));
     }
 }
 
