@@ -166,11 +166,17 @@ def e2e_passes(path, params_args, device, steps, warmup, workdir):
             cli.main(argv)
     stats = {}
     t0 = time.perf_counter()
+    import gc
+    teardown = 0.0
     for _ in range(steps):
         stats = {"trace": []}
         t_pass = time.perf_counter()
         with contextlib.redirect_stdout(io.StringIO()):
             cli.main(argv, stats=stats)
+        t_ret = time.perf_counter()
+        gc.collect()                     # the pass's pinned host memory is released here (inside the timed region)
+        teardown = time.perf_counter() - t_ret
+    stats["teardown_s"] = teardown
     dt = time.perf_counter() - t0
     trace = stats.pop("trace")
     log("last pass timeline (ms from CLI start): " +

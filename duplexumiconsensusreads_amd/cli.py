@@ -473,9 +473,11 @@ def main(argv: Optional[list] = None, backend=None, rng=random, stats: Optional[
         excl.close()
         unproc.close()
         cons.close()
+        t_wclose = time.perf_counter()
         ing.close()
         if stats is not None:
             stats["close_s"] = time.perf_counter() - t_close
+            stats["close_writers_s"] = t_wclose - t_close
     return 0
 
 

@@ -207,9 +207,16 @@ size_t bgzf_block(const uint8_t *in, size_t len, int level, uint8_t *out) {
 struct dcr_bgzw {
     FILE *f = nullptr;
     int level = 6;
+    // the pool and the pending buffer are made on first use: the side-file
+    // writers of most runs never write a record
+    int n_threads = 0;
     std::unique_ptr<Pool> pool;
-    std::vector<uint8_t> in;     // pending uncompressed bytes
-    size_t n_in = 0;
+    std::unique_ptr<uint8_t[]> in;   // pending uncompressed bytes [in_cap]
+    size_t in_cap = 0, n_in = 0;
+    Pool &pl() {
+        if (!pool) pool.reset(new Pool(pick_threads(n_threads)));
+        return *pool;
+    }
     std::vector<std::vector<uint8_t>> out;
     std::vector<size_t> out_len;
     int64_t bytes_in = 0, bytes_out = 0;
@@ -220,13 +227,16 @@ struct dcr_bgzw {
         const size_t nb = (n + kBlockData - 1) / kBlockData;
         if (out.size() < nb) { out.resize(nb); out_len.resize(nb); }
         const int lvl = level;
-        const bool ok = pool->run(nb, [&](size_t i) {
+        auto one = [&](size_t i) {
             const size_t off = i * kBlockData, len = std::min(kBlockData, n - off);
             std::vector<uint8_t> &o = out[i];
             if (o.size() < 0x10000) o.resize(0x10000);
-            out_len[i] = bgzf_block(in.data() + off, len, lvl, o.data());
+            out_len[i] = bgzf_block(in.get() + off, len, lvl, o.data());
             return out_len[i] != 0;
-        });
+        };
+        bool ok = true;
+        if (nb == 1) ok = one(0);            // a header, a short tail: no pool needed
+        else ok = pl().run(nb, one);
         if (!ok) { g_err = "BGZF block failed to deflate"; return false; }
         for (size_t i = 0; i < nb; ++i) {
             if (std::fwrite(out[i].data(), 1, out_len[i], f) != out_len[i]) { g_err = "write failed"; return false; }
@@ -242,11 +252,15 @@ struct dcr_bgzw {
         return true;
     }
     bool write(const uint8_t *s, size_t n) {
+        if (n && !in_cap) {
+            in_cap = kBlockData * (size_t)std::max(64, 8 * pick_threads(n_threads));
+            in.reset(new uint8_t[in_cap]);
+        }
         while (n > 0) {
-            const size_t k = std::min(in.size() - n_in, n);
-            std::memcpy(in.data() + n_in, s, k);
+            const size_t k = std::min(in_cap - n_in, n);
+            std::memcpy(in.get() + n_in, s, k);
             n_in += k; s += k; n -= k;
-            if (n_in == in.size()) {
+            if (n_in == in_cap) {
                 if (!flush(n_in)) return false;
                 n_in = 0;
             }
@@ -348,8 +362,7 @@ dcr_bgzw *dcr_bgzw_open(const char *path, int level, int n_threads) {
     auto *w = new dcr_bgzw;
     w->f = f;
     w->level = level;
-    w->pool.reset(new Pool(pick_threads(n_threads)));
-    w->in.resize(kBlockData * (size_t)std::max(64, 8 * w->pool->size()));
+    w->n_threads = n_threads;
     return w;
 }
 
@@ -437,13 +450,13 @@ int dcr_fmt_write(dcr_bgzw *w, const dcr_host_batch *hb, const dcr_fmt_out *ss, 
     // own run of BGZF blocks (a record may span blocks), written in order
     const int32_t chunk = 128;
     const int32_t nch = (n_fam + chunk - 1) / chunk;
-    const int32_t group = std::max(1, 4 * w->pool->size());
+    const int32_t group = std::max(1, 4 * w->pl().size());
     struct Task { Buf raw; std::vector<uint8_t> comp; size_t n_comp = 0; };
     std::vector<Task> tasks((size_t)std::min(nch, group));
     const int lvl = w->level;
     for (int32_t g0 = 0; g0 < nch; g0 += group) {
         const int32_t g1 = std::min(nch, g0 + group);
-        const bool ok = w->pool->run((size_t)(g1 - g0), [&](size_t gi) {
+        const bool ok = w->pl().run((size_t)(g1 - g0), [&](size_t gi) {
             Task &t = tasks[gi];
             Buf &o = t.raw;
             o.n = 0;

@@ -171,6 +171,7 @@ struct Job {
     size_t rec;         // window offset of the record
     int64_t dst_base;
     int64_t dst_cig;
+    int32_t read;       // batch read index: the per-read fields are written by the copy job
 };
 
 }  // namespace
@@ -249,6 +250,9 @@ struct RecParser {
             const void *sl = std::memchr(base + rc.o_mi, '/', rc.l_mi);
             if (sl) rc.l_code = (uint16_t)((const uint8_t *)sl - (base + rc.o_mi));
         }
+        // inline copies, zero-padded: the walk compares them as whole words
+        std::memset(rc.code, 0, sizeof rc.code);
+        std::memset(rc.rx, 0, sizeof rc.rx);
         if (rc.mi_type == 'Z' && rc.l_code <= sizeof rc.code) std::memcpy(rc.code, base + rc.o_mi, rc.l_code);
         if (rc.rx_type == 'Z' && rc.l_rx <= sizeof rc.rx) std::memcpy(rc.rx, base + rc.o_rx, rc.l_rx);
         int msg = 0;
@@ -585,7 +589,7 @@ class Inflater {
         // compressed bytes are only moved while no parsed block points into them
         if (!file_eof_ && cend_ - cbeg_ < cbuf_.size() / 2) top_up();
         for (;;) {
-            while (!range_done_ && cend_ - cbeg_ >= 18 && total + 0x10000 <= kWant) {
+            while (!range_done_ && cend_ - cbeg_ >= 18 && total + 0x10000 <= want_) {
                 if (end_coff_ >= 0 && cpos_ + cbeg_ >= (uint64_t)end_coff_) {
                     // the range's last block: only its first end_uoff bytes
                     range_done_ = true;
@@ -639,6 +643,7 @@ class Inflater {
         if (!ok) { c.err = "BGZF block failed to inflate or CRC mismatch"; return; }
         c.len = total;
         if (blks.empty() && file_eof_ && cend_ == cbeg_) c.eof = true;
+        want_ = kWant;
         if (range_done_) {
             if (cut != SIZE_MAX) {
                 if (cut > total) { c.err = "range end past the end of its BGZF block"; return; }
@@ -655,6 +660,7 @@ class Inflater {
     uint32_t end_uoff_;
     uint64_t cpos_ = 0;             // file offset of cbuf_[0]
     bool range_done_ = false;
+    size_t want_ = (size_t)4 << 20;   // the first chunk is small: the walk starts sooner
     HugeBuf cbuf_;
     size_t cbeg_ = 0, cend_ = 0;
     bool file_eof_ = false;
@@ -795,6 +801,13 @@ struct dcr_ingest {
                 const uint32_t l_rn = r[8];
                 const uint32_t n_cig = rd16(r + 12);
                 const int32_t l_seq = rdi32(r + 16);
+                const int32_t i = jb.read;
+                b->read_pos[i] = rdi32(r + 4);
+                b->read_mapq[i] = r[9];
+                b->seq_len[i] = l_seq;
+                b->seq_off[i] = jb.dst_base;
+                b->cig_off[i] = (int32_t)jb.dst_cig;
+                b->cig_n[i] = (int32_t)n_cig;
                 const uint8_t *cig = r + 32 + l_rn;
                 std::memcpy(b->cigar + jb.dst_cig, cig, 4u * n_cig);
                 const uint8_t *s = cig + 4u * n_cig;
@@ -904,7 +917,14 @@ struct dcr_ingest {
     }
     const char *rx_of(const Rec &r) const { return r.l_rx <= sizeof r.rx ? r.rx : (const char *)at(r, r.o_rx); }
     bool same_code(const Rec &a, const Rec &b) const {
-        return a.l_code == b.l_code && std::memcmp(code_of(a), code_of(b), a.l_code) == 0;
+        if (a.l_code != b.l_code) return false;
+        if (a.l_code <= sizeof a.code) {            // zero-padded inline copies: three words
+            uint64_t x[3], y[3];
+            std::memcpy(x, a.code, sizeof x);
+            std::memcpy(y, b.code, sizeof y);
+            return ((x[0] ^ y[0]) | (x[1] ^ y[1]) | (x[2] ^ y[2])) == 0;
+        }
+        return std::memcmp(code_of(a), code_of(b), a.l_code) == 0;
     }
 
     std::vector<const Rec *> sub[4];
@@ -943,11 +963,30 @@ struct dcr_ingest {
         umi2_.assign(umi1 + d1 + 1, e2 - d1 - 1);
         umi2_ += '-';
         umi2_.append(umi1, d1);
+        // both forms zero-padded to the inline width: four-word compares
+        constexpr size_t kRx = sizeof(Rec::rx);
+        const bool inl = l1 <= kRx;
+        uint64_t w1[kRx / 8] = {0}, w2[kRx / 8] = {0};
+        if (inl) {
+            std::memcpy(w1, umi1, l1);
+            std::memcpy(w2, umi2_.data(), umi2_.size());   // same length as umi1
+        }
+        auto same = [&](const Rec *r, const uint64_t *w) {
+            uint64_t x[kRx / 8];
+            std::memcpy(x, r->rx, kRx);
+            return ((x[0] ^ w[0]) | (x[1] ^ w[1]) | (x[2] ^ w[2]) | (x[3] ^ w[3])) == 0;
+        };
         for (const Rec *r : fam) {
             if (r->rx_type != 'Z') return stop(DCR_ERR_ATTRIBUTE, "RX tag is not a string");
             const char *x = rx_of(*r);
-            const bool eq1 = r->l_rx == l1 && std::memcmp(x, umi1, l1) == 0;
-            const bool eq2 = !eq1 && r->l_rx == umi2_.size() && std::memcmp(x, umi2_.data(), r->l_rx) == 0;
+            bool eq1, eq2;
+            if (inl && r->l_rx == l1) {
+                eq1 = same(r, w1);
+                eq2 = !eq1 && l1 == umi2_.size() && same(r, w2);
+            } else {
+                eq1 = r->l_rx == l1 && std::memcmp(x, umi1, l1) == 0;
+                eq2 = !eq1 && r->l_rx == umi2_.size() && std::memcmp(x, umi2_.data(), r->l_rx) == 0;
+            }
             if (!eq1 && !eq2)
                 return stop(DCR_ERR_EXIT, "ERROR: family " + std::string(code, l_code) +
                                               " has different UMI tags. \n Please check output file of previous "
@@ -1013,13 +1052,7 @@ struct dcr_ingest {
             for (const Rec *rp : sub[k]) {
                 const Rec &r = *rp;
                 const int32_t i = b->n_reads++;
-                b->read_pos[i] = r.pos;
-                b->read_mapq[i] = r.mapq;
-                b->seq_len[i] = r.l_seq;
-                b->seq_off[i] = b->n_bases;
-                b->cig_off[i] = (int32_t)b->n_cigar;
-                b->cig_n[i] = r.n_cig;
-                jobs.push_back(Job{r.off, b->n_bases, b->n_cigar});
+                jobs.push_back(Job{r.off, b->n_bases, b->n_cigar, i});
                 b->n_bases += r.l_seq;
                 b->n_cigar += r.n_cig;
                 const int64_t end = r.end_kept;

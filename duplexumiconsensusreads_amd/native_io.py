@@ -130,13 +130,19 @@ class HostBatch:
     on the GPU path)."""
 
     def __init__(self, reads=1 << 20, avg_len=160, side_bytes=64 << 20, alloc=numpy_alloc):
-        f = max(reads // 2 + 16, 16)
+        # a processed family holds at least one read per subfamily (min_reads
+        # >= 1); a batch simply ends early when a table fills first
+        f = max(reads // 4 + 16, 16)
         t = 2 * f
         caps = {"r": reads, "f": f, "4f": 4 * f, "4f1": 4 * f + 1, "2f": 2 * f, "2f1": 2 * f + 1, "t": t,
                 "c": 8 * reads, "b": avg_len * reads, "n": 96 * t + (1 << 16), "s": side_bytes}
+        # pinned: what crosses PCIe (the dcr_batch arrays and the writer's
+        # metadata); the family table and the side-file records stay host-only
+        host_only = {"side_exc", "side_filt", "tab_kind", "tab_proc", "tab_sampled", "tab_code", "tab_exc_cut",
+                     "tab_filt_cut"}
         lay, off = [], 0
         for name, dt, ln in _HB_ARRAYS:
-            if ln == "s":
+            if name in host_only:
                 continue
             nb = np.dtype(dt).itemsize * caps[ln]
             off = (off + 255) & ~255
@@ -151,9 +157,8 @@ class HostBatch:
         for name, dt, o, n in lay:
             self.a[name] = self.mem[o:o + n * np.dtype(dt).itemsize].view(dt)
             setattr(s, name, base + o)
-        # the side-file records never cross PCIe: ordinary (lazily paged) memory
         for name, dt, ln in _HB_ARRAYS:
-            if ln == "s":
+            if name in host_only:                   # ordinary (lazily paged) memory
                 self.a[name] = np.empty(caps[ln], dt)
                 setattr(s, name, self.a[name].ctypes.data)
         self.s = s
