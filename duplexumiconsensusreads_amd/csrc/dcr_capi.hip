@@ -96,6 +96,7 @@ struct dcr_ctx {
     uint32_t *d_wtab = nullptr;    // device [DCR_LUT_N] (general kernel's decision pass)
     int n_cu = 256;     // compute units (persistent grid size)
     int dfl_blocks = 1; // resident k_deflate workgroups per CU (dynamic LDS = sizeof(dfl::Shared))
+    size_t rs_bytes = 0;  // the workspace's record-scalar rows
     int fast_blocks[4] = {1, 1, 1, 1};   // resident k_consensus_fast blocks per CU (ss, ds; exact ss, exact ds)
 };
 
@@ -321,6 +322,7 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     const size_t o_stamp = o; o = align_up(o + 32 * sizeof(unsigned long long));
     const size_t n_rec = (size_t)std::max<int64_t>(4LL * s->n_fam, 1);
     const size_t o_ovf = o;  o = align_up(o + sizeof(int) * n_rec);
+    const size_t o_rs = o;   o = align_up(o + 48 * n_rec);
     const size_t o_xl = o;   o = align_up(o + sizeof(int) * n_rec);
     const size_t o_meta = o; o = align_up(o + sizeof(dcr::RecMeta) * n_rec);
     const size_t o_rm = o;   o = align_up(o + sizeof(uint2) * std::max<size_t>((size_t)s->n_reads, n_rec));
@@ -341,6 +343,8 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     c->w.xcount = (int *)(b + o_err) + 5;
     c->w.gen_next = (int *)(b + o_err) + 7;      // [2], in the same block: reset with it per batch
     c->w.xlist = (int *)(b + o_xl);
+    c->w.rs = (uint32_t *)(b + o_rs);
+    c->rs_bytes = 48 * n_rec;
     c->w.stamps = (unsigned long long *)(b + o_stamp);
     c->w.ovf = (int *)(b + o_ovf);
     c->w.meta = (dcr::RecMeta *)(b + o_meta);
@@ -355,6 +359,9 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemsetAsync(c->w.err, 0, 64, c->stream));
+    // record-scalar rows: their markers must read 0 (k_scatter_scalars clears
+    // the rows it uses; the region moves with the workspace layout)
+    if (in->n_fam > 0) HIP_TRY(hipMemsetAsync(c->w.rs, 0, (size_t)48 * 4 * (size_t)in->n_fam, c->stream));
     c->last_reads = in->n_reads;
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     // per-read preprocessing (:191-325) is fused: k_recmeta<ss> analyses the
@@ -381,6 +388,9 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     // ~8 records per wave
     auto fast_grid = [&](int64_t n_rec, int k) {
         return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_rec + 127) / 128, (int64_t)c->fast_blocks[k] * c->n_cu));
+    };
+    auto scatter_grid = [&](int64_t n_rec) {
+        return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_rec + 255) / 256, (int64_t)c->n_cu * 16));
     };
     auto fast_args = [&](bool duplex) {
         dcr::FastArgs f{};
@@ -409,6 +419,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         f.lo_check = duplex || c->host_params.min_base_quality < c->fast_qlo;
         f.llr16 = c->d_llr16;
         f.want_info = (c->options & DCR_OPT_READ_INFO) ? 1 : 0;
+        f.rs = c->w.rs;
         return f;
     };
     auto strand = [&](bool duplex) -> int {
@@ -434,6 +445,8 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
                                0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL((dcr::k_consensus_fast<true, true>), dim3(gx), dim3(dcr::kFastBlock), 0, c->stream, fa);
+            hipLaunchKernelGGL(dcr::k_scatter_scalars, dim3(scatter_grid(a.n_rec)), dim3(256), 0, c->stream,
+                               dcr::ScatterArgs{c->w.rs, c->w.rs, *ds, in->ds_col_off, a.n_rec});
             HIP_TRY(hipEventRecord(ev[2], c->stream));
             hipLaunchKernelGGL(dcr::k_decide<true>, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
             hipLaunchKernelGGL(dcr::k_consensus_general<true>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
@@ -446,6 +459,8 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
                                dim3(dcr::kFastBlock), 0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL((dcr::k_consensus_fast<false, true>), dim3(gx), dim3(dcr::kFastBlock), 0, c->stream, fa);
+            hipLaunchKernelGGL(dcr::k_scatter_scalars, dim3(scatter_grid(a.n_rec)), dim3(256), 0, c->stream,
+                               dcr::ScatterArgs{c->w.rs, c->w.rs, *ss, in->ss_col_off, a.n_rec});
             HIP_TRY(hipEventRecord(ev[2], c->stream));
             hipLaunchKernelGGL(dcr::k_decide<false>, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
             hipLaunchKernelGGL(dcr::k_consensus_general<false>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,

@@ -40,6 +40,7 @@ struct Workspace {
     int *fast_count;        // [2] single-strand / duplex fast-list lengths
     int *xcount;            // [2] single-strand / duplex exact-queue lengths
     int *gen_next;          // [2] next general-list entry to claim (k_consensus_general)
+    uint32_t *rs;           // [n_rec][12] record scalars of the fast kernel's records (k_scatter_scalars)
     int *xlist;             // [n_rec] exact queue: fast-list indices (k_consensus_fast<., true>)
     unsigned long long *stamps;   // [32] diagnostic phase cycles (DCR_STAMP builds only)
     RecMeta *meta;          // [n_rec] fast list
@@ -86,6 +87,17 @@ struct FastArgs {
     int lo_check;                   // some unmasked quality may lie below fast_qlo: check the bytes
     const uint16_t *llr16;          // [123] per-quality LLR term, 1/16 nat, rounded down
     int want_info;                  // single-strand: write every read's dcr_read_info (DCR_OPT_READ_INFO)
+    uint32_t *rs;                   // [n_rec][12] the record's scalar fields, [10] = 1 (k_scatter_scalars)
+};
+
+// the fast kernels' record scalars, one contiguous 48-byte row per record,
+// scattered into the dcr_out arrays by one coalesced pass
+struct ScatterArgs {
+    const uint32_t *rs;
+    uint32_t *rs_clear;
+    dcr_out O;
+    const int64_t *col_off;
+    int64_t n_rec;
 };
 
 __global__ void k_prep(dcr_batch in, const dcr_params *P, Workspace ws);
@@ -94,5 +106,6 @@ __global__ void k_prep_big(Args a);
 template <bool DUPLEX, bool EXACT> __global__ void k_consensus_fast(FastArgs a);
 template <bool DUPLEX> __global__ void k_consensus_general(Args a);
 template <bool DUPLEX> __global__ void k_decide(Args a);
+__global__ void k_scatter_scalars(ScatterArgs s);
 
 }  // namespace dcr

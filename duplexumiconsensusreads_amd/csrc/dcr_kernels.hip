@@ -2669,12 +2669,12 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         }
         lds_fence();
         const int v = *(const int *)(sc + 4 * min(lane, 9));
-        const uint64_t dst = *(const uint64_t *)(lds + fk::kPtrs + 8 * min(lane, 9));
-        uint8_t *p = (uint8_t *)(uintptr_t)(dst & 0x00FFFFFFFFFFFFFFull);
-        if (DCR_ABL != 13) {            // diagnostic 13: no record-scalar stores
-            if (lane < 10) *(int *)(p + rec * (int64_t)((dst >> 56) & 15u) + off * (int64_t)(dst >> 60)) = v;
-            if (lane == 0) O.status[rec] = DCR_ST_OK;
-        }
+        // one contiguous 48-byte row (fields, then the marker) per record,
+        // scattered into the dcr_out arrays by k_scatter_scalars: ten 4-byte
+        // stores into ten arrays each landed in a line L2 evicted before its
+        // neighbours arrived (write amplification, PMC WRITE_SIZE)
+        (void)O;
+        if (DCR_ABL != 13 && lane < 11) a.rs[rec * 12 + lane] = lane < 10 ? (uint32_t)v : 1u;
     }
     sp.mark(10);                         // [9] record scalars
     return true;
@@ -2958,6 +2958,29 @@ __global__ __launch_bounds__(256) void k_decide(Args a) {
         if (T > col_off[rec + 1] - off) continue;
         if (decide_record<DUPLEX>(a, rec, R, T, minpos, a.ws.cons + off, s_stage[wave], s_wtab, lane) && lane == 0)
             a.ws.ovf[i] = (int)rec | (int)0x80000000u;
+    }
+}
+
+// the fast kernels' record scalars (finish_record, one 48-byte row per
+// record, marker [10]) into the dcr_out arrays; rows are cleared for the next
+// strand / batch.  Thread = record: every store is coalesced.
+__global__ __launch_bounds__(256) void k_scatter_scalars(ScatterArgs S) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < S.n_rec; r += (int64_t)gridDim.x * blockDim.x) {
+        const uint4 *row = (const uint4 *)(S.rs + 12 * r);
+        const uint4 c = row[2];
+        if (c.z != 1u) continue;
+        const uint4 a = row[0], b = row[1];
+        S.O.pos[r] = (int32_t)a.x;
+        S.O.mapq[r] = (int32_t)a.y;
+        S.O.len[r] = (int32_t)a.z;
+        S.O.n_cig[r] = (int32_t)a.w;
+        S.O.n_de[r] = (int32_t)b.x;
+        S.O.D[r] = (int32_t)b.y;
+        S.O.M[r] = (int32_t)b.z;
+        ((uint2 *)S.O.E)[r] = make_uint2(b.w, c.x);
+        S.O.cigar[S.col_off[r]] = c.y;
+        S.O.status[r] = DCR_ST_OK;
+        ((uint4 *)(S.rs_clear + 12 * r))[2] = make_uint4(0u, 0u, 0u, 0u);
     }
 }
 
