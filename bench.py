@@ -24,7 +24,8 @@ cpu_baseline: the C restatement (oracle/, kind "port") on the same batch.
 --config C3 / C4 / C5 runs the other BASELINE.json shapes (per-GPU shards).
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
 (N > 1 is launched by torch.distributed.run, one process per GPU; every rank
-owns its own shard of families: weak scaling, no data-path collective.)
+owns its own shard of families: weak scaling, no data-path collective.  C4
+at N > 1 deals one shared stream of N x 1,000 families to the ranks by LPT.)
 """
 from __future__ import annotations
 
@@ -67,6 +68,24 @@ def make_batch(config, families, seed):
     if config == "C2":
         return synth.packed_fixed_size(families, seed=seed)
     return synth.packed_config(synth.CONFIGS[config], families, seed=seed, max_reads=1000)
+
+
+def shared_share(config, families, seed, rank, world):
+    """C4 at N > 1 (the load-balance case): one shared stream
+    of families x N families, cut into consecutive chunks and dealt to ranks
+    by LPT on their read bases (shard.rank_share), so a few deep families do
+    not pile onto one GPU.  Every rank plans from the stream's family sizes
+    (cheap, identical on all ranks) and generates only its own families."""
+    from duplexumiconsensusreads_amd import shard, synth
+    cfg = synth.CONFIGS[config]
+    total = families * world
+    costs = (synth.config_family_reads(cfg, total, seed, max_reads=1000) * cfg.read_len).tolist()
+    mine, loads = shard.rank_share(costs, rank, world)
+    packed = synth.packed_config(cfg, total, seed=seed, max_reads=1000, keep=mine)
+    mean = sum(loads) / world
+    return packed, {"families": total, "rank_read_bases": loads,
+                    "max_over_mean": (max(loads) / mean) if mean else None,
+                    "split": "consecutive chunks of ~1/32 of a rank's share, dealt by LPT (shard.rank_share)"}
 
 
 def log(*a):
@@ -215,7 +234,11 @@ def main():
 
     t0 = time.perf_counter()
     families = args.families or CONFIG_FAMILIES[args.config]
-    packed = make_batch(args.config, families, args.seed + 1000 * rank)
+    shared = None
+    if args.config == "C4" and dist:
+        packed, shared = shared_share(args.config, families, args.seed, rank, world)
+    else:
+        packed = make_batch(args.config, families, args.seed + 1000 * rank)
     log(f"[rank {rank}] generated {packed.n_reads} reads in {time.perf_counter() - t0:.1f} s")
     # C4 runs with --max_reads 1000; the batch is already downsampled
     params = ConsensusParams(max_reads=1000) if args.config == "C4" else ConsensusParams()
@@ -295,7 +318,7 @@ def main():
                                            "records_not_ok": n_bad},
                        "single_strand_stage_GBps": alg / (sum(kavg[k] for k in _lib.KERNELS[1:5]) / 1e3) / 1e9,
                        "parallelism": f"family-sharded x{world}, one process per GPU, no data-path collective",
-                       "per_rank": per_rank},
+                       "per_rank": per_rank, "shared_stream": shared},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": dom_label,

@@ -197,6 +197,38 @@ def _end_soft_clips(cigar, cig_off, cig_n):
     return np.where(has, c5 + c3, 0)
 
 
+def _ranges(starts, lens):
+    """Concatenated aranges [s, s + n) (vectorised)."""
+    lens = lens.astype(np.int64)
+    tot = int(lens.sum())
+    if tot == 0:
+        return np.zeros(0, np.int64)
+    first = np.repeat(np.cumsum(lens) - lens, lens)
+    return np.repeat(starts.astype(np.int64), lens) + (np.arange(tot, dtype=np.int64) - first)
+
+
+def subset_families(packed: PackedBatch, fams) -> PackedBatch:
+    """The batch of families ``fams`` (increasing indices) of ``packed``, in
+    that order: a rank's share of a shared family stream."""
+    fams = np.asarray(fams, np.int64)
+    so = packed.sub_off.astype(np.int64)
+    subs = (fams[:, None] * 4 + np.arange(4)[None, :]).reshape(-1)
+    cnt = so[subs + 1] - so[subs]
+    rd = _ranges(so[subs], cnt)
+    sub_off = np.zeros(len(subs) + 1, np.int64)
+    sub_off[1:] = np.cumsum(cnt)
+    seq_len = packed.seq_len[rd]
+    seq_off = np.zeros(len(rd), np.int64)
+    seq_off[1:] = np.cumsum(seq_len[:-1].astype(np.int64))
+    bi = _ranges(packed.seq_off[rd], seq_len)
+    cig_n = packed.cig_n[rd]
+    cig_off = np.zeros(len(rd), np.int64)
+    cig_off[1:] = np.cumsum(cig_n[:-1].astype(np.int64))
+    ci = _ranges(packed.cig_off[rd], cig_n)
+    return finish_batch(sub_off, packed.read_pos[rd], packed.read_mapq[rd], seq_off, seq_len, cig_off, cig_n,
+                        packed.cigar[ci], packed.bases[bi], packed.quals[bi])
+
+
 def finish_batch(sub_off, read_pos, read_mapq, seq_off, seq_len, cig_off, cig_n, cigar, bases, quals):
     """Compute the output-region offsets (vectorised) and build the batch."""
     n_sub = len(sub_off) - 1

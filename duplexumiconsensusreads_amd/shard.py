@@ -61,6 +61,21 @@ def assign_chunks(chunk_costs: Sequence[int], world: int) -> List[int]:
     return owner
 
 
+def rank_share(costs: Sequence[int], rank: int, world: int, pieces_per_rank: int = 32):
+    """This rank's families of one shared stream with per-family ``costs``:
+    consecutive chunks of about total / (world * pieces_per_rank) each, owned
+    by LPT.  Returns (increasing family indices, every rank's total cost)."""
+    total = int(sum(costs))
+    chunks = plan_chunks(costs, max(1, total // max(1, world * pieces_per_rank)))
+    ccost = [int(sum(costs[a:b])) for a, b in chunks]
+    owner = assign_chunks(ccost, world)
+    loads = [0] * world
+    for c, r in zip(ccost, owner):
+        loads[r] += c
+    mine = [f for (a, b), r in zip(chunks, owner) if r == rank for f in range(a, b)]
+    return mine, loads
+
+
 def run_rank_chunks(results: List[pipeline.FamilyResult], params: ConsensusParams, backend, rank: int,
                     world: int, target_cost: int):
     """This rank's share: run every chunk it owns; returns [(chunk, results)]."""

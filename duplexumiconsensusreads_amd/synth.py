@@ -299,8 +299,19 @@ def packed_fixed_size(n_families, sub_size=8, read_len=150, seed=2, chunk_reads=
     return finish_batch(sub_off, read_pos, mapq, seq_off, seq_len, cig_off, cig_n, cigar, bases, quals)
 
 
+def config_family_reads(cfg: SynthConfig, n_families=None, seed=None, max_reads=None):
+    """Reads per family of ``packed_config``'s stream (its first draw), for
+    planning a split of the stream before generating it."""
+    rng = np.random.default_rng(cfg.seed if seed is None else seed)
+    F = cfg.n_families if n_families is None else n_families
+    sizes = _sub_sizes(rng, cfg, 4 * F).astype(np.int64)
+    if max_reads is not None:
+        sizes = np.minimum(sizes, max_reads)
+    return sizes.reshape(F, 4).sum(1)
+
+
 def packed_config(cfg: SynthConfig, n_families=None, seed=None, max_reads=None, chunk_reads=1 << 18,
-                  threads=None):
+                  threads=None, keep=None):
     """Vectorised generator for any config shape: subfamily
     sizes from ``cfg.sub_size`` (capped at ``max_reads``, the downsampling the
     host would have applied), one I or D of 1-3 bp at offset 20-130 on
@@ -308,10 +319,12 @@ def packed_config(cfg: SynthConfig, n_families=None, seed=None, max_reads=None, 
     ``softclip_frac`` of them, deep-panel loci when ``cfg.n_loci``.  Same base
     / quality / substitution model as ``family_records``; reads are the ones
     that passed ``pass_filters`` (MAPQ 20..60).  For bench-scale batches of
-    the C3 / C4 / C5 shapes, where the per-record generator is too slow."""
+    the C3 / C4 / C5 shapes, where the per-record generator is too slow.
+    ``keep`` (increasing family indices) returns only those families, the
+    same bytes as in the whole stream (a rank's share of a shared stream)."""
     from concurrent.futures import ThreadPoolExecutor
 
-    from .batch import finish_batch
+    from .batch import finish_batch, subset_families
     rng = np.random.default_rng(cfg.seed if seed is None else seed)
     F = cfg.n_families if n_families is None else n_families
     L = cfg.read_len
@@ -396,7 +409,9 @@ def packed_config(cfg: SynthConfig, n_families=None, seed=None, max_reads=None, 
         bases[r0 * L:r1 * L] = seq.reshape(-1)
         quals[r0 * L:r1 * L] = q.reshape(-1)
 
+    todo = range(n_chunks) if keep is None else sorted(set(int(f) // fam_chunk for f in keep))
     with ThreadPoolExecutor(threads or min(16, os.cpu_count() or 1)) as ex:
-        list(ex.map(fill, range(n_chunks)))
-    return finish_batch(sub_off.astype(np.int32), read_pos, mapq, seq_off, seq_len, cig_off, cig_n, cigar, bases,
-                        quals)
+        list(ex.map(fill, todo))
+    packed = finish_batch(sub_off.astype(np.int32), read_pos, mapq, seq_off, seq_len, cig_off, cig_n, cigar, bases,
+                          quals)
+    return packed if keep is None else subset_families(packed, keep)
