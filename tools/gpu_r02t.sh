@@ -13,7 +13,7 @@ cat "$O/bench.json"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/kt" -o kt --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu > "$O/bench_prof.json" 2> "$O/bench_prof.log" || { echo "prof failed"; tail -30 "$O/bench_prof.log"; exit 1; }
 find "$O/kt" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats.csv" \;
 cut -d, -f1-8 "$O/kernel_stats.csv" | head -24
-find "$O/kt" -name "*kernel_trace.csv" -exec python3 tools/kt_grid.py {} k_consensus_fast k_scatter ; > "$O/kernel_grid.csv"
+find "$O/kt" -name "*kernel_trace.csv" -exec python3 tools/kt_grid.py {} k_consensus_fast k_scatter \; > "$O/kernel_grid.csv"
 cat "$O/kernel_grid.csv"
 rm -rf "$O/kt"
 for c in C3 C4 C5; do
