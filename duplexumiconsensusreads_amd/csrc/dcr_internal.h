@@ -18,7 +18,7 @@ constexpr int kFastBlock = kWave * kFastWaves;
 // fast-list order (one scalar 32-byte load per record).
 struct RecMeta {
     uint32_t base_al;   // 16-aligned byte offset of the record's kept bases/quals (< 2^32 - 4096)
-    int32_t d0;         // pos of the record's first read - min_pos
+    int32_t d0;         // pos of the record's first read - min_pos (< 2^16) | MAPQ << 16
     int64_t off;        // output column offset (ss_col_off / ds_col_off)
     int32_t rec;        // record index
     int32_t g0;         // index of its first read in the read-meta array

@@ -1873,7 +1873,7 @@ struct RecAgg {
     int minpos, maxend, flags, kind;
     unsigned long long lo, hi;     // kept byte window; lo becomes base_al for fast records
     unsigned long long fst;        // first failing read: global index << 4 | its status
-    int pos0, pad;                 // pos of the record's first read
+    int pos0, msum;                // pos of the record's first read, sum of the reads' MAPQs
 };
 
 template <bool DUPLEX>
@@ -1944,6 +1944,7 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
                              dpos > 32767) << 2);   // single M run only
             atomicMin(&agg[k].minpos, rd.pos);
             atomicMax(&agg[k].maxend, rd.pos + rd.len);
+            atomicAdd(&agg[k].msum, rd.mapq & 255);
             if (fl) atomicOr(&agg[k].flags, fl);
             if (rd.status) atomicMin(&agg[k].fst, ((unsigned long long)gr << 4) | (unsigned)(rd.status & 15));
             atomicMin(&agg[k].lo, (unsigned long long)rd.seq_start);
@@ -1985,7 +1986,9 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
             } else {
                 kind = 0;
                 m.base_al = (uint32_t)base_al;
-                m.d0 = g.pos0 - g.minpos;
+                // MAPQ = trunc(mean) of the reads' MAPQs (:874-889, :1377), here
+                // rather than a wave reduction per record in the fast kernel
+                m.d0 = (g.pos0 - g.minpos) | ((g.msum / R) << 16);
                 m.off = off;
                 m.rec = (int32_t)rk;
                 m.g0 = g0;
@@ -2084,11 +2087,11 @@ constexpr int kPtrs = kSent + 16;                          // u64 [10] record-sc
 constexpr int kRm = kPtrs + 16 * 8;                        // per wave: u64 [64] the current record's read words
 constexpr int kMv = kRm + kWaves * kWave * 8;              // per wave: u32 [8] a later record's descriptor
 constexpr int kOv = kMv + kWaves * 32;                     // per wave: u16 [256] column words d | e << 6 | call << 12
-constexpr int kDivR = kOv + kWaves * 512;                  // u32 [64] ceil(2^24 / R): msum / R = msum * [R] >> 24
+constexpr int kM720 = kOv + kWaves * 512;                  // u32 [64] 720720 / d for depths d <= 16, else 0
 #ifndef DCR_LDS_PAD
 #define DCR_LDS_PAD 0
 #endif
-constexpr int kLdsBytes = kDivR + 64 * 4 + DCR_LDS_PAD;       // PAD: diagnostic builds only
+constexpr int kLdsBytes = kM720 + 64 * 4 + DCR_LDS_PAD;       // PAD: diagnostic builds only
 static_assert(kStageElems * 2 == 0x1000, "one 4 KiB stage per wave");
 static_assert(16 * (kRowMax + 5) <= 0x800, "a class bank fits 2 KiB");
 static_assert(5 * kLdsBytes <= 160 * 1024, "five blocks (20 waves) per CU");
@@ -2363,7 +2366,6 @@ __device__ __forceinline__ void send_to_general(const FastArgs &a, const RecMeta
 struct Staged {
     uint2 rm;      // the lane's read meta (single-strand: length after the 3' trim)
     int T;         // columns (:458-459, on the trimmed reads)
-    int msum;      // sum of the reads' MAPQs
     int state;     // 0 consensus here, 1 general kernel, 2 finished (status written)
 };
 
@@ -2374,7 +2376,6 @@ __device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &
     Staged s;
     const int R = (int)(m.w & 127u);
     s.T = (int)((m.w >> 7) & 255u);
-    s.msum = wave_sum(lane < R ? ((int)rm.x >> 16) & 255 : 0);
     s.state = 0;
     lds_fence();
     if (!DUPLEX) {
@@ -2402,7 +2403,8 @@ __device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &
             a.info[m.g0 + lane] = inf;
         }
         rm.x = (rm.x & ~0xFF00u) | ((uint32_t)tl << 8);
-        s.T = wave_max(lane < R ? col + tl : 0);
+        // T shrinks only when every read reaching the untrimmed end lost its tail
+        if (__ballot(lane < R && col + tl == s.T) == 0) s.T = wave_max(lane < R ? col + tl : 0);
         if (__ballot(lane < R && tl == 0)) {
             if (lane == 0) write_status_at(a.O, m.rec, DCR_ST_PREP | DCR_ST_INDEX_ERROR);
             s.state = 2;
@@ -2411,6 +2413,15 @@ __device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &
     s.rm = rm;
     if (s.state == 0 && __ballot(bad != 0)) s.state = 1;
     return s;
+}
+
+// k / 1000 correctly rounded for 0 <= k <= 1000 (numpy's round(x, 3) divides
+// rint(1000 x) by 1000): the product with 0.001 and one fma correction,
+// checked exhaustively over that range (tests/test_fast_math.py)
+__device__ __forceinline__ double div1000(int k) {
+    const double kd = (double)k;
+    const double q = kd * 0.001;
+    return __builtin_fma(__builtin_fma(-q, 1000.0, kd), 0.001, q);
 }
 
 // products, finalize, outputs of a staged record of T <= 64 NT columns.
@@ -2426,11 +2437,10 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     const int64_t off = m.off;
     const int R = (int)(m.w & 127u);
     const int T = sg.T;
-    const int msum = sg.msum;
     const int minpos = m.minpos;
     const uint2 rm = sg.rm;
     if (DCR_ABL == 1) {                 // diagnostic: staging only
-        if (lane == 0) O.pos[rec] = *(const uint16_t *)(lds + stage_addr + 2 * (int)(rm.y & 7)) + msum;
+        if (lane == 0) O.pos[rec] = *(const uint16_t *)(lds + stage_addr + 2 * (int)(rm.y & 7)) + m.d0;
         return true;
     }
     const int colr = (int)(rm.x & 255u), lenr = (int)((rm.x >> 8) & 255u);
@@ -2455,7 +2465,11 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     // more reads than r_safe: L_b may underflow (fast_constants), no column is decided here
     const bool force = R > a.r_safe;
     int dmax = -1, dmin = 0x7fffffff;
-    double ex[NT];                     // e/d of the lane's column (0 outside T)
+    // sum over the lane's live columns of e * 720720 / d: the mean's numerator
+    // in fixed point, exact for depths <= 16 (720720 = lcm(1..16); < 2^32 over
+    // 240 columns)
+    uint32_t fx = 0;
+    const uint32_t *m720 = (const uint32_t *)(lds + fk::kM720);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
         const int t = 64 * tt + lane;
@@ -2477,10 +2491,8 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         // decided: LLR_b - max(LLR_k, 0) >= (Lb - L2 - (d - nb)) / 16 >= T16 / 16
         const bool undecided = (int)(Lb - L2) - (d - nb) < a.t16 || force;
         und |= (uint32_t)(live && undecided) << tt;
-        const double etv = (double)e * invd[d];                      // e/d to 1 ulp (the mean's decision
-                                                                     // tolerates 1e-9; the exact walk divides)
         *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (kb << 12));
-        ex[tt] = live ? etv : 0.0;
+        fx += live ? __umul24((uint32_t)e, m720[d]) : 0u;
         dmax = max(dmax, live ? d : -1);
         dmin = min(dmin, live ? d : 0x7fffffff);
     }
@@ -2536,14 +2548,6 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
             }
         }
         lds_fence();
-#pragma unroll
-        for (int tt = 0; tt < NT; ++tt) {
-            if ((und >> tt) & 1u) {
-                const uint32_t w = *(const uint16_t *)(ov + 2 * (64 * tt + lane));
-                const uint32_t d = w & 63u;
-                ex[tt] = d == 0 ? 1.0 : (double)((w >> 6) & 63u) * invd[d];   // e/d, d == 0 -> 1 (:1010-1012)
-            }
-        }
         // kept span: first / last column whose character is not 'N'
         int fst = 0x7fffffff, lst = -1;
 #pragma unroll
@@ -2618,9 +2622,37 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     // sits that close to a half-integer; a DPP tree sum decides, and the exact
     // pairwise walk (over the e/d columns written into the now free stage) runs
     // only near such a boundary.
+    // Every column decided and R <= 16: the mean is the rational
+    // 1000 sum(e/d) / T = 25 fx / (18018 T) exactly (fx = 720720 sum(e/d)), and
+    // its rounding is read off the integer remainder.  A value that is not a
+    // tie lies >= 1 / (2 * 18018 T) > 1e-7 from a half-integer, far beyond the
+    // reference's own double rounding (< 1e-9 here), so rint agrees with
+    // numpy's; a tie, or any other record, takes the double sum below.
+    double E = 0.0;
+    bool slow = exact || R > 16 || DCR_ABL == 4;
+    if (!slow) {
+        const uint32_t S = (uint32_t)wave_sum((int)fx);
+        const int64_t num = 25 * (int64_t)S;
+        const int den = 18018 * T;
+        const double dn = (double)den;
+        double rc = __builtin_amdgcn_rcp(dn);
+        rc = __builtin_fma(__builtin_fma(-dn, rc, 1.0), rc, rc);
+        const int k = __builtin_amdgcn_readfirstlane((int)__builtin_rint((double)num * rc));
+        const int64_t r = num - (int64_t)k * den;
+        slow = 2 * (r < 0 ? -r : r) >= den || k > 1000;                   // a tie (or a bad estimate)
+        E = div1000(k);
+    }
+    if (slow) {
     double sum = 0.0;
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) sum += ex[tt];
+    for (int tt = 0; tt < NT; ++tt) {
+        const int t = 64 * tt + lane;
+        const uint32_t w = *(const uint16_t *)(ov + 2 * t);
+        const uint32_t d = w & 63u;
+        // e/d to 1 ulp (the decision below tolerates 1e-9; the exact walk divides), d == 0 -> 1 (:1010-1012)
+        const double etv = d == 0 ? 1.0 : (double)((w >> 6) & 63u) * invd[d];
+        sum += (tt < NT - 1 || t < T) ? etv : 0.0;
+    }
     sum += dpp_f64<0xB1>(sum);                   // quad_perm [1,0,3,2]
     sum += dpp_f64<0x4E>(sum);                   // quad_perm [2,3,0,1]
     sum += dpp_f64<0x141>(sum);                  // row_half_mirror
@@ -2630,9 +2662,9 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     rt = __builtin_fma(__builtin_fma(-(double)T, rt, 1.0), rt, rt);
     const double y = (sum * rt) * 1000.0;                                    // mean x 1000, to ~1e-15
     const double fr = y - __builtin_floor(y);
-    double E;
     if (__builtin_expect(__builtin_fabs(fr - 0.5) > 1e-9 * (1.0 + y), 1) && DCR_ABL != 4) {
-        E = __builtin_rint(y) / 1000.0;
+        const double ky = __builtin_rint(y);
+        E = ky >= 0.0 && ky <= 1000.0 ? div1000((int)ky) : ky / 1000.0;
     } else {
         lds_fence();
         double *et = (double *)(lds + stage_addr);
@@ -2651,14 +2683,14 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         const double total = 0.0 + pairwise_et(et, T, ln);
         E = __builtin_rint((total / (double)T) * 1000.0) / 1000.0;
     }
+    }
     sp.mark(9);                          // [8] mean
     // the record's scalar fields in one dword store (lane k writes field k,
     // lane 9 the single M run of the CIGAR) plus the status byte
     {
         const int E_lo = (int)(uint32_t)__double_as_longlong(E);
         const int E_hi = (int)(uint32_t)((uint64_t)__double_as_longlong(E) >> 32);
-        // MAPQ = msum / R (:874-889, :1377): exact as msum * ceil(2^24 / R) >> 24 for msum < 2^14
-        const int mapq = (int)(((uint64_t)(uint32_t)msum * *(const uint32_t *)(lds + fk::kDivR + 4 * R)) >> 24);
+        const int mapq = (int)((uint32_t)m.d0 >> 16);                        // k_recmeta
         // lane k takes field k through the wave's (now free) read-word LDS:
         // pos (:790), MAPQ, len, n_cig, n_de, D, M, E (two words), one M run of the kept columns
         uint8_t *sc = lds + rm_addr;
@@ -2722,7 +2754,7 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
     if (threadIdx.x == 0) *(uint16_t *)(lds + fk::kSent) = (uint16_t)fk::kPadCode;
     if (threadIdx.x < 64) {
         const int t = threadIdx.x;
-        ((uint32_t *)(lds + fk::kDivR))[t] = t == 0 ? 0u : ((1u << 24) + (uint32_t)t - 1u) / (uint32_t)t;
+        ((uint32_t *)(lds + fk::kM720))[t] = t == 0 || t > 16 ? 0u : 720720u / (uint32_t)t;
     }
     if (threadIdx.x < 16) {
         const int k = threadIdx.x;
@@ -2789,7 +2821,7 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
         lds_fence();
         const uint2 rw = *(const uint2 *)(lds + rm_addr + 8 * lane);
         // the read's word relative to this record: col | len << 8 | mapq << 16, stage offset
-        const uint2 rm = make_uint2((uint32_t)(((int)rw.x >> 16) + m0.d0) | (rw.x & 0xFFFFu) << 8,
+        const uint2 rm = make_uint2((uint32_t)(((int)rw.x >> 16) + (m0.d0 & 0xFFFF)) | (rw.x & 0xFFFFu) << 8,
                                     rw.y - m0.base_al);
         const RecMeta m2 = meta_from_lanes(*(const uint32_t *)(lds + fk::kMv + 32 * wave + 4 * (lane & 7)));   // record i + 2
         const Staged sg = trim_record<DUPLEX>(a, m0, rm, bad, lds, stage_addr, lane);
