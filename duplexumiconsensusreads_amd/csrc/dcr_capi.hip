@@ -324,6 +324,7 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     const size_t o_ovf = o;  o = align_up(o + sizeof(int) * n_rec);
     const size_t o_rs = o;   o = align_up(o + 48 * n_rec);
     const size_t o_xl = o;   o = align_up(o + sizeof(int) * n_rec);
+    const size_t o_deep = o; o = align_up(o + sizeof(int) * n_rec);
     const size_t o_meta = o; o = align_up(o + sizeof(dcr::RecMeta) * n_rec);
     const size_t o_rm = o;   o = align_up(o + sizeof(uint2) * std::max<size_t>((size_t)s->n_reads, n_rec));
     if (o > c->ws.cap) {
@@ -342,6 +343,8 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     c->w.fast_count = (int *)(b + o_err) + 3;
     c->w.xcount = (int *)(b + o_err) + 5;
     c->w.gen_next = (int *)(b + o_err) + 7;      // [2], in the same block: reset with it per batch
+    c->w.deep_count = (int *)(b + o_err) + 9;    // [1], likewise
+    c->w.deep = (int *)(b + o_deep);
     c->w.xlist = (int *)(b + o_xl);
     c->w.rs = (uint32_t *)(b + o_rs);
     c->rs_bytes = 48 * n_rec;
@@ -463,6 +466,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
                                dcr::ScatterArgs{c->w.rs, c->w.rs, *ss, in->ss_col_off, a.n_rec});
             HIP_TRY(hipEventRecord(ev[2], c->stream));
             hipLaunchKernelGGL(dcr::k_decide<false>, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
+            hipLaunchKernelGGL(dcr::k_decide_deep, dim3(2 * c->n_cu), dim3(dcr::kDeepWaves * dcr::kWave), 0, c->stream, a);
             hipLaunchKernelGGL(dcr::k_consensus_general<false>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
                                c->stream, a);
         }

@@ -13,6 +13,8 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kFastWaves = 4;               // k_consensus_fast: five 4-wave blocks per CU (5 waves per SIMD)
 constexpr int kFastBlock = kWave * kFastWaves;
+constexpr int kDeepReads = 64;              // k_decide: single-strand records of this many reads go to k_decide_deep
+constexpr int kDeepWaves = 8;               // k_decide_deep: waves per record (one 512-thread block, two per CU)
 
 // Per-record launch metadata written by k_recmeta for the fast kernel, in
 // fast-list order (one scalar 32-byte load per record).
@@ -40,6 +42,8 @@ struct Workspace {
     int *fast_count;        // [2] single-strand / duplex fast-list lengths
     int *xcount;            // [2] single-strand / duplex exact-queue lengths
     int *gen_next;          // [2] next general-list entry to claim (k_consensus_general)
+    int *deep;              // [n_rec] general-list indices of deep single-strand records (k_decide_deep)
+    int *deep_count;        // [1] their number
     uint32_t *rs;           // [n_rec][12] record scalars of the fast kernel's records (k_scatter_scalars)
     int *xlist;             // [n_rec] exact queue: fast-list indices (k_consensus_fast<., true>)
     unsigned long long *stamps;   // [32] diagnostic phase cycles (DCR_STAMP builds only)
@@ -106,6 +110,7 @@ __global__ void k_prep_big(Args a);
 template <bool DUPLEX, bool EXACT> __global__ void k_consensus_fast(FastArgs a);
 template <bool DUPLEX> __global__ void k_consensus_general(Args a);
 template <bool DUPLEX> __global__ void k_decide(Args a);
+__global__ void k_decide_deep(Args a);
 __global__ void k_scatter_scalars(ScatterArgs s);
 
 }  // namespace dcr

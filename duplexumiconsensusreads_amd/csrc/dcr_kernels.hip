@@ -673,13 +673,8 @@ struct DecideAcc {
     uint32_t z;
 };
 
-template <bool DUPLEX, int NT>
-__device__ bool decide_tiles(const Args &a, const int64_t rec, const int R, const int T, const int minpos,
-                             int32_t *cw, uint16_t *stage, const uint32_t *s_wtab, const int lane) {
-    const int minbq = a.P->min_base_quality;
-    const uint8_t *gb = DUPLEX ? a.ss.seq : a.in.bases;
-    const uint8_t *gq = DUPLEX ? a.ss.qual : a.in.quals;
-    DecideAcc A[NT];
+template <int NT>
+__device__ __forceinline__ void decide_zero(DecideAcc (&A)[NT]) {
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
 #pragma unroll
@@ -688,14 +683,27 @@ __device__ bool decide_tiles(const Args &a, const int64_t rec, const int R, cons
         for (int k = 0; k < 6; ++k) A[tt].n[k] = 0;
         A[tt].z = 0;
     }
+}
+
+// the rows of reads [r0, r1) of the record added into A (lane = column of
+// each tile); false on an invalid letter, a row quality the bound does not
+// cover, or a read layout other than M / M D M
+
+template <bool DUPLEX, int NT>
+__device__ bool decide_accumulate(const Args &a, const int64_t rec, const int r0, const int r1, const int T,
+                                  const int minpos, uint16_t *stage, const uint32_t *s_wtab, const int lane,
+                                  DecideAcc (&A)[NT]) {
+    const int minbq = a.P->min_base_quality;
+    const uint8_t *gb = DUPLEX ? a.ss.seq : a.in.bases;
+    const uint8_t *gq = DUPLEX ? a.ss.qual : a.in.quals;
     bool bad = false;
-    for (int cb = 0; cb < R; cb += kWave) {
+    for (int cb = r0; cb < r1; cb += kWave) {
         // lane r: read cb + r -- first column, kept length, first byte, and
         // the runs M a1, D b1 (a1 = len, b1 = 0 for one M run)
         int col = 0, len = 0, a1 = 0, b1 = 0;
         int64_t ss = 0;
         bool other = false;
-        const int nr = min(kWave, R - cb);
+        const int nr = min(kWave, r1 - cb);
         if (lane < nr) {
             const ReadRef rd = get_read<DUPLEX>(a, rec, cb + lane);
             col = rd.pos - minpos;
@@ -703,10 +711,10 @@ __device__ bool decide_tiles(const Args &a, const int64_t rec, const int R, cons
             ss = rd.seq_start;
             a1 = len;
             if (rd.ncig == 3) {
-                const uint32_t r0 = rd.cig[0], r1 = rd.cig[1], r2 = rd.cig[2];
-                other = (r0 & 15u) != 0 || (r1 & 15u) != 2 || (r2 & 15u) != 0;
-                a1 = (int)(r0 >> 4);
-                b1 = (int)(r1 >> 4);
+                const uint32_t c0 = rd.cig[0], c1 = rd.cig[1], c2 = rd.cig[2];
+                other = (c0 & 15u) != 0 || (c1 & 15u) != 2 || (c2 & 15u) != 0;
+                a1 = (int)(c0 >> 4);
+                b1 = (int)(c1 >> 4);
             } else {
                 other = rd.ncig != 1 || (rd.cig[0] & 15u) != 0;
             }
@@ -784,6 +792,14 @@ __device__ bool decide_tiles(const Args &a, const int64_t rec, const int R, cons
             rr += nfit;
         }
     }
+    return true;
+}
+
+// the decision from the sums of all R rows: column words kb | d << 3 | e << 15
+// into cw; true when every column is decided
+template <int NT>
+__device__ bool decide_columns(const Args &a, const int R, const int T, const DecideAcc (&A)[NT], int32_t *cw,
+                               const int lane) {
     bool undecided = false;
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
@@ -813,6 +829,15 @@ __device__ bool decide_tiles(const Args &a, const int64_t rec, const int R, cons
     return __ballot(undecided) == 0;
 }
 
+template <bool DUPLEX, int NT>
+__device__ bool decide_tiles(const Args &a, const int64_t rec, const int R, const int T, const int minpos,
+                             int32_t *cw, uint16_t *stage, const uint32_t *s_wtab, const int lane) {
+    DecideAcc A[NT];
+    decide_zero<NT>(A);
+    if (!decide_accumulate<DUPLEX, NT>(a, rec, 0, R, T, minpos, stage, s_wtab, lane, A)) return false;
+    return decide_columns<NT>(a, R, T, A, cw, lane);
+}
+
 template <bool DUPLEX>
 __device__ bool decide_record(const Args &a, const int64_t rec, const int R, const int T, const int minpos,
                               int32_t *cw, uint16_t *stage, const uint32_t *s_wtab, const int lane) {
@@ -823,6 +848,245 @@ __device__ bool decide_record(const Args &a, const int64_t rec, const int R, con
     if (T <= 128) return decide_tiles<DUPLEX, 2>(a, rec, R, T, minpos, cw, stage, s_wtab, lane);
     if (T <= 192) return decide_tiles<DUPLEX, 3>(a, rec, R, T, minpos, cw, stage, s_wtab, lane);
     return decide_tiles<DUPLEX, 4>(a, rec, R, T, minpos, cw, stage, s_wtab, lane);
+}
+
+// ------------------------------------------------ k_decide_deep's row table
+// The staged codes are byte offsets of 32-byte rows of `tab` that hold an
+// element's increments, packed: the LLR terms of A T C G in 16-bit fields
+// (P0); the '-' term (16 bits), the six row counts and a bad-row count (6-bit
+// fields) (P1); z.  A row is one ds_read_b128 plus one ds_read_b32 and three
+// adds instead of a dozen compares and conditional adds; the packed sums are
+// widened every 62 rows (no field overflows: 62 x 1040 < 2^16, 62 < 2^6).
+// Rows (class, quality): A T C G N (0..4) x qualities 0..127 at 5 q + class,
+// so the five classes of one quality sit in five different LDS bank groups
+// (lanes = columns of one read read rows of one quality and mixed letters);
+// the single-strand mask (:280) is folded in (rows of a quality below
+// min_base_quality are 'N' rows); then '-' and the invalid-input row.
+// Qualities >= 128 and invalid letters give up the record (general kernel).
+constexpr uint32_t kTabDel = 5u * 128u * 32u;              // '-' (LUT row 257)
+constexpr uint32_t kTabBad = kTabDel + 32u;                // unused by the codes; kept for completeness
+constexpr uint32_t kTabZero = kTabBad + 32u;               // no row (the missing partner of an odd read)
+constexpr uint32_t kTabPad = (5u * 2u + 4u) * 32u;         // 'N', quality 2 (:509-510, :543-544)
+constexpr int kTabBytes = (int)kTabZero + 32;
+
+// row i of the table; wtab: the LUT rows of the decision pass (dcr_capi.hip wide_table)
+__device__ __forceinline__ void deep_tab_row(uint8_t *tab, int i, const uint32_t *wtab, int minbq) {
+    uint32_t cls, row;
+    if (i < 5 * 128) {
+        cls = (uint32_t)i % 5u;
+        row = (uint32_t)i / 5u;
+        if (cls == 4 || (int)row < minbq) cls = 6;             // 'N' (sequenced or masked)
+    } else if (i == (int)(kTabDel / 32u)) { cls = 5; row = DCR_LUT_DEL; }
+    else if (i == (int)(kTabBad / 32u)) { cls = 7; row = 0; }
+    else {
+        *(uint4 *)(tab + 32 * i) = make_uint4(0u, 0u, 0u, 0u);
+        *(uint4 *)(tab + 32 * i + 16) = make_uint4(0u, 0u, 0u, 0u);
+        return;
+    }
+    const uint32_t w = wtab[row];
+    const uint32_t l = w & 0xFFFFu;
+    const uint32_t bad = cls == 7 || (cls != 6 && (w >> 31) != 0);
+    const uint64_t p0 = cls < 4 ? (uint64_t)l << (16 * cls) : 0ull;
+    const int k = cls < 4 ? (int)cls : (cls == 5 ? 4 : 5);
+    const uint64_t p1 = (cls == 5 ? (uint64_t)l : 0ull) | (cls == 7 ? 0ull : 1ull << (16 + 6 * k)) |
+                        ((uint64_t)bad << 52);
+    *(uint4 *)(tab + 32 * i) = make_uint4((uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32));
+    *(uint4 *)(tab + 32 * i + 16) = make_uint4((w >> 16) & 0x7FFFu, 0u, 0u, 0u);
+}
+
+// four row offsets from four bases and qualities (SWAR): the class from a
+// byte permute of (b >> 1) & 7 (A 0, C 2, T 1, G 3, N 4), whose letter a
+// second permute checks (:580-585); `bad` collects the bits of an invalid
+// letter or a quality >= 128 in the bytes `keep` selects (their codes are
+// then don't-care)
+__device__ __forceinline__ uint2 tab_codes4(uint32_t B, uint32_t Q, uint32_t keep, uint32_t &bad) {
+    const uint32_t h = (B >> 1) & 0x07070707u;
+    const uint32_t cls = __builtin_amdgcn_perm(0x04000000u, 0x03010200u, h);
+    bad |= ((B ^ __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, h)) | (Q & 0x80808080u)) & keep;
+    // per 16-bit field (5 q + class) * 32; no field carries into the next (q < 128)
+    const uint32_t qlo = __builtin_amdgcn_perm(0u, Q, 0x04010400u), qhi = __builtin_amdgcn_perm(0u, Q, 0x04030402u);
+    const uint32_t clo = __builtin_amdgcn_perm(0u, cls, 0x04010400u), chi = __builtin_amdgcn_perm(0u, cls, 0x04030402u);
+    return make_uint2(__umul24(qlo & 0x007F007Fu, 160u) + (clo << 5), __umul24(qhi & 0x007F007Fu, 160u) + (chi << 5));
+}
+
+// decide_accumulate for k_decide_deep (single-strand): the rows of reads
+// [r0, r1) through the table, widened into the block's LDS sums `acc`
+// (12 x 256 words: s[5], n[6], z per column) with ds_add_u32.
+// - staging: range-checked buffer loads based at the stage's first byte (no
+//   exec-masked loads to zero-fill), the next stage's bytes loaded before the
+//   current stage's rows are added;
+// - rows two reads at a time: both reads' codes, then their table rows, then
+//   the adds (64-bit adds of the packed sums), so LDS latencies overlap;
+//   reads without a deletion (the common case) take a short address path.
+template <int NT>
+__device__ bool decide_accumulate_tab(const Args &a, const int64_t rec, const int r0, const int r1, const int T,
+                                      const int minpos, uint16_t *stage, const uint8_t *tab, uint32_t *acc,
+                                      const int lane) {
+    constexpr int kU = kStageElems / 4 / kWave;
+    uint64_t P0[NT], P1[NT];
+    uint32_t Z[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+        P0[tt] = P1[tt] = 0;
+        Z[tt] = 0;
+    }
+    int prow = 0;
+    uint32_t bad = 0;
+    auto widen = [&]() {
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            uint32_t *c = acc + 64 * tt + lane;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) atomicAdd(c + 256 * k, (uint32_t)(P0[tt] >> (16 * k)) & 0xFFFFu);
+            atomicAdd(c + 256 * 4, (uint32_t)P1[tt] & 0xFFFFu);
+#pragma unroll
+            for (int k = 0; k < 6; ++k) atomicAdd(c + 256 * (5 + k), (uint32_t)(P1[tt] >> (16 + 6 * k)) & 63u);
+            atomicAdd(c + 256 * 11, Z[tt]);
+            bad |= (uint32_t)(P1[tt] >> 52);
+            P0[tt] = 0;
+            P1[tt] = 0;
+            Z[tt] = 0;
+        }
+        prow = 0;
+    };
+    for (int cb = r0; cb < r1; cb += kWave) {
+        // lane r: read cb + r -- first column, kept length, first byte, runs M a1, D b1
+        int col = 0, len = 0, a1 = 0, b1 = 0;
+        int64_t ss = 0;
+        bool other = false;
+        const int nr = min(kWave, r1 - cb);
+        if (lane < nr) {
+            const ReadRef rd = get_read<false>(a, rec, cb + lane);
+            col = rd.pos - minpos;
+            len = rd.len;
+            ss = rd.seq_start;
+            a1 = len;
+            if (rd.ncig == 3) {
+                const uint32_t c0 = rd.cig[0], c1 = rd.cig[1], c2 = rd.cig[2];
+                other = (c0 & 15u) != 0 || (c1 & 15u) != 2 || (c2 & 15u) != 0;
+                a1 = (int)(c0 >> 4);
+                b1 = (int)(c1 >> 4);
+            } else {
+                other = rd.ncig != 1 || (rd.cig[0] & 15u) != 0;
+            }
+            other |= len > kStageElems - 4;
+        }
+        if (__ballot(other)) return false;
+        // bytes are addressed from the chunk's first read (a chunk spans < 2^31 bytes)
+        const int64_t s0 = (int64_t)(((uint64_t)(uint32_t)readlane((int)((uint64_t)ss >> 32), 0) << 32) |
+                                     (uint32_t)readlane((int)(uint32_t)ss, 0)) & ~(int64_t)3;
+        const int rel = (int)(ss - s0);              // the lane's read: first byte from s0
+        const int u = rel - col;                      // stage offset of its column 0 + the stage's base
+        // one stage: the reads rr.. that end inside [base, base + 2 KiB)
+        struct Plan { int base, rr, nfit, span; };
+        auto plan = [&](int rr) {
+            Plan p;
+            p.rr = rr;
+            p.base = readlane(rel, rr) & ~3;
+            const bool in = lane >= rr && lane < nr && rel + len - p.base <= kStageElems;
+            const uint64_t fm = ~__ballot(in) >> rr;
+            p.nfit = fm ? min((int)__builtin_ctzll(fm), nr - rr) : nr - rr;
+            const int rlast = rr + p.nfit - 1;
+            p.span = readlane(rel, rlast) + readlane(len, rlast) - p.base;
+            return p;
+        };
+        uint32_t vb[kU], vq[kU];
+        auto load = [&](const Plan &p) {
+            const int nbytes = (p.span + 3) & ~3;
+            const __amdgpu_buffer_rsrc_t rb =
+                __builtin_amdgcn_make_buffer_rsrc((void *)(a.in.bases + s0 + p.base), (short)0, nbytes, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rq =
+                __builtin_amdgcn_make_buffer_rsrc((void *)(a.in.quals + s0 + p.base), (short)0, nbytes, 0x00020000);
+#pragma unroll
+            for (int k = 0; k < kU; ++k) {
+                vb[k] = __builtin_amdgcn_raw_buffer_load_b32(rb, 4 * lane + 256 * k, 0, 0);
+                vq[k] = __builtin_amdgcn_raw_buffer_load_b32(rq, 4 * lane + 256 * k, 0, 0);
+            }
+        };
+        Plan cur = plan(0);
+        load(cur);
+        for (;;) {
+            wave_fence();                             // the previous stage's readers are done
+            const int nd = (cur.span + 3) >> 2;
+#pragma unroll
+            for (int k = 0; k < kU; ++k) {
+                const int d = k * kWave + lane;
+                if (k * kWave < nd) {                 // wave-uniform
+                    const int nb = cur.span - 4 * d;  // bytes of the span in this dword
+                    const uint32_t keep = nb >= 4 ? 0xFFFFFFFFu : (nb > 0 ? (1u << (8 * nb)) - 1u : 0u);
+                    *(uint2 *)&stage[4 * d] = tab_codes4(vb[k], vq[k], keep, bad);
+                }
+            }
+            wave_fence();
+            const int rend = cur.rr + cur.nfit;
+            Plan nxt = cur;
+            if (rend < nr) {                          // the next stage's bytes in flight meanwhile
+                nxt = plan(rend);
+                load(nxt);
+            }
+            // stage index of read r's element in column t: su(r) + t
+            auto su = [&](int r) { return readlane(u, r) - cur.base; };
+            for (int r = cur.rr; r < rend; r += 2) {
+                const bool two = r + 1 < rend;
+                const int rb = two ? r + 1 : r;
+                const int br0 = readlane(b1, r), br1 = two ? readlane(b1, rb) : 0;
+                uint32_t e0[NT], e1[NT];
+                if ((br0 | br1) == 0) {
+                    // one M run each: column t holds element t - col when 0 <= t - col < len
+                    const int c0 = readlane(col, r), l0 = readlane(len, r), s0a = su(r);
+                    const int c1 = readlane(col, rb), l1 = readlane(len, rb), s1a = su(rb);
+#pragma unroll
+                    for (int tt = 0; tt < NT; ++tt) {
+                        const int t = 64 * tt + lane;
+                        e0[tt] = (uint32_t)(t - c0) < (uint32_t)l0 ? (uint32_t)stage[s0a + t] : kTabPad;
+                        e1[tt] = !two ? kTabZero : (uint32_t)(t - c1) < (uint32_t)l1 ? (uint32_t)stage[s1a + t] : kTabPad;
+                    }
+                } else {
+                    auto code = [&](int rr2, uint32_t (&e)[NT]) {
+                        const int cr = readlane(col, rr2), lr = readlane(len, rr2);
+                        const int ar = readlane(a1, rr2), br = readlane(b1, rr2);
+                        const int so = readlane(rel, rr2) - cur.base;
+#pragma unroll
+                        for (int tt = 0; tt < NT; ++tt) {
+                            const int t = 64 * tt + lane;
+                            const int j = t - cr;
+                            const bool del = j >= ar && j < ar + br;
+                            const int is = j < ar ? j : j - br;
+                            if (t >= T || j < 0 || (del ? ar : is) >= lr) e[tt] = kTabPad;   // pad (:514, :540)
+                            else e[tt] = del ? kTabDel : (uint32_t)stage[so + is];
+                        }
+                    };
+                    code(r, e0);
+                    if (two) code(rb, e1);
+                    else
+#pragma unroll
+                        for (int tt = 0; tt < NT; ++tt) e1[tt] = kTabZero;
+                }
+                uint4 f0[NT], f1[NT];
+                uint32_t g0[NT], g1[NT];
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt) {
+                    f0[tt] = *(const uint4 *)(tab + e0[tt]);
+                    g0[tt] = *(const uint32_t *)(tab + e0[tt] + 16);
+                    f1[tt] = *(const uint4 *)(tab + e1[tt]);
+                    g1[tt] = *(const uint32_t *)(tab + e1[tt] + 16);
+                }
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt) {
+                    P0[tt] += (((uint64_t)f0[tt].y << 32) | f0[tt].x) + (((uint64_t)f1[tt].y << 32) | f1[tt].x);
+                    P1[tt] += (((uint64_t)f0[tt].w << 32) | f0[tt].z) + (((uint64_t)f1[tt].w << 32) | f1[tt].z);
+                    Z[tt] += g0[tt] + g1[tt];
+                }
+                prow += 2;
+                if (prow >= 62) widen();              // <= 62 rows per packed field
+            }
+            if (__ballot(bad != 0)) return false;     // an invalid byte staged; bad rows at the next widening
+            if (rend >= nr) break;
+            cur = nxt;
+        }
+    }
+    widen();
+    return __ballot(bad != 0) == 0;
 }
 
 // One column tile of the general kernel's layouts decided from integer LLR
@@ -2971,6 +3235,10 @@ __global__ __launch_bounds__(256) void k_decide(Args a) {
         const int64_t rec = a.ws.ovf[i];
         const int R = DUPLEX ? 2 : (a.in.sub_off[rec + 1] - a.in.sub_off[rec]);
         if (R <= 0) continue;
+        if (!DUPLEX && R >= kDeepReads) {            // the block-cooperative pass below
+            if (lane == 0) a.ws.deep[atomicAdd(a.ws.deep_count, 1)] = i;
+            continue;
+        }
         int minpos = 0x7fffffff, maxend = -0x7fffffff, up = 0;
         for (int c = 0; c < R; c += kWave) {
             const int r = c + lane;
@@ -2991,6 +3259,112 @@ __global__ __launch_bounds__(256) void k_decide(Args a) {
         if (decide_record<DUPLEX>(a, rec, R, T, minpos, a.ws.cons + off, s_stage[wave], s_wtab, lane) && lane == 0)
             a.ws.ovf[i] = (int)rec | (int)0x80000000u;
     }
+}
+
+// k_decide for deep single-strand records (R >= kDeepReads, queued by
+// k_decide): one 8-wave block per record, two blocks per CU.  Wave w adds the
+// rows of reads [R w / 8, R (w + 1) / 8) (decide_accumulate with the packed
+// row table, its own LDS stage); the integer partial sums meet in LDS
+// (ds_add_u32, exact: the sums are order-free) and wave 0 decides.  A
+// 1,000-read subfamily no longer sets the pass's length on one wave (C4).
+template <int NT, class Mark>
+__device__ void decide_deep_record(const Args &a, const int i, const int64_t rec, const int R, const int T,
+                                   const int minpos, uint16_t *stage, const uint32_t *s_wtab, const uint8_t *tab,
+                                   uint32_t *s_acc, int *s_fail, const int wave, const int lane, Mark mark) {
+    DecideAcc A[NT];
+    const int r0 = (int)((int64_t)R * wave / kDeepWaves), r1 = (int)((int64_t)R * (wave + 1) / kDeepWaves);
+    const bool ok = decide_accumulate_tab<NT>(a, rec, r0, r1, T, minpos, stage, tab, s_acc, lane);
+    if (!ok && lane == 0) *s_fail = 1;
+    mark();
+    __syncthreads();
+    if (wave == 0 && *s_fail == 0) {
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            const uint32_t *c = s_acc + 64 * tt + lane;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) A[tt].s[k] = c[256 * k];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) A[tt].n[k] = c[256 * (5 + k)];
+            A[tt].z = c[256 * 11];
+        }
+        const int64_t off = a.in.ss_col_off[rec];
+        if (decide_columns<NT>(a, R, T, A, a.ws.cons + off, lane) && lane == 0) a.ws.ovf[i] = (int)rec | (int)0x80000000u;
+    }
+}
+
+__global__ __launch_bounds__(kDeepWaves * kWave, 2 * kDeepWaves / 4) void k_decide_deep(Args a) {
+    __shared__ uint32_t s_wtab[DCR_LUT_N];
+    __shared__ __attribute__((aligned(16))) uint16_t s_stage[kDeepWaves][kStageElems];
+    __shared__ uint32_t s_acc[12 * 256];        // per column: s[5], n[6], z
+    __shared__ int s_red[4];                    // min pos, max end, unusable read, failed wave
+    __shared__ __attribute__((aligned(16))) uint8_t s_tab[kTabBytes];
+    if (a.t16 < 0) return;
+    for (int i = threadIdx.x; i < DCR_LUT_N; i += blockDim.x) s_wtab[i] = a.wtab[i];
+    {
+        const int minbq = a.P->min_base_quality;
+        for (int i = threadIdx.x; i < kTabBytes / 32; i += blockDim.x) deep_tab_row(s_tab, i, a.wtab, minbq);
+    }
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int n = *a.ws.deep_count;
+    const bool aligned = ((((uintptr_t)a.in.bases) | ((uintptr_t)a.in.quals)) & 3) == 0;
+    uint64_t st_acc[4] = {0, 0, 0, 0}, st_t = 0;           // DCR_STAMP builds: cycles per phase
+    auto stamp = [&](int ph) {
+        if (DCR_STAMP) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            if (ph > 0) st_acc[ph - 1] += now - st_t;
+            st_t = now;
+        }
+    };
+    for (int k = blockIdx.x; k < n; k += gridDim.x) {
+        stamp(0);
+        const int i = a.ws.deep[k];
+        const int64_t rec = a.ws.ovf[i];
+        const int g0 = a.in.sub_off[rec];
+        const int R = a.in.sub_off[rec + 1] - g0;
+        for (int j = threadIdx.x; j < 12 * 256; j += blockDim.x) s_acc[j] = 0;
+        if (threadIdx.x == 0) {
+            s_red[0] = 0x7fffffff;
+            s_red[1] = -0x7fffffff;
+            s_red[2] = 0;
+            s_red[3] = 0;
+        }
+        __syncthreads();
+        // k_decide's checks over the whole block (:458-459 for T)
+        int minpos = 0x7fffffff, maxend = -0x7fffffff, up = 0;
+        for (int r = threadIdx.x; r < R; r += blockDim.x) {
+            const ReadRef rd = get_read<false>(a, rec, r);
+            up |= rd.status != 0 || rd.len <= 0 || a.ws.info[g0 + r].has_ins;
+            minpos = min(minpos, rd.pos);
+            maxend = max(maxend, rd.pos + rd.len);
+        }
+        minpos = wave_min(minpos);
+        maxend = wave_max(maxend);
+        const bool wup = __ballot(up) != 0;
+        if (lane == 0) {
+            atomicMin(&s_red[0], minpos);
+            atomicMax(&s_red[1], maxend);
+            if (wup) s_red[2] = 1;
+        }
+        __syncthreads();
+        const int mp = s_red[0];
+        const int T = s_red[1] - mp;
+        const int64_t off = a.in.ss_col_off[rec];
+        const bool take = !s_red[2] && aligned && R <= 4095 && T > 0 && T <= 256 && T <= a.in.ss_col_off[rec + 1] - off;
+        stamp(1);                               // [0] checks over the reads
+        if (take) {                             // block-uniform
+            uint16_t *st = s_stage[wave];
+            auto mk = [&]() { stamp(2); };      // [1] the wave's rows (decide_accumulate_tab)
+            if (T <= 64) decide_deep_record<1>(a, i, rec, R, T, mp, st, s_wtab, s_tab, s_acc, &s_red[3], wave, lane, mk);
+            else if (T <= 128) decide_deep_record<2>(a, i, rec, R, T, mp, st, s_wtab, s_tab, s_acc, &s_red[3], wave, lane, mk);
+            else if (T <= 192) decide_deep_record<3>(a, i, rec, R, T, mp, st, s_wtab, s_tab, s_acc, &s_red[3], wave, lane, mk);
+            else decide_deep_record<4>(a, i, rec, R, T, mp, st, s_wtab, s_tab, s_acc, &s_red[3], wave, lane, mk);
+        }
+        __syncthreads();                        // s_acc / s_red reused by the next record
+        stamp(3);                               // [2] the rest (the decision on wave 0, barriers)
+    }
+    if (DCR_STAMP && lane == 0)
+        for (int q = 0; q < 3; ++q) atomicAdd(&a.ws.stamps[26 + q], (unsigned long long)st_acc[q]);
 }
 
 // the fast kernels' record scalars (finish_record, one 48-byte row per
