@@ -45,10 +45,48 @@ inline void wr32(uint8_t *p, uint32_t v) {
     p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
 }
 
+// Mappings of released HugeBufs kept for the next ones (up to 1 GiB per
+// process): an ingest maps ~210 MB of chunk buffers, and a fresh mapping pays
+// its page faults again on every open (the CLI run after run in one process).
+// Never unmapped at exit (the process's end reclaims them).
+struct HugeCache {
+    std::mutex mu;
+    std::vector<std::pair<uint8_t *, size_t>> regions;
+    size_t bytes = 0;
+    static constexpr size_t kMax = (size_t)1 << 30;
+    static HugeCache &get() {
+        static HugeCache *c = new HugeCache;
+        return *c;
+    }
+    // the smallest kept mapping of at least `cap` bytes (and at most twice that)
+    uint8_t *take(size_t cap, size_t &got) {
+        std::lock_guard<std::mutex> g(mu);
+        size_t best = regions.size();
+        for (size_t i = 0; i < regions.size(); ++i)
+            if (regions[i].second >= cap && regions[i].second <= 2 * cap &&
+                (best == regions.size() || regions[i].second < regions[best].second))
+                best = i;
+        if (best == regions.size()) return nullptr;
+        uint8_t *p = regions[best].first;
+        got = regions[best].second;
+        regions.erase(regions.begin() + (long)best);
+        bytes -= got;
+        return p;
+    }
+    bool give(uint8_t *p, size_t cap) {
+        std::lock_guard<std::mutex> g(mu);
+        if (bytes + cap > kMax) return false;
+        regions.emplace_back(p, cap);
+        bytes += cap;
+        return true;
+    }
+};
+
 // Large host buffer on transparent huge pages (2 MiB) where the kernel
 // allows it: the record walk reads inflated data at irregular strides, and
 // with 4 KiB pages every few records cost a TLB miss.  resize() keeps the
-// contents only when the capacity suffices.
+// contents only when the capacity suffices; a new buffer's bytes are
+// unspecified (a recycled mapping, HugeCache).
 class HugeBuf {
   public:
     HugeBuf() = default;
@@ -60,6 +98,14 @@ class HugeBuf {
         release();
         constexpr size_t kHP = (size_t)2 << 20;
         const size_t cap = (n + kHP - 1) & ~(kHP - 1);
+        size_t got = 0;
+        uint8_t *q = HugeCache::get().take(cap, got);
+        if (q) {
+            p_ = q;
+            cap_ = got;
+            n_ = n;
+            return;
+        }
         void *p = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
         if (p == MAP_FAILED) throw std::bad_alloc();
         (void)madvise(p, cap, MADV_HUGEPAGE);
@@ -73,7 +119,7 @@ class HugeBuf {
 
   private:
     void release() {
-        if (p_) munmap(p_, cap_);
+        if (p_ && !HugeCache::get().give(p_, cap_)) munmap(p_, cap_);
         p_ = nullptr;
         cap_ = n_ = 0;
     }

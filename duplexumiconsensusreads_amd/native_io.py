@@ -130,6 +130,7 @@ class HostBatch:
     on the GPU path)."""
 
     def __init__(self, reads=1 << 20, avg_len=160, side_bytes=64 << 20, alloc=numpy_alloc):
+        self.reads = reads
         # a processed family holds at least one read per subfamily (min_reads
         # >= 1); a batch simply ends early when a table fills first
         f = max(reads // 4 + 16, 16)

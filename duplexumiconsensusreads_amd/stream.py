@@ -171,10 +171,16 @@ class DeviceStream:
     device (dcr_submit_write); otherwise the kernel outputs come back for the
     host writer (dcr_submit)."""
 
-    def __init__(self, ctx, n_slots=2, owns_ctx=False, device_writer=True):
+    def __init__(self, ctx, n_slots=2, owns_ctx=False, device_writer=True, persistent=False):
+        """``persistent``: ``close`` only drains the slots (the context and the
+        released host batches stay for the next run, cli.default_backend);
+        ``close(final=True)`` frees them."""
         from . import _lib
         self.ctx = ctx
         self.owns_ctx = owns_ctx
+        self.persistent = persistent
+        self.closed = False
+        self._spare = {}                 # reads -> [HostBatch] released by earlier runs
         self.device_writer = device_writer
         self.lib = _lib.load()
         self.n_slots = n_slots
@@ -185,7 +191,16 @@ class DeviceStream:
         self._pins = []
 
     def host_batch(self, reads=1 << 20):
+        spare = self._spare.get(reads)
+        if spare:
+            return spare.pop()
         return native_io.HostBatch(reads=reads, alloc=pinned_allocator(self.lib, self._pins))
+
+    def release(self, batches):
+        """Host batches a run is done with, kept for the next run (persistent)."""
+        if self.persistent and not self.closed:
+            for hb in batches:
+                self._spare.setdefault(hb.reads, []).append(hb)
 
     def submit(self, hb):
         slot = self.next_slot
@@ -241,7 +256,9 @@ class DeviceStream:
         out = self.outs[slot]
         return out.fmt_out("ss"), out.fmt_out("ds"), None
 
-    def close(self):
+    def close(self, final=False):
+        if self.closed:
+            return
         for slot in range(self.n_slots):
             if self.busy[slot]:
                 if self.device_writer:
@@ -249,6 +266,20 @@ class DeviceStream:
                 else:
                     self.lib.dcr_wait(self.ctx._ctx, slot)
                 self.busy[slot] = False
+        if self.persistent and not final:
+            return
+        self.closed = True
+        self._spare.clear()
+        for p in self._pins:
+            p.free()
+        self._pins.clear()
+        for o in self.outs:
+            if o.mem is not None:
+                o.mem.free()
+        for w in self.wouts:
+            for m in (w.small, w.blocks):
+                if m is not None:
+                    m.free()
         if self.owns_ctx:
             self.ctx.close()
 
