@@ -220,3 +220,38 @@ def test_gpu_underflow_columns(ctx, maxq, nreads):
     want = dcr_oracle_c.run(packed, params, n_threads=8)
     assert want[0].record(0, packed.ss_col_off)["seq"][10] == "A"
     assert_same(packed, got, want)
+
+
+# k_decide_deep (records of >= 64 reads): its staged codes carry the class,
+# the single-strand mask and the invalid-input checks four bytes at a time,
+# and its row table covers qualities 0..127.  Deep subfamilies with deletions
+# and insertions, 'N', invalid letters, masked and out-of-table qualities
+# sprinkled over their reads, under two mask thresholds.
+@pytest.mark.parametrize("seed,minbq,rate", [(21, 20, 0.01), (22, 30, 0.02), (23, 2, 0.005)])
+def test_gpu_deep_records_edge_bytes(ctx, seed, minbq, rate):
+    cfg = synth.SynthConfig("t", 6, sub_size="loguniform", logu_lo=64, logu_hi=400, indel_frac=0.1,
+                            softclip_frac=0.2, n_loci=1, seed=seed)
+    packed = synth.packed_from_records(cfg)
+    rng = np.random.default_rng(seed)
+    n = len(packed.bases)
+    hit = np.nonzero(rng.random(n) < rate)[0]
+    kind = rng.integers(0, 4, len(hit))
+    b, q = packed.bases.copy(), packed.quals.copy()
+    packed.bases, packed.quals = b, q
+    b[hit[kind == 0]] = ord("N")
+    q[hit[kind == 1]] = 1                 # masked below min_base_quality (:280)
+    q[hit[kind == 2]] = 0
+    # outside the row table (the record leaves the decision pass): a few records only
+    q[hit[(kind == 3) & (hit < n // 6)]] = 130
+    # invalid letters (the reference exits, :580-585) in two subfamilies, one masked
+    s0, s1 = packed.seq_off[packed.sub_off[5]], packed.seq_off[packed.sub_off[14]]
+    b[s0 + 40] = ord("X")
+    b[s1 + 7], q[s1 + 7] = ord("a"), 1
+    params = ConsensusParams(max_reads=10_000, min_base_quality=minbq)
+    ctx.set_params(params)
+    try:
+        got = ctx.run_host(packed)
+        want = dcr_oracle_c.run(packed, params)
+        assert_same(packed, got, want)
+    finally:
+        ctx.set_params(ConsensusParams())
