@@ -377,7 +377,7 @@ class _Driver:
 
     def run(self, batch_reads):
         """Ingest thread -> device -> writer, in input order."""
-        n_buf = 3
+        n_buf = 4                       # filling, queued, on the device, being written
         free = queue.Queue()
         t0 = time.perf_counter()
         batches = [self.backend.host_batch(batch_reads) for _ in range(n_buf)]
