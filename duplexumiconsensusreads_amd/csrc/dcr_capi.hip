@@ -98,6 +98,8 @@ struct dcr_ctx {
     int dfl_blocks = 1; // resident k_deflate workgroups per CU (dynamic LDS = sizeof(dfl::Shared))
     size_t rs_bytes = 0;  // the workspace's record-scalar rows
     int fast_blocks[4] = {1, 1, 1, 1};   // resident k_consensus_fast blocks per CU (ss, ds; exact ss, exact ds)
+    int pair_blocks = 1;                  // resident k_consensus_pair blocks per CU
+    int pair_env = 0;                     // DCR_PAIR=1 turns the pair kernel on (measured slower)
 };
 
 // The fast kernel's assumptions (dcr_kernels.hip, fast kernel v2): every
@@ -244,6 +246,14 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->fast_blocks[k], fk[k], dcr::kFastBlock, 0) != hipSuccess ||
             c->fast_blocks[k] < 1)
             c->fast_blocks[k] = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->pair_blocks, (const void *)dcr::k_consensus_pair,
+                                                     dcr::kWave * 4, 0) != hipSuccess ||
+        c->pair_blocks < 1)
+        c->pair_blocks = 1;
+    {
+        const char *e = std::getenv("DCR_PAIR");
+        c->pair_env = e && e[0] == '1';
+    }
     if (hipFuncSetAttribute((const void *)dcrw::k_deflate, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(dfl::Shared)) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->dfl_blocks, dcrw::k_deflate, dfl::kT, sizeof(dfl::Shared)) !=
@@ -344,6 +354,7 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     c->w.xcount = (int *)(b + o_err) + 5;
     c->w.gen_next = (int *)(b + o_err) + 7;      // [2], in the same block: reset with it per batch
     c->w.deep_count = (int *)(b + o_err) + 9;    // [1], likewise
+    c->w.pair_count = (int *)(b + o_err) + 10;   // [1], likewise
     c->w.deep = (int *)(b + o_deep);
     c->w.xlist = (int *)(b + o_xl);
     c->w.rs = (uint32_t *)(b + o_rs);
@@ -380,6 +391,9 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     a.ds = *ds;
     a.fast_ok = c->fast_ok;
     a.t16 = c->wide_ok ? c->fast_t16 : -1;     // -1: no decision pass
+    // the pair kernel: the fast kernel's default quality checks (no quality
+    // below fast_qlo left unmasked) and its decision constants
+    a.pair_ok = c->pair_env && c->fast_ok && c->host_params.min_base_quality >= c->fast_qlo;
     a.wtab = c->d_wtab;
     // per strand: k_recmeta classifies every record (fast list / general list /
     // status written), then the fast kernel (8 records per wave) drains the fast list and
@@ -423,6 +437,8 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         f.llr16 = c->d_llr16;
         f.want_info = (c->options & DCR_OPT_READ_INFO) ? 1 : 0;
         f.rs = c->w.rs;
+        f.pair_count = c->w.pair_count;
+        f.pair_top = a.n_rec - 1;
         return f;
     };
     auto strand = [&](bool duplex) -> int {
@@ -458,6 +474,13 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
             hipLaunchKernelGGL(dcr::k_recmeta<false>, dim3(nb), dim3(256), 0, c->stream, a);
             hipLaunchKernelGGL(dcr::k_prep_big, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
             HIP_TRY(hipEventRecord(ev[0], c->stream));
+            // the pair list (two records per wave) and the fast list: the
+            // single-strand consensus slot times both
+            if (a.pair_ok)
+                hipLaunchKernelGGL(dcr::k_consensus_pair,
+                                   dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((a.n_rec + 255) / 256,
+                                                                    (int64_t)c->pair_blocks * c->n_cu))),
+                                   dim3(dcr::kWave * 4), 0, c->stream, fa);
             hipLaunchKernelGGL((dcr::k_consensus_fast<false, false>), dim3(fast_grid(a.n_rec, 0)),
                                dim3(dcr::kFastBlock), 0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[1], c->stream));

@@ -2248,7 +2248,11 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
                 !a.fast_ok || base_al + span >= 0xFFFFF000ll) {
                 kind = 1;
             } else {
-                kind = 0;
+                // the pair shape (k_consensus_pair): few reads, short, in the batch's first 2 GiB
+                kind = !DUPLEX && a.pair_ok && R <= kPairMaxR && T <= kPairMaxT && span <= 4 * kPairMaxDw &&
+                               base_al + span < 0x7FFFF000ll
+                           ? 3
+                           : 0;
                 m.base_al = (uint32_t)base_al;
                 // MAPQ = trunc(mean) of the reads' MAPQs (:874-889, :1377), here
                 // rather than a wave reduction per record in the fast kernel
@@ -2266,22 +2270,26 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
     }
     const uint64_t bf = __ballot(kind == 0);
     const uint64_t bg = __ballot(kind == 1);
-    int basef = 0, baseg = 0;
+    const uint64_t bp = __ballot(kind == 3);
+    int basef = 0, baseg = 0, basep = 0;
     if (lane == 0) {
         if (bf) basef = atomicAdd(&a.ws.fast_count[DUPLEX ? 1 : 0], __popcll(bf));
         if (bg) baseg = atomicAdd(&a.ws.ovf_count[DUPLEX ? 1 : 0], __popcll(bg));
+        if (bp) basep = atomicAdd(a.ws.pair_count, __popcll(bp));
     }
     basef = __shfl(basef, 0);
     baseg = __shfl(baseg, 0);
+    basep = __shfl(basep, 0);
     const uint64_t lt = lanemask_lt(lane);
     if (kind == 0) a.ws.meta[basef + __popcll(bf & lt)] = m;
+    if (kind == 3) a.ws.meta[a.n_rec - 1 - (basep + __popcll(bp & lt))] = m;   // the pair list, from the top
     if (kind == 1) a.ws.ovf[baseg + __popcll(bg & lt)] = (int)rk;
     // single-strand reads of records the fast kernel does not take need the full
     // preprocessing (3' trim included) for the general kernel and the host;
     // records of more than 64 reads are left to k_prep_big (a block per record,
     // not one wave walking every read of 64 records)
-    if (!DUPLEX) agg[lane].kind = (vk && R > kWave) ? 2 : kind;
-    if (DUPLEX || __ballot(vk && kind != 0 && R <= kWave) == 0) return;
+    if (!DUPLEX) agg[lane].kind = (vk && R > kWave) ? 2 : (kind == 3 ? 0 : kind);
+    if (DUPLEX || __ballot(vk && kind != 0 && kind != 3 && R <= kWave) == 0) return;
     lds_fence();
     carry = -1;
     for (int64_t c = gbeg; c < gend; c += kWave) {
@@ -3133,6 +3141,467 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
     if (!EXACT && npend) flush(lane0);
     if (DCR_STAMP && lane0 == 0)
         for (int k = 0; k < 10; ++k) atomicAdd(&a.stamps[k + (DUPLEX ? 16 : 0)], (unsigned long long)sp.acc[k]);
+}
+
+// ------------------------------------------------ pair kernel (two records per wave)
+// k_consensus_fast's records of the pair shape (single-strand, R <= 16,
+// T <= 160, <= 1,280 staged bytes, default quality checks): lanes 0-31 take
+// one record and lanes 32-63 the next, each half with its own LDS stage, read
+// words and column words.  The per-column work runs on five 32-column half
+// tiles per record (150 columns: 160 lanes instead of 192), and every
+// per-record step (descriptors, trim, reductions, mean, stores, scalars) is
+// shared by two records.  The arithmetic is k_consensus_fast's: the integer
+// decision over 1/16-nat LLR bounds, d / e / call words, the fixed-point mean
+// (R <= 16).  A record with a column the bound does not decide, a tie in the
+// mean, or R above r_safe goes to the EXACT queue (k_consensus_fast<., true>
+// recomputes it whole); invalid input goes to the general kernel.
+namespace pk {
+constexpr int kWaves = 4;
+constexpr int kBlockThreads = kWave * kWaves;
+constexpr int kNT = kPairMaxT / 32;                        // half tiles per record
+constexpr int kDw = kPairMaxDw / 32;                       // staged dwords per half lane
+constexpr int kStageB = 4 * kPairMaxDw * 2;                // codes of one record: 2,560 B
+constexpr int kZero = fk::kTable;                          // 16 zero bytes: a row that adds nothing
+constexpr int kSent = kZero + 16;                          // u16 fk::kPadCode: a column outside the read
+constexpr int kZSent = kSent + 2;                          // u16 kZero: a read the half's record does not have
+constexpr int kM720 = kSent + 16;                          // u32 [64] 720720 / d for d <= 16
+constexpr int kW0 = kM720 + 256;                           // per-wave regions
+constexpr int kRmO = 2 * kStageB;                          // uint2 [2][16] read words
+constexpr int kCrO = kRmO + 2 * 16 * 8;                    // int [2][16] LDS address of read r's column 0
+constexpr int kOvO = kCrO + 2 * 16 * 4;                    // u16 [2][160] column words d | e << 6 | call << 12
+constexpr int kScO = kOvO + 2 * kPairMaxT * 2;             // [2][48] record scalars
+constexpr int kPW = kScO + 2 * 48;
+constexpr int kLds = kW0 + kWaves * kPW;
+static_assert(kPW % 16 == 0, "16-byte aligned per-wave regions");
+static_assert(4 * kLds <= 160 * 1024, "four blocks per CU");
+}  // namespace pk
+
+// max / min / sum over each half of the wave: DPP inside rows, then the row
+// broadcast that folds row 0 into row 1 and row 2 into row 3 (no row_bcast:31);
+// .x = lanes 0-31, .y = lanes 32-63
+template <class F>
+__device__ __forceinline__ int2 half_reduce(int v, int ident, F op) {
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x140, 0xF, 0xF, false));  // row_mirror
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    return make_int2(__builtin_amdgcn_readlane(v, 31), __builtin_amdgcn_readlane(v, 63));
+}
+__device__ __forceinline__ int2 half_max(int v) {
+    return half_reduce(v, -0x7fffffff - 1, [](int x, int y) { return max(x, y); });
+}
+__device__ __forceinline__ int2 half_min(int v) {
+    return half_reduce(v, 0x7fffffff, [](int x, int y) { return min(x, y); });
+}
+__device__ __forceinline__ int2 half_sum(int v) {
+    return half_reduce(v, 0, [](int x, int y) { return x + y; });
+}
+__device__ __forceinline__ uint32_t half_bits(uint64_t b, int h) { return (uint32_t)(h ? b >> 32 : b); }
+
+// a pair's staged bytes (both halves) and read words, in flight during the
+// previous pair
+struct PairStage {
+    uint32_t vb[pk::kDw], vq[pk::kDw];   // dword 32 u + (lane & 31) of the half's record
+    uint2 rm;                            // read (lane & 31) of the half's record
+};
+
+__device__ __forceinline__ void pair_load(const FastArgs &a, const RecMeta &m, int R, int l, PairStage &st,
+                                          const __amdgpu_buffer_rsrc_t rb, const __amdgpu_buffer_rsrc_t rq,
+                                          int ndw_max) {
+#pragma unroll
+    for (int u = 0; u < pk::kDw; ++u) {
+        if (u * 32 < ndw_max) {
+            const int off = (int)m.base_al + 4 * (32 * u + l);
+            st.vb[u] = __builtin_amdgcn_raw_buffer_load_b32(rb, off, 0, 0);
+            st.vq[u] = __builtin_amdgcn_raw_buffer_load_b32(rq, off, 0, 0);
+        }
+    }
+    st.rm = a.rmeta[m.g0 + min(l, max(R - 1, 0))];
+}
+
+// the per-column state a record's half tiles leave behind
+struct PairCols {
+    uint32_t und;    // bit tt: the lane's live column of half tile tt is not decided
+    uint32_t fx;     // sum over its live columns of e * 720720 / d (the mean's numerator)
+    int dmax, dmin;
+};
+
+// evidence sums and the decision for half tiles [T0, T1) of both records of
+// the pair (k_consensus_fast's arithmetic): column words d | e << 6 | call << 12
+// into the half's LDS column words
+template <int T0, int T1>
+__device__ __forceinline__ void pair_tiles(const FastArgs &a, const uint8_t *lds, bool full, int Rmax, int R, int T,
+                                           int h, int l, int crv, int x0, int ov_h, PairCols &pc) {
+    constexpr int N = T1 - T0;
+    uint64_t llr[N];
+    uint32_t cnt[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        llr[k] = 0;
+        cnt[k] = 0;
+    }
+    // the LDS address of read r's column 32 T0 + l in this lane's half (lane r of
+    // each half holds its record's column-0 address: no LDS round trip per read)
+    auto addr0 = [&](int r) {
+        const int a0 = readlane(crv, r), a1 = readlane(crv, 32 + r);
+        return (h ? a1 : a0) + 2 * (32 * T0 + l);
+    };
+    auto row = [&](uint32_t code, uint2 &f, uint32_t &c) {   // 8-byte LLR increment, count increment (word 3)
+        const uint4 v = *(const uint4 *)(lds + code);           // one ds_read_b128 (word 2 is 0)
+        f = make_uint2(v.x, v.y);
+        c = v.z + v.w;
+    };
+    if (full) {
+        // two reads per step: the rows of reads r, r + 1 in flight while the codes
+        // of r + 2, r + 3 are read; no 16-bit field reaches 2^16 (16 rows of at
+        // most 1040), so the halves add without carries
+        uint32_t c0[N], c1[N];
+        {
+            const int a0 = addr0(0), a1 = addr0(min(1, Rmax - 1));
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                c0[k] = *(const uint16_t *)(lds + a0 + 64 * k);
+                c1[k] = Rmax > 1 ? *(const uint16_t *)(lds + a1 + 64 * k) : (uint32_t)pk::kZero;
+            }
+        }
+        for (int r = 0; r < Rmax; r += 2) {
+            uint2 f0[N], f1[N];
+            uint32_t g0[N], g1[N];
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                row(c0[k], f0[k], g0[k]);
+                row(c1[k], f1[k], g1[k]);
+            }
+            const int a0 = addr0(min(r + 2, Rmax - 1)), a1 = addr0(min(r + 3, Rmax - 1));
+            const bool n0 = r + 2 < Rmax, n1 = r + 3 < Rmax;
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                c0[k] = n0 ? *(const uint16_t *)(lds + a0 + 64 * k) : (uint32_t)pk::kZero;
+                c1[k] = n1 ? *(const uint16_t *)(lds + a1 + 64 * k) : (uint32_t)pk::kZero;
+            }
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                const uint32_t lo = (uint32_t)llr[k] + f0[k].x + f1[k].x;
+                const uint32_t hi = (uint32_t)(llr[k] >> 32) + f0[k].y + f1[k].y;
+                llr[k] = ((uint64_t)hi << 32) | lo;
+                cnt[k] += g0[k] + g1[k];
+            }
+        }
+    } else {
+        // one read per step; columns outside a read load the pad code (class
+        // 'N', :509-510, :543-544), reads the half's record lacks the zero row
+        auto codes = [&](int r, uint32_t (&cd)[N]) {
+            const int c0 = addr0(r) - 2 * (32 * T0 + l);
+            const int xa = readlane(x0, r), xb = readlane(x0, 32 + r);
+            const int x = h ? xb : xa;
+            const int rc = x & 255, rl = (x >> 8) & 255;
+            const int sent = r < R ? pk::kSent : pk::kZSent;
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                const int t = 32 * (T0 + k) + l;
+                const int ad = r < R && (uint32_t)(t - rc) < (uint32_t)rl ? c0 + 2 * t : sent;
+                cd[k] = *(const uint16_t *)(lds + ad);
+            }
+        };
+        uint32_t c0[N];
+        codes(0, c0);
+        for (int r = 0; r < Rmax; ++r) {
+            uint2 f0[N];
+            uint32_t g0[N];
+#pragma unroll
+            for (int k = 0; k < N; ++k) row(c0[k], f0[k], g0[k]);
+            uint32_t n0[N];
+            codes(min(r + 1, Rmax - 1), n0);
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                llr[k] += ((uint64_t)f0[k].y << 32) | f0[k].x;
+                cnt[k] += g0[k];
+                c0[k] = n0[k];
+            }
+        }
+    }
+    // the decision per column (as k_consensus_fast): call, d, e
+    const bool force = R > a.r_safe;
+    const uint32_t *m720 = (const uint32_t *)(lds + pk::kM720);
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const int t = 32 * (T0 + k) + l;
+        const bool live = t < T;
+        const uint32_t lo = (uint32_t)llr[k], hi = (uint32_t)(llr[k] >> 32);
+        const u16x2 P1 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi, lo, 0x05040100u));
+        const u16x2 P2 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi, lo, 0x07060302u));
+        const u16x2 Mx = __builtin_elementwise_max(P1, P2), Mn = __builtin_elementwise_min(P1, P2);
+        const uint32_t Lb = max((uint32_t)Mx.x, (uint32_t)Mx.y);
+        const uint32_t L2 = max(min((uint32_t)Mx.x, (uint32_t)Mx.y), max((uint32_t)Mn.x, (uint32_t)Mn.y));
+        uint32_t kb = (uint32_t)P1.y == Lb ? 2u : 3u;                        // the first largest ("ATCG")
+        kb = (uint32_t)P2.x == Lb ? 1u : kb;
+        kb = (uint32_t)P1.x == Lb ? 0u : kb;
+        const uint32_t cn = cnt[k];
+        const int d = R - (int)(cn & 63u);                                  // rows that are not 'N'
+        const int nb = (int)__builtin_amdgcn_ubfe(cn, 6u * kb + 6u, 6u);
+        const int e = R - nb;                                               // rows that differ from the call
+        const bool undecided = (int)(Lb - L2) - (d - nb) < a.t16 || force;
+        pc.und |= (uint32_t)(live && undecided) << (T0 + k);
+        *(uint16_t *)(lds + ov_h + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (kb << 12));
+        pc.fx += live ? __umul24((uint32_t)e, m720[max(d, 0)]) : 0u;
+        pc.dmax = max(pc.dmax, live ? d : -1);
+        pc.dmin = min(pc.dmin, live ? d : 0x7fffffff);
+    }
+}
+
+__global__ __launch_bounds__(pk::kBlockThreads, 3) void k_consensus_pair(FastArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[pk::kLds];
+    for (int i = threadIdx.x; i < 5 * (fk::kRowMax + 1); i += pk::kBlockThreads) {
+        const int k = i / (fk::kRowMax + 1), q = i % (fk::kRowMax + 1);
+        const bool nrow = k == 0 || q < a.minbq;          // 'N', or masked below min_base_quality (:280)
+        const uint64_t inc = nrow ? 0ull : (uint64_t)a.llr16[q] << (16 * (k - 1));
+        // the count increment in the row's last word (x, y, w: one ds_read_b128, not a b96)
+        *(uint4 *)(lds + 0x800 * k + 16 * (q + k)) = make_uint4((uint32_t)inc, (uint32_t)(inc >> 32), 0u, nrow ? 1u : 1u << (6 * k));
+    }
+    if (threadIdx.x < 4) ((uint32_t *)(lds + pk::kZero))[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) {
+        *(uint16_t *)(lds + pk::kSent) = (uint16_t)fk::kPadCode;
+        *(uint16_t *)(lds + pk::kZSent) = (uint16_t)pk::kZero;
+    }
+    if (threadIdx.x < 64) {
+        const int t = threadIdx.x;
+        ((uint32_t *)(lds + pk::kM720))[t] = t == 0 || t > 16 ? 0u : 720720u / (uint32_t)t;
+    }
+    __syncthreads();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, l = lane & 31;
+    const int W = pk::kW0 + wave * pk::kPW;
+    const int stage_h = W + h * pk::kStageB;              // this half's stage
+    const int rm_h = W + pk::kRmO + h * 128;
+    const int cr_h = W + pk::kCrO + h * 64;
+    const int ov_h = W + pk::kOvO + h * (2 * kPairMaxT);
+    const int sc_h = W + pk::kScO + h * 48;
+
+    const int64_t np = *a.pair_count;                    // records in the pair list
+    const int64_t npairs = (np + 1) >> 1;
+    const int64_t nw = (int64_t)gridDim.x * pk::kWaves;
+    const int64_t gw = (int64_t)blockIdx.x * pk::kWaves + wave;
+    int64_t p = npairs * gw / nw;
+    const int64_t pend = npairs * (gw + 1) / nw;
+    if (p >= pend) return;
+    const RecMeta *ML = a.meta;
+    // record k of the list (k < np) and an empty stand-in past its end
+    auto meta_of = [&](int64_t k, RecMeta &m, int &R) {
+        if (k < np) {
+            m = ML[a.pair_top - k];
+            R = (int)(m.w & 127u);
+        } else {
+            m = ML[a.pair_top - (np - 1)];                 // any valid descriptor; R = 0 marks the half empty
+            R = 0;
+        }
+    };
+    const int64_t lim = ((a.nbytes + 3) & ~(int64_t)3);
+    const int nrec = (int)min(lim, (int64_t)0x7FFFFFF0);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void *)a.gb, (short)0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void *)a.gq, (short)0, nrec, 0x00020000);
+
+    RecMeta M0, M1;
+    int R0, R1;
+    meta_of(2 * p, M0, R0);
+    meta_of(2 * p + 1, M1, R1);
+    PairStage st;
+    {
+        const RecMeta &m = h ? M1 : M0;
+        pair_load(a, m, h ? R1 : R0, l, st, rb, rq, max((int)(M0.w >> 15), (int)(M1.w >> 15)));
+    }
+    for (;;) {
+        // ---- this pair's descriptors (wave-uniform) and the half's view
+        const RecMeta A0 = M0, A1 = M1;
+        const int AR0 = R0, AR1 = R1;
+        const int R = h ? AR1 : AR0;                        // this lane's record
+        const int ndw = (int)((h ? A1.w : A0.w) >> 15);
+        const uint32_t base_al = h ? A1.base_al : A0.base_al;
+        const int d0 = h ? A1.d0 : A0.d0;
+        // ---- element codes of the staged bytes into the half's stage
+        uint32_t bad = 0;
+#pragma unroll
+        for (int u = 0; u < pk::kDw; ++u) {
+            if (u * 32 < max((int)(A0.w >> 15), (int)(A1.w >> 15))) {
+                if (32 * u + l < ndw) {
+                    const uint2 c = make_codes4<false, false>(st.vb[u], st.vq[u], a.kq, a.kqlo, bad);
+                    *(uint2 *)(lds + stage_h + 8 * (32 * u + l)) = c;
+                }
+            }
+        }
+        *(uint2 *)(lds + rm_h + 8 * l) = l < 16 ? st.rm : make_uint2(0u, 0u);
+        // the next pair's descriptors and bytes, in flight during this pair
+        const bool more = p + 1 < pend;
+        if (more) {
+            meta_of(2 * (p + 1), M0, R0);
+            meta_of(2 * (p + 1) + 1, M1, R1);
+        }
+        {
+            __builtin_amdgcn_sched_barrier(0);
+            const RecMeta &m = h ? M1 : M0;
+            pair_load(a, m, h ? R1 : R0, l, st, rb, rq, max((int)(M0.w >> 15), (int)(M1.w >> 15)));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        lds_fence();
+        const uint2 rw = *(const uint2 *)(lds + rm_h + 8 * l);
+        // the read's word relative to this record: col | len << 8, stage offset
+        const int col = (int)(((int)rw.x >> 16) + (d0 & 0xFFFF));
+        const int y = (int)(rw.y - base_al);
+        const bool rd = l < R;                              // lane = read of the half's record
+        int T = (int)(((h ? A1.w : A0.w) >> 7) & 255u);
+        int state = R > 0 ? 0 : 2;                          // 0 consensus here, 1 general, 2 finished, 3 exact queue
+        // ---- trim_3prime_N (:292-325): trailing 'N' rows (sequenced, or masked, :280)
+        int tl = rd ? (int)(rw.x & 255u) : 0;
+        {
+            bool go = tl > 0;
+            while (__ballot(go)) {
+                if (go) {
+                    const uint32_t code = *(const uint16_t *)(lds + stage_h + 2 * (y + tl - 1));
+                    if (*(const uint32_t *)(lds + code + 12) & 63u) --tl; else go = false;
+                    go = go && tl > 0;
+                }
+            }
+        }
+        const int64_t g0 = h ? A1.g0 : A0.g0;
+        if (rd && (a.want_info || tl == 0)) {
+            dcr_read_info inf;
+            inf.seq_start = (int64_t)base_al + y;
+            inf.len = tl;
+            inf.n_cig = tl > 0 ? 1 : 0;
+            inf.status = tl > 0 ? DCR_ST_OK : DCR_ST_INDEX_ERROR;   // compress_cigarlist([]) :740 via :322
+            inf.has_ins = 0;
+            a.info[g0 + l] = inf;
+        }
+        {
+            // T shrinks only when every read reaching the untrimmed end lost its tail
+            const uint32_t reach = half_bits(__ballot(rd && col + tl == T), h);
+            const int2 tm = half_max(rd ? col + tl : 0);
+            if (reach == 0) T = h ? tm.y : tm.x;
+            if (half_bits(__ballot(rd && tl == 0), h) != 0 && state == 0) {
+                if (l == 0) write_status_at(a.O, h ? A1.rec : A0.rec, DCR_ST_PREP | DCR_ST_INDEX_ERROR);
+                state = 2;
+            }
+            if (state == 0 && half_bits(__ballot(bad != 0), h) != 0) state = 1;
+        }
+        // the general kernel takes a record with invalid input (it reads the
+        // preprocessed reads: read info, one normalised M run)
+        if (state == 1) {
+            if (!a.want_info && rd) {
+                dcr_read_info inf;
+                inf.seq_start = (int64_t)base_al + y;
+                inf.len = tl;
+                inf.n_cig = tl > 0 ? 1 : 0;
+                inf.status = tl > 0 ? DCR_ST_OK : DCR_ST_INDEX_ERROR;
+                inf.has_ins = 0;
+                a.info[g0 + l] = inf;
+            }
+            if (rd && tl > 0) a.norm_cig[a.cig_off[g0 + l]] = (uint32_t)tl << 4;
+            if (l == 0) {
+                const int idx = atomicAdd(a.ovf_count, 1);
+                a.ovf[idx] = h ? A1.rec : A0.rec;
+            }
+        }
+        // read words for the column pass: LDS address of column 0, col | len << 8
+        if (rd) {
+            *(int *)(lds + cr_h + 4 * l) = stage_h + 2 * (y - col);
+            *(uint32_t *)(lds + rm_h + 8 * l) = (uint32_t)col | ((uint32_t)tl << 8);
+        }
+        lds_fence();
+        const uint64_t live_any = __ballot(state == 0);
+        if (live_any) {
+            // ---- evidence sums and the decision, lane = column t = 32 tt + l of
+            // the half's record, in two groups of half tiles (fewer rows in flight)
+            const int Rmax = max(AR0, AR1);
+            // every read of both records covers every column, and both have R reads
+            const bool full = AR0 == AR1 && __ballot(rd && (col != 0 || tl != T)) == 0;
+            const int crv = stage_h + 2 * (y - col);       // lane r of each half: read r's column 0
+            const int x0 = (int)((uint32_t)col | ((uint32_t)tl << 8));   // lane r: col | len << 8
+            PairCols pc;
+            pc.und = 0;
+            pc.fx = 0;
+            pc.dmax = -1;
+            pc.dmin = 0x7fffffff;
+            pair_tiles<0, 3>(a, lds, full, Rmax, R, T, h, l, crv, x0, ov_h, pc);
+            pair_tiles<3, pk::kNT>(a, lds, full, Rmax, R, T, h, l, crv, x0, ov_h, pc);
+            const uint32_t und = pc.und, fx = pc.fx;
+            const int dmax = pc.dmax, dmin = pc.dmin;
+            // ---- E = round(mean(e/d), 3) (:1015-1018), exactly: 25 fx / (18018 T)
+            const int2 S2 = half_sum((int)fx);
+            const int2 Dx = half_max(dmax), Dn = half_min(dmin);
+            const int2 Tp = make_int2(readlane(T, 0), readlane(T, 32));
+            double E2[2];
+            bool slow2[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t S = (uint32_t)(k ? S2.y : S2.x);
+                const int Tk = k ? Tp.y : Tp.x;
+                const int64_t num = 25 * (int64_t)S;
+                const int den = 18018 * max(Tk, 1);
+                const double dn = (double)den;
+                double rc = __builtin_amdgcn_rcp(dn);
+                rc = __builtin_fma(__builtin_fma(-dn, rc, 1.0), rc, rc);
+                const int kk = __builtin_amdgcn_readfirstlane((int)__builtin_rint((double)num * rc));
+                const int64_t rr = num - (int64_t)kk * den;
+                slow2[k] = 2 * (rr < 0 ? -rr : rr) >= den || kk > 1000 || kk < 0;   // a tie (or a bad estimate)
+                E2[k] = div1000(kk);
+            }
+            const bool slow = h ? slow2[1] : slow2[0];
+            // ---- an undecided column or a tie: the record goes to the exact pass
+            if (state == 0 && (half_bits(__ballot(und != 0), h) != 0 || slow)) {
+                if (l == 0) {
+                    const int idx = atomicAdd(a.xcount, 1);
+                    a.xlist[idx] = (int)(a.pair_top - (2 * p + h));
+                }
+                state = 3;
+            }
+            lds_fence();
+            // ---- d / e / seq / qual, eight columns per lane (one 16-, 16-, 8- and 8-byte store)
+            const int T16 = ((int)(((h ? A1.w : A0.w) >> 7) & 255u) + 15) & ~15;
+            const int64_t off = h ? A1.off : A0.off;
+            const int cb = 8 * l;
+            if (state == 0 && cb < T16) {
+                const uint4 w = *(const uint4 *)(lds + ov_h + 16 * l);
+                *(uint4 *)(a.O.d + off + cb) =
+                    make_uint4(w.x & 0x003F003Fu, w.y & 0x003F003Fu, w.z & 0x003F003Fu, w.w & 0x003F003Fu);
+                *(uint4 *)(a.O.e + off + cb) = make_uint4((w.x >> 6) & 0x003F003Fu, (w.y >> 6) & 0x003F003Fu,
+                                                          (w.z >> 6) & 0x003F003Fu, (w.w >> 6) & 0x003F003Fu);
+                auto letters4 = [](uint32_t u, uint32_t v) {
+                    const uint32_t sel = ((u >> 12) & 3u) | ((u >> 20) & 0x300u) | ((v << 4) & 0x30000u) |
+                                         ((v >> 4) & 0x3000000u);
+                    return __builtin_amdgcn_perm(0u, 0x47435441u, sel);        // "ATCG"[call]
+                };
+                const int nl0 = min(max(T - cb, 0), 4), nl1 = min(max(T - cb - 4, 0), 4);
+                const uint32_t k0 = nl0 == 4 ? 0xFFFFFFFFu : (1u << (8 * nl0)) - 1u;
+                const uint32_t k1 = nl1 == 4 ? 0xFFFFFFFFu : (1u << (8 * nl1)) - 1u;
+                const uint32_t q4 = (uint32_t)a.maxq * 0x01010101u;
+                *(uint2 *)(a.O.seq + off + cb) = make_uint2((letters4(w.x, w.y) & k0) | (0x4E4E4E4Eu & ~k0),
+                                                            (letters4(w.z, w.w) & k1) | (0x4E4E4E4Eu & ~k1));
+                *(uint2 *)(a.O.qual + off + cb) = make_uint2(q4 & k0, q4 & k1);
+            }
+            // ---- the record's scalar row (k_scatter_scalars): pos (:790), MAPQ,
+            // len, n_cig, n_de, D, M, E, one M run of the kept columns, marker
+            if (state == 0) {
+                const double E = h ? E2[1] : E2[0];
+                const int minpos = h ? A1.minpos : A0.minpos;
+                if (l == 0) {
+                    *(int4 *)(lds + sc_h) = make_int4(minpos, (int)((uint32_t)d0 >> 16), T, 1);
+                    *(int4 *)(lds + sc_h + 16) = make_int4(T, h ? Dx.y : Dx.x, h ? Dn.y : Dn.x,
+                                                           (int)(uint32_t)__double_as_longlong(E));
+                    *(int2 *)(lds + sc_h + 32) =
+                        make_int2((int)(uint32_t)((uint64_t)__double_as_longlong(E) >> 32), (int)((uint32_t)T << 4));
+                }
+            }
+            lds_fence();
+            if (state == 0 && l < 11) {
+                const int v = *(const int *)(lds + sc_h + 4 * min(l, 9));
+                const int64_t rec = h ? A1.rec : A0.rec;
+                a.rs[rec * 12 + l] = l < 10 ? (uint32_t)v : 1u;
+            }
+        }
+        if (!more) break;
+        ++p;
+    }
 }
 
 // persistent: drains the general list written by k_recmeta.  A wave takes
