@@ -191,16 +191,19 @@ def e2e_passes(path, params_args, device, steps, warmup, workdir):
     # (cli.default_backend): the warmup passes pay their allocation, timed
     # passes reuse them, as a long-running converter would
     t0 = time.perf_counter()
+    passes = []
     for _ in range(steps):
         stats = {"trace": []}
         t_pass = time.perf_counter()
         with contextlib.redirect_stdout(io.StringIO()):
             cli.main(argv, stats=stats)
+        passes.append(round(time.perf_counter() - t_pass, 4))
     dt = time.perf_counter() - t0
     trace = stats.pop("trace")
     log("last pass timeline (ms from CLI start): " +
         " ".join(f"{k}[{(a - t_pass) * 1e3:.0f},{(b - t_pass) * 1e3:.0f}]" for k, a, b in trace))
     stats["first_pass_s"] = cold        # the cold first pass (allocations included)
+    stats["passes_s"] = passes
     return dt, stats
 
 
@@ -303,7 +306,7 @@ def main():
         else:
             value, ms_step = e2e_bases / slowest, slowest * 1e3 / args.steps
             value_kind = "whole node: CLI from BAM open to output close"
-        stage = {k: round(v, 4) for k, v in stats.items() if k.endswith("_s")}
+        stage = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in stats.items() if k.endswith("_s")}
         res = {
             "metric": METRIC, "value": value, "unit": "consensus bases/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,

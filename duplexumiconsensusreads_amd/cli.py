@@ -160,6 +160,8 @@ def default_backend(params: ConsensusParams, device: int = 0):
     caching host allocator would: the first call pays the allocation."""
     from . import _lib
     from .stream import DeviceStream
+    if os.environ.get("DCR_BACKEND_CACHE") == "0":        # A/B runs: a fresh context per call
+        return DeviceStream(_lib.Context(params, device=device), owns_ctx=True)
     be = _BACKENDS.get(device)
     if be is None or be.closed:
         ctx = _lib.Context(params, device=device)

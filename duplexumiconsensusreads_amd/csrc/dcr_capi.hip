@@ -71,6 +71,7 @@ struct dcr_ctx {
     // that it does not queue behind the next batch's downloads on s_d2h
     // (which wait for that batch's kernels)
     hipStream_t s_fetch = nullptr;
+    hipEvent_t ev_fetch = nullptr;      // blocking-sync event after the compressed-block copy
     struct Slot {
         DevBuf buf;
         DevBuf wbuf;              // device record writer: metadata, record stream, BGZF blocks
@@ -288,6 +289,7 @@ void dcr_destroy(dcr_ctx *c) {
     if (c->s_h2d) (void)hipStreamDestroy(c->s_h2d);
     if (c->s_d2h) (void)hipStreamDestroy(c->s_d2h);
     if (c->s_fetch) (void)hipStreamDestroy(c->s_fetch);
+    if (c->ev_fetch) (void)hipEventDestroy(c->ev_fetch);
     if (c->d_params) (void)hipFree(c->d_params);
     if (c->d_llr16) (void)hipFree(c->d_llr16);
     if (c->d_wtab) (void)hipFree(c->d_wtab);
@@ -713,7 +715,9 @@ int dcr_submit(dcr_ctx *c, int slot, const dcr_batch *h, dcr_out *hss, dcr_out *
     if (!S.ev_h2d) {
         HIP_TRY(hipEventCreateWithFlags(&S.ev_h2d, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&S.ev_comp, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&S.ev_d2h, hipEventDisableTiming));
+        // the host waits on this one (dcr_wait / dcr_wait_write): blocking, so the
+        // waiting thread sleeps instead of spinning on a core the ingest needs
+        HIP_TRY(hipEventCreateWithFlags(&S.ev_d2h, hipEventDisableTiming | hipEventBlockingSync));
         HIP_TRY(hipHostMalloc((void **)&S.h_err, sizeof(int), hipHostMallocDefault));
         *S.h_err = 0;
     }
@@ -792,7 +796,9 @@ int dcr_submit_write(dcr_ctx *c, int slot, const dcr_batch *h, const dcr_wmeta *
     if (!S.ev_h2d) {
         HIP_TRY(hipEventCreateWithFlags(&S.ev_h2d, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&S.ev_comp, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&S.ev_d2h, hipEventDisableTiming));
+        // the host waits on this one (dcr_wait / dcr_wait_write): blocking, so the
+        // waiting thread sleeps instead of spinning on a core the ingest needs
+        HIP_TRY(hipEventCreateWithFlags(&S.ev_d2h, hipEventDisableTiming | hipEventBlockingSync));
         HIP_TRY(hipHostMalloc((void **)&S.h_err, sizeof(int), hipHostMallocDefault));
         *S.h_err = 0;
     }
@@ -916,8 +922,10 @@ int dcr_wait_write(dcr_ctx *c, int slot, dcr_wres *res) {
     const int64_t n = res->totals[0];
     if (n > res->cap_bgzf) return fail(DCR_ECAPACITY, "BGZF output larger than cap_bgzf (see totals[0])");
     if (n > 0) {
+        if (!c->ev_fetch) HIP_TRY(hipEventCreateWithFlags(&c->ev_fetch, hipEventDisableTiming | hipEventBlockingSync));
         HIP_TRY(hipMemcpyAsync(res->bgzf, S.d_comp, (size_t)n, hipMemcpyDeviceToHost, c->s_fetch));
-        HIP_TRY(hipStreamSynchronize(c->s_fetch));
+        HIP_TRY(hipEventRecord(c->ev_fetch, c->s_fetch));
+        HIP_TRY(hipEventSynchronize(c->ev_fetch));
     }
     return DCR_OK;
 }
