@@ -10,6 +10,7 @@ namespace dcr {
 
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
+constexpr int kRecmetaWaves = 16;   // k_recmeta: waves per block (one list atomic per block)
 constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kFastWaves = 4;               // k_consensus_fast: five 4-wave blocks per CU (5 waves per SIMD)
 constexpr int kFastBlock = kWave * kFastWaves;

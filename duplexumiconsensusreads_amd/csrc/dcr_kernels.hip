@@ -2140,16 +2140,22 @@ struct RecAgg {
     int pos0, msum;                // pos of the record's first read, sum of the reads' MAPQs
 };
 
+// The list appends take one device-scope atomic per list per BLOCK of
+// kRecmetaWaves waves (a prefix over the block's waves in LDS): appends to one
+// counter serialise at about 30 ns each on this part (one extra atomic per
+// wave cost +0.62 ms per 1.25 M records, tools/ablate.py), so a per-wave
+// atomic alone had made this pass 0.26 ms.  A wave past the last record still
+// reaches the block's barriers (no reads, no records).
 template <bool DUPLEX>
-__global__ __launch_bounds__(256) void k_recmeta(Args a) {
-    __shared__ RecAgg s_agg[kWavesPerBlock][kWave];
-    __shared__ int s_mark[kWavesPerBlock][kWave];
+__global__ __launch_bounds__(kRecmetaWaves * kWave) void k_recmeta(Args a) {
+    __shared__ RecAgg s_agg[kRecmetaWaves][kWave];
+    __shared__ int s_mark[kRecmetaWaves][kWave];
+    __shared__ int s_cnt[3][kRecmetaWaves];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     RecAgg *agg = s_agg[wave];
     int *mark = s_mark[wave];
-    const int64_t rb = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * a.rpw;
-    if (rb >= a.n_rec) return;
+    const int64_t rb = min(((int64_t)blockIdx.x * kRecmetaWaves + wave) * a.rpw, a.n_rec);
     const int64_t rk = rb + lane;
     const bool vk = lane < a.rpw && rk < a.n_rec;
     const int64_t rend = min(rb + a.rpw, a.n_rec);
@@ -2271,15 +2277,22 @@ __global__ __launch_bounds__(256) void k_recmeta(Args a) {
     const uint64_t bf = __ballot(kind == 0);
     const uint64_t bg = __ballot(kind == 1);
     const uint64_t bp = __ballot(kind == 3);
-    int basef = 0, baseg = 0, basep = 0;
-    if (lane == 0) {
-        if (bf) basef = atomicAdd(&a.ws.fast_count[DUPLEX ? 1 : 0], __popcll(bf));
-        if (bg) baseg = atomicAdd(&a.ws.ovf_count[DUPLEX ? 1 : 0], __popcll(bg));
-        if (bp) basep = atomicAdd(a.ws.pair_count, __popcll(bp));
+    if (lane < 3) s_cnt[lane][wave] = __popcll(lane == 0 ? bf : (lane == 1 ? bg : bp));
+    __syncthreads();
+    if (threadIdx.x < 3) {                       // list t: the waves' exclusive prefix, one atomic
+        const int t = threadIdx.x;
+        int tot = 0;
+        for (int w = 0; w < kRecmetaWaves; ++w) {
+            const int c = s_cnt[t][w];
+            s_cnt[t][w] = tot;
+            tot += c;
+        }
+        int *ctr = t == 0 ? &a.ws.fast_count[DUPLEX ? 1 : 0] : (t == 1 ? &a.ws.ovf_count[DUPLEX ? 1 : 0] : a.ws.pair_count);
+        const int base = tot ? atomicAdd(ctr, tot) : 0;
+        for (int w = 0; w < kRecmetaWaves; ++w) s_cnt[t][w] += base;
     }
-    basef = __shfl(basef, 0);
-    baseg = __shfl(baseg, 0);
-    basep = __shfl(basep, 0);
+    __syncthreads();
+    const int basef = s_cnt[0][wave], baseg = s_cnt[1][wave], basep = s_cnt[2][wave];
     const uint64_t lt = lanemask_lt(lane);
     if (kind == 0) a.ws.meta[basef + __popcll(bf & lt)] = m;
     if (kind == 3) a.ws.meta[a.n_rec - 1 - (basep + __popcll(bp & lt))] = m;   // the pair list, from the top
@@ -3671,6 +3684,9 @@ __global__ __launch_bounds__(kBlock, DCR_GEN_OCC) void k_consensus_general(Args 
 #endif
     // the first record of each wave by position (no atomic on the way in: most
     // general lists are shorter than the grid), then claims past the grid
+    // (one record per claim: claiming 4 or 8 at a time measured slower on C3,
+    // 3.85 -> 3.97 / 4.13 ms at 100 k families, the tail imbalance outweighing
+    // the serialised claims)
     const int nw = gridDim.x * kWavesPerBlock;
     for (int i = blockIdx.x * kWavesPerBlock + wave;;) {
         if (i >= n) break;

@@ -36,7 +36,8 @@ for rnd in range(6):
     for path, lib, ctx in handles:
         assert lib.dcr_run_batch(ctx, ctypes.byref(db.batch_struct), ctypes.byref(db.ss_struct),
                                  ctypes.byref(db.ds_struct)) == 0
-        assert lib.dcr_sync(ctx) in (0, 3)
+        rc = lib.dcr_sync(ctx)
+        assert rc in (0, 3), (path, rnd, rc)
         ms = (ctypes.c_float * 9)()
         lib.dcr_last_kernel_timing(ctx, ms)
         if rnd:

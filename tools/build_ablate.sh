@@ -6,8 +6,8 @@ cd "$(dirname "$0")/.."
 C=duplexumiconsensusreads_amd/csrc
 for n in 1 2 4 5 6 7 8; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -DDCR_ABL=$n \
-    -o duplexumiconsensusreads_amd/libdcr_abl$n.so $C/dcr_kernels.hip $C/dcr_capi.hip &
+    -o duplexumiconsensusreads_amd/libdcr_abl$n.so $C/dcr_kernels.hip $C/dcr_capi.hip $C/dcr_writer.hip &
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -DDCR_STAMP=1 \
-  -o duplexumiconsensusreads_amd/libdcr_stamp.so $C/dcr_kernels.hip $C/dcr_capi.hip &
+  -o duplexumiconsensusreads_amd/libdcr_stamp.so $C/dcr_kernels.hip $C/dcr_capi.hip $C/dcr_writer.hip &
 wait
