@@ -454,14 +454,16 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
             while (rpw > 1 && (int64_t)rpw * avg > 1024) rpw >>= 1;
         }
         a.rpw = rpw;
-        const int64_t rpb = (int64_t)dcr::kRecmetaWaves * rpw;   // records per k_recmeta block
+        const int rm_waves = rpw == 64 ? dcr::kRecmetaWaves : 4;   // heavy records: small blocks
+        const int64_t rpb = (int64_t)rm_waves * rpw;                // records per k_recmeta block
         const unsigned nb = (unsigned)((a.n_rec + rpb - 1) / rpb);
+        const size_t rm_lds = dcr::recmeta_lds_bytes(rm_waves);
         hipEvent_t *ev = c->ev + (duplex ? 6 : 2);
         // the exact queue is filled by the common kernel; its length is only
         // known on the device, so the exact kernel gets the resident grid
         const unsigned gx = (unsigned)((int64_t)c->fast_blocks[duplex ? 3 : 2] * c->n_cu);
         if (duplex) {
-            hipLaunchKernelGGL(dcr::k_recmeta<true>, dim3(nb), dim3(dcr::kRecmetaWaves * dcr::kWave), 0, c->stream, a);
+            hipLaunchKernelGGL(dcr::k_recmeta<true>, dim3(nb), dim3(rm_waves * dcr::kWave), rm_lds, c->stream, a);
             HIP_TRY(hipEventRecord(ev[0], c->stream));
             hipLaunchKernelGGL((dcr::k_consensus_fast<true, false>), dim3(fast_grid(a.n_rec, 1)), dim3(dcr::kFastBlock),
                                0, c->stream, fa);
@@ -474,7 +476,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
             hipLaunchKernelGGL(dcr::k_consensus_general<true>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
                                c->stream, a);
         } else {
-            hipLaunchKernelGGL(dcr::k_recmeta<false>, dim3(nb), dim3(dcr::kRecmetaWaves * dcr::kWave), 0, c->stream, a);
+            hipLaunchKernelGGL(dcr::k_recmeta<false>, dim3(nb), dim3(rm_waves * dcr::kWave), rm_lds, c->stream, a);
             hipLaunchKernelGGL(dcr::k_prep_big, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
             HIP_TRY(hipEventRecord(ev[0], c->stream));
             // the pair list (two records per wave) and the fast list: the

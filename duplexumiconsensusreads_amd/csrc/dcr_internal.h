@@ -10,7 +10,9 @@ namespace dcr {
 
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
-constexpr int kRecmetaWaves = 16;   // k_recmeta: waves per block (one list atomic per block)
+constexpr int kRecmetaWaves = 16;   // k_recmeta: waves per block (one list atomic per block), at most
+// k_recmeta's dynamic LDS for a block of nw waves: RecAgg[nw][64], int[nw][64], int[3][nw]
+inline size_t recmeta_lds_bytes(int nw) { return (size_t)nw * (48 * 64 + 4 * 64 + 12); }
 constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kFastWaves = 4;               // k_consensus_fast: five 4-wave blocks per CU (5 waves per SIMD)
 constexpr int kFastBlock = kWave * kFastWaves;

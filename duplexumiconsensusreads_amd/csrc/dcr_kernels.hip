@@ -2139,23 +2139,29 @@ struct RecAgg {
     unsigned long long fst;        // first failing read: global index << 4 | its status
     int pos0, msum;                // pos of the record's first read, sum of the reads' MAPQs
 };
+static_assert(sizeof(RecAgg) == 48, "recmeta_lds_bytes assumes a 48-byte RecAgg");
 
 // The list appends take one device-scope atomic per list per BLOCK of
 // kRecmetaWaves waves (a prefix over the block's waves in LDS): appends to one
 // counter serialise at about 30 ns each on this part (one extra atomic per
 // wave cost +0.62 ms per 1.25 M records, tools/ablate.py), so a per-wave
 // atomic alone had made this pass 0.26 ms.  A wave past the last record still
-// reaches the block's barriers (no reads, no records).
+// reaches the block's barriers (no reads, no records).  Blocks of records with
+// many reads (rpw < 64) are 4 waves: a block's barrier waits for its slowest
+// wave, and their lists are short.  LDS is sized by the launch
+// (recmeta_lds_bytes).
 template <bool DUPLEX>
 __global__ __launch_bounds__(kRecmetaWaves * kWave) void k_recmeta(Args a) {
-    __shared__ RecAgg s_agg[kRecmetaWaves][kWave];
-    __shared__ int s_mark[kRecmetaWaves][kWave];
-    __shared__ int s_cnt[3][kRecmetaWaves];
+    extern __shared__ __attribute__((aligned(16))) uint8_t rm_lds[];
+    const int nwb = (int)(blockDim.x >> 6);                      // waves in this block
+    RecAgg (*s_agg)[kWave] = (RecAgg (*)[kWave])rm_lds;
+    int (*s_mark)[kWave] = (int (*)[kWave])(rm_lds + sizeof(RecAgg) * kWave * nwb);
+    int *s_cnt = (int *)(rm_lds + (sizeof(RecAgg) + sizeof(int)) * kWave * nwb);   // [3][nwb]
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     RecAgg *agg = s_agg[wave];
     int *mark = s_mark[wave];
-    const int64_t rb = min(((int64_t)blockIdx.x * kRecmetaWaves + wave) * a.rpw, a.n_rec);
+    const int64_t rb = min(((int64_t)blockIdx.x * nwb + wave) * a.rpw, a.n_rec);
     const int64_t rk = rb + lane;
     const bool vk = lane < a.rpw && rk < a.n_rec;
     const int64_t rend = min(rb + a.rpw, a.n_rec);
@@ -2277,22 +2283,22 @@ __global__ __launch_bounds__(kRecmetaWaves * kWave) void k_recmeta(Args a) {
     const uint64_t bf = __ballot(kind == 0);
     const uint64_t bg = __ballot(kind == 1);
     const uint64_t bp = __ballot(kind == 3);
-    if (lane < 3) s_cnt[lane][wave] = __popcll(lane == 0 ? bf : (lane == 1 ? bg : bp));
+    if (lane < 3) s_cnt[lane * nwb + wave] = __popcll(lane == 0 ? bf : (lane == 1 ? bg : bp));
     __syncthreads();
     if (threadIdx.x < 3) {                       // list t: the waves' exclusive prefix, one atomic
         const int t = threadIdx.x;
         int tot = 0;
-        for (int w = 0; w < kRecmetaWaves; ++w) {
-            const int c = s_cnt[t][w];
-            s_cnt[t][w] = tot;
+        for (int w = 0; w < nwb; ++w) {
+            const int c = s_cnt[t * nwb + w];
+            s_cnt[t * nwb + w] = tot;
             tot += c;
         }
         int *ctr = t == 0 ? &a.ws.fast_count[DUPLEX ? 1 : 0] : (t == 1 ? &a.ws.ovf_count[DUPLEX ? 1 : 0] : a.ws.pair_count);
         const int base = tot ? atomicAdd(ctr, tot) : 0;
-        for (int w = 0; w < kRecmetaWaves; ++w) s_cnt[t][w] += base;
+        for (int w = 0; w < nwb; ++w) s_cnt[t * nwb + w] += base;
     }
     __syncthreads();
-    const int basef = s_cnt[0][wave], baseg = s_cnt[1][wave], basep = s_cnt[2][wave];
+    const int basef = s_cnt[wave], baseg = s_cnt[nwb + wave], basep = s_cnt[2 * nwb + wave];
     const uint64_t lt = lanemask_lt(lane);
     if (kind == 0) a.ws.meta[basef + __popcll(bf & lt)] = m;
     if (kind == 3) a.ws.meta[a.n_rec - 1 - (basep + __popcll(bp & lt))] = m;   // the pair list, from the top
