@@ -11,6 +11,8 @@
 //
 // Reference: /root/reference/DuplexUMIConsensusReads.py (":line" below).
 #include <zlib.h>
+#include <tmmintrin.h>
+#include <sys/stat.h>
 
 #include <cctype>
 #include <cmath>
@@ -130,6 +132,26 @@ struct SeqTable {
     }
 };
 const SeqTable kSeq;
+
+// 4-bit BAM sequence -> ASCII letters: 16 packed bytes (32 bases) per step
+// with two byte shuffles of the 16-letter table (SSSE3, in x86-64-v2), the
+// tail by the pair table.  Part of the pack copy, which runs on the pool for
+// every read of a batch.
+inline void decode_seq(const uint8_t *s, int32_t l_seq, uint8_t *d) {
+    const int32_t half = l_seq >> 1;
+    int32_t i = 0;
+    const __m128i tab = _mm_loadu_si128((const __m128i *)"=ACMGRSVTWYHKDBN");
+    const __m128i m = _mm_set1_epi8(15);
+    for (; i + 16 <= half; i += 16) {
+        const __m128i v = _mm_loadu_si128((const __m128i *)(s + i));
+        const __m128i hi = _mm_shuffle_epi8(tab, _mm_and_si128(_mm_srli_epi16(v, 4), m));
+        const __m128i lo = _mm_shuffle_epi8(tab, _mm_and_si128(v, m));
+        _mm_storeu_si128((__m128i *)(d + 2 * i), _mm_unpacklo_epi8(hi, lo));
+        _mm_storeu_si128((__m128i *)(d + 2 * i + 16), _mm_unpackhi_epi8(hi, lo));
+    }
+    for (; i < half; ++i) std::memcpy(d + 2 * i, &kSeq.pair[s[i]], 2);
+    if (l_seq & 1) d[l_seq - 1] = (uint8_t)(kSeq.pair[s[half]] & 0xff);
+}
 
 // One parsed record (offsets relative to the window start)
 struct Rec {
@@ -391,12 +413,33 @@ class Inflater {
              uint32_t start_uoff = 0, int64_t end_coff = -1, uint32_t end_uoff = 0)
         : f_(f), pool_(n_threads), spool_(n_threads), rp_(rp), end_coff_(end_coff), end_uoff_(end_uoff) {
         if (ranged) {
-            std::fseek(f_, (long)start_coff, SEEK_SET);
-            cpos_ = start_coff;
             st_ = kRec;
             skip_ = start_uoff;
         }
-        cbuf_.resize((size_t)48 << 20);
+        // A regular file is mapped whole: the blocks inflate straight from the
+        // page cache, with no serial fread copy on this thread in front of the
+        // pool (48 MiB before the first chunk could start, ~0.1 s per 0.5 GB
+        // file), and the workers fault their own pages in parallel.  Anything
+        // else (a pipe) streams through cbuf_.
+        struct stat sb;
+        const int fd = fileno(f_);
+        if (fd >= 0 && fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode) && sb.st_size > 0) {
+            void *p = mmap(nullptr, (size_t)sb.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+            if (p != MAP_FAILED) {
+                map_ = (const uint8_t *)p;
+                map_len_ = (size_t)sb.st_size;
+                cbeg_ = ranged ? (size_t)std::min<uint64_t>(start_coff, map_len_) : 0;
+                cend_ = map_len_;
+                file_eof_ = true;
+            }
+        }
+        if (!map_) {
+            if (ranged) {
+                std::fseek(f_, (long)start_coff, SEEK_SET);
+                cpos_ = start_coff;
+            }
+            cbuf_.resize((size_t)48 << 20);
+        }
         for (auto &c : chunks_) {
             c.buf.resize(kHead + kWant + 0x10000);
             empty_.push_back(&c);
@@ -412,6 +455,7 @@ class Inflater {
         cv_.notify_all();
         th_.join();
         sth_.join();
+        if (map_) munmap((void *)map_, map_len_);
     }
     Chunk *next() {
         std::unique_lock<std::mutex> lk(mu_);
@@ -596,7 +640,7 @@ class Inflater {
                     if (cpos_ + cbeg_ != (uint64_t)end_coff_ || end_uoff_ == 0) break;
                     cut = total + end_uoff_;
                 }
-                const uint8_t *h = cbuf_.data() + cbeg_;
+                const uint8_t *h = cdata() + cbeg_;
                 if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) { c.err = "not a BGZF file"; return; }
                 const size_t xlen = rd16(h + 10);
                 if (cend_ - cbeg_ < 12 + xlen) break;
@@ -630,7 +674,7 @@ class Inflater {
             top_up();
         }
         uint8_t *dst = c.buf.data();
-        const uint8_t *src = cbuf_.data();
+        const uint8_t *src = cdata();
         const bool ok = pool_.run(blks.size(), [&](size_t i) {
             const Blk &b = blks[i];
             if (b.isize == 0) return b.clen <= 2;      // empty block (the EOF marker)
@@ -658,7 +702,10 @@ class Inflater {
     RecParser rp_;
     int64_t end_coff_;
     uint32_t end_uoff_;
-    uint64_t cpos_ = 0;             // file offset of cbuf_[0]
+    uint64_t cpos_ = 0;             // file offset of cdata()[0]
+    const uint8_t *map_ = nullptr;  // the whole file, when it maps (then cpos_ = 0 and no top_up)
+    size_t map_len_ = 0;
+    const uint8_t *cdata() const { return map_ ? map_ : cbuf_.data(); }
     bool range_done_ = false;
     size_t want_ = (size_t)4 << 20;   // the first chunk is small: the walk starts sooner
     HugeBuf cbuf_;
@@ -811,10 +858,7 @@ struct dcr_ingest {
                 const uint8_t *cig = r + 32 + l_rn;
                 std::memcpy(b->cigar + jb.dst_cig, cig, 4u * n_cig);
                 const uint8_t *s = cig + 4u * n_cig;
-                uint8_t *d = b->bases + jb.dst_base;
-                const int32_t half = l_seq >> 1;
-                for (int32_t i = 0; i < half; ++i) std::memcpy(d + 2 * i, &kSeq.pair[s[i]], 2);
-                if (l_seq & 1) d[l_seq - 1] = (uint8_t)(kSeq.pair[s[half]] & 0xff);
+                decode_seq(s, l_seq, b->bases + jb.dst_base);
                 std::memcpy(b->quals + jb.dst_base, s + ((l_seq + 1) >> 1), (size_t)l_seq);
             }
             return true;
