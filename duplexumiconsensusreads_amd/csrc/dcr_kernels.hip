@@ -2722,7 +2722,7 @@ __device__ __forceinline__ double div1000(int k) {
 template <bool DUPLEX, int NT, bool EXACT>
 __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &m, const Staged &sg, uint8_t *lds,
                                               const int stage_addr, const int ov_addr, const int rm_addr, const int lane,
-                                              Stamps &sp, const double2 *xt) {
+                                              Stamps &sp, const double2 *xt, const uint32_t *r1) {
     const dcr_out &O = a.O;
     const int64_t rec = m.rec;
     const int64_t off = m.off;
@@ -2807,9 +2807,30 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
             const bool mine = (und >> tt) & 1u;
             if (__ballot(mine) == 0) continue;
             const int t = 64 * tt + lane;
+            Posterior po;
+            uint32_t cnt = 0;          // 8-bit row counts of A T C G
+            if (!DUPLEX && R == 1) {
+                // one read: the column's posterior is a function of its row
+                // (class after the mask, raw quality), tabulated per block in
+                // the kernel's prologue by this loop's products and posterior()
+                const int cr = readlane(crv, 0);
+                const int x = readlane((int)rm.x, 0);
+                const int col = x & 255, len = (x >> 8) & 255;
+                const uint32_t ad = (uint32_t)(t - col) < (uint32_t)len ? (uint32_t)(cr + 2 * t) : (uint32_t)fk::kSent;
+                const uint32_t code = *(const uint16_t *)(lds + ad);
+                const uint32_t kc = code >> 11;
+                const uint32_t q = ((code >> 4) & 127u) - kc;
+                const uint32_t k = (*(const uint32_t *)(lds + code + 8) & 63u) ? 0u : kc;
+                const uint32_t te = r1[k * 128u + q];
+                po.ch = (int)(te & 255u);
+                po.q = (int)((te >> 8) & 1023u) - 1;
+                po.best = (int)((te >> 18) & 7u);
+                po.masked = (te >> 21) & 1u;
+                po.overflow = (te >> 22) & 1u;
+                cnt = k ? 1u << (8 * (k - 1)) : 0u;
+            } else {
             double L4[4] = {1.0, 1.0, 1.0, 1.0};
             double U = 1.0;
-            uint32_t cnt = 0;          // 8-bit row counts of A T C G
             for (int r = 0; r < R; ++r) {
                 const int cr = readlane(crv, r);
                 const int x = readlane((int)rm.x, r);
@@ -2827,7 +2848,8 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
                 cnt += k ? 1u << (8 * (k - 1)) : 0u;
             }
             const double L[6] = {L4[0], L4[1], L4[2], L4[3], U, U};
-            const Posterior po = posterior(L, false, P, qthr, true);
+            po = posterior(L, false, P, qthr, true);
+            }
             if (mine) {
                 fail |= po.overflow || (!po.masked && po.best > 3);
                 const uint32_t w = *(const uint16_t *)(ov + 2 * t);
@@ -3035,6 +3057,24 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
     __shared__ double2 s_xt[EXACT ? 128 : 1];
     if (EXACT)
         for (int i = threadIdx.x; i < 128; i += fk::kBlockThreads) s_xt[i] = make_double2(a.P->match[i], a.P->mismatch[i]);
+    // EXACT single-strand: the posterior of a one-read column per (class after
+    // the mask, quality), as finish_record's per-read loop and posterior()
+    // compute it for R = 1 (the same products: 1.0 * factor)
+    __shared__ uint32_t s_r1[EXACT && !DUPLEX ? 5 * 128 : 1];
+    if (EXACT && !DUPLEX)
+        for (int i = threadIdx.x; i < 5 * 128; i += fk::kBlockThreads) {
+            const uint32_t k = (uint32_t)i >> 7, q = (uint32_t)i & 127u;
+            const double fm = a.P->match[q], fx = a.P->mismatch[q];
+            double L4[4] = {1.0, 1.0, 1.0, 1.0};
+            double U = 1.0;
+            U = U * fx;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) L4[j] = L4[j] * (k == (uint32_t)(j + 1) ? fm : fx);
+            const double L[6] = {L4[0], L4[1], L4[2], L4[3], U, U};
+            const Posterior po = posterior(L, false, a.P, a.P->qthresh, true);
+            s_r1[i] = ((uint32_t)po.ch & 255u) | ((uint32_t)(po.q + 1) & 1023u) << 8 | ((uint32_t)po.best & 7u) << 18 |
+                      (uint32_t)po.masked << 21 | (uint32_t)po.overflow << 22;
+        }
     for (int i = threadIdx.x; i < 5 * (fk::kRowMax + 1); i += fk::kBlockThreads) {
         const int k = i / (fk::kRowMax + 1), q = i % (fk::kRowMax + 1);
         const bool nrow = k == 0 || q < a.minbq;          // 'N', or masked below min_base_quality (:280)
@@ -3144,10 +3184,10 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
             send_to_general<DUPLEX>(a, m0, sg.rm, lds, lane);
         } else if (sg.state == 0) {
             bool done;
-            if (sg.T <= 64) done = finish_record<DUPLEX, 1, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt);
-            else if (sg.T <= 128) done = finish_record<DUPLEX, 2, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt);
-            else if (sg.T <= 192) done = finish_record<DUPLEX, 3, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt);
-            else done = finish_record<DUPLEX, 4, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt);
+            if (sg.T <= 64) done = finish_record<DUPLEX, 1, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1);
+            else if (sg.T <= 128) done = finish_record<DUPLEX, 2, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1);
+            else if (sg.T <= 192) done = finish_record<DUPLEX, 3, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1);
+            else done = finish_record<DUPLEX, 4, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1);
             if (!EXACT && !done) {
                 if (lane == npend) pend = i;
                 if (++npend == kWave) flush(lane);
