@@ -175,3 +175,19 @@ def test_ingest_rejects_non_bam(tmp_path):
     p.write_bytes(b"not a bam at all" * 10)
     with pytest.raises(native_io.IOError_):
         native_io.Ingest(str(p))
+
+
+def test_bgzf_writer_rewrites_a_longer_file(tmp_path):
+    """The writer opens without truncation and cuts the file at close: a
+    rewrite over a longer file of the same name gives the bytes of a fresh one."""
+    import gzip
+    small, big = b"BAM\x01" + bytes(range(256)) * 4, os.urandom(3 << 20)
+    fresh, reused = tmp_path / "fresh.bam", tmp_path / "reused.bam"
+    w = native_io.BgzfWriter(str(reused), big, 1, 2)
+    w.close()
+    assert reused.stat().st_size > 3 << 20
+    for path in (fresh, reused):
+        w = native_io.BgzfWriter(str(path), small, 1, 2)
+        w.close()
+    assert reused.read_bytes() == fresh.read_bytes()
+    assert gzip.decompress(reused.read_bytes()) == small
