@@ -3052,6 +3052,14 @@ __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
 template <bool DUPLEX, bool EXACT>
 __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[fk::kLdsBytes];
+    // a block none of whose waves has a record leaves before its tables are
+    // built (the EXACT grid is the resident one, its queue mostly short)
+    const int64_t n = EXACT ? *a.xcount : *a.fast_count;
+    const int64_t nw = (int64_t)gridDim.x * fk::kWaves;
+    {
+        const int64_t b0 = (int64_t)blockIdx.x * fk::kWaves;
+        if (n * b0 / nw == n * (b0 + fk::kWaves) / nw) return;
+    }
     // EXACT: the likelihood factors of quality rows 0..127 (the exact columns'
     // per-read products read them once per row; the common kernel keeps none)
     __shared__ double2 s_xt[EXACT ? 128 : 1];
@@ -3107,8 +3115,6 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
     const int rm_addr = fk::kRm + wave * kWave * 8;
     const int ov_addr = fk::kOv + wave * 512;
     __syncthreads();
-    const int64_t n = EXACT ? *a.xcount : *a.fast_count;
-    const int64_t nw = (int64_t)gridDim.x * fk::kWaves;
     const int64_t gw = (int64_t)blockIdx.x * fk::kWaves + wave;
     int i = (int)(n * gw / nw);
     const int iend = (int)(n * (gw + 1) / nw);
