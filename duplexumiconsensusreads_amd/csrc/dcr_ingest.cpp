@@ -22,6 +22,7 @@
 #include <mutex>
 #include <thread>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -401,6 +402,13 @@ struct Chunk {
     std::vector<Rec> recs;          // boundary in this chunk and ending in it (off from buf start)
 };
 
+// override of a pool's size (A/B runs): the variable's value if set and positive
+inline int env_threads(const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    const int n = v ? std::atoi(v) : 0;
+    return n > 0 ? std::min(n, 64) : dflt;
+}
+
 class Inflater {
   public:
     static constexpr size_t kHead = (size_t)8 << 20;
@@ -411,7 +419,9 @@ class Inflater {
     // stop end_uoff bytes into the data of the block at end_coff
     Inflater(FILE *f, int n_threads, const RecParser &rp, bool ranged = false, uint64_t start_coff = 0,
              uint32_t start_uoff = 0, int64_t end_coff = -1, uint32_t end_uoff = 0)
-        : f_(f), pool_(n_threads), spool_(n_threads), rp_(rp), end_coff_(end_coff), end_uoff_(end_uoff) {
+        : f_(f), pool_(env_threads("DCR_INFLATE_THREADS", n_threads)),
+          spool_(env_threads("DCR_SCAN_THREADS", std::max(1, n_threads / 2))), rp_(rp), end_coff_(end_coff),
+          end_uoff_(end_uoff) {
         if (ranged) {
             st_ = kRec;
             skip_ = start_uoff;
@@ -1374,7 +1384,12 @@ static dcr_ingest *open_impl(const char *path, const dcr_ingest_cfg *cfg, bool r
     std::unique_ptr<dcr_ingest> ing(new dcr_ingest);
     ing->f = f;
     ing->cfg = *cfg;
-    ing->pool.reset(new Pool(pick_threads(cfg->n_threads)));
+    // the scanner's and the pack copy's pools get half the threads: the three
+    // pools run at once, and beyond the process's CPU share (16 on the GPU
+    // box) their threads only preempt the serial stages (inflate thread,
+    // walk) and draw quota throttling (profiles/r02pool: 192-194 -> 217-224 M
+    // consensus bases/s with 8 + 8 instead of 16 + 16)
+    ing->pool.reset(new Pool(env_threads("DCR_PACK_THREADS", std::max(1, pick_threads(cfg->n_threads) / 2))));
     ing->rp.min_map_quality = cfg->min_map_quality;
     ing->rp.min_base_quality = cfg->min_base_quality;
     const int64_t end_coff = end_voff >= 0 ? (end_voff >> 16) : -1;
