@@ -26,6 +26,12 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
 (N > 1 is launched by torch.distributed.run, one process per GPU; every rank
 owns its own shard of families: weak scaling, no data-path collective.  C4
 at N > 1 deals one shared stream of N x 1,000 families to the ranks by LPT.)
+
+--sharded: strong scaling of the drop-in itself: ONE input BAM (rank 0's
+batch) through the sharded CLI (cli --gpus: split points at family starts,
+one process per GPU over its range, parallel part merge), every pass between
+barriers on all ranks.  --in-level sets the input's BGZF level (default 1;
+6 is samtools' default).
 """
 from __future__ import annotations
 
@@ -176,12 +182,22 @@ def e2e_passes(path, params_args, device, steps, warmup, workdir):
     """W untimed + K timed CLI runs over the BAM at ``path``; returns
     (seconds of the K runs, stats of the last run)."""
     from duplexumiconsensusreads_amd import cli
-    out = os.path.join(workdir, "cons.bam")
-    argv = ["-i", path, "-o", out, "--device", str(device), *params_args]
     import contextlib
     import io
+
+    def argv_of(i):
+        # a fresh output name per pass (the previous pass's files deleted
+        # outside the timed region): every pass writes new files, as a
+        # first-time run does, never a rewrite of the last pass's outputs
+        for f in os.listdir(workdir):
+            if f.startswith("cons"):
+                os.remove(os.path.join(workdir, f))
+        out = os.path.join(workdir, f"cons{i}.bam")
+        return ["-i", path, "-o", out, "--device", str(device), *params_args]
+
     cold = None
-    for _ in range(warmup):
+    for i in range(warmup):
+        argv = argv_of(i)
         tw = time.perf_counter()
         with contextlib.redirect_stdout(io.StringIO()):
             cli.main(argv)
@@ -190,19 +206,60 @@ def e2e_passes(path, params_args, device, steps, warmup, workdir):
     # the CLI keeps its device context and pinned host batches per process
     # (cli.default_backend): the warmup passes pay their allocation, timed
     # passes reuse them, as a long-running converter would
-    t0 = time.perf_counter()
+    dt = 0.0
     passes = []
-    for _ in range(steps):
+    for i in range(steps):
+        argv = argv_of(warmup + i)
         stats = {"trace": []}
         t_pass = time.perf_counter()
         with contextlib.redirect_stdout(io.StringIO()):
             cli.main(argv, stats=stats)
-        passes.append(round(time.perf_counter() - t_pass, 4))
-    dt = time.perf_counter() - t0
+        dt_pass = time.perf_counter() - t_pass
+        dt += dt_pass
+        passes.append(round(dt_pass, 4))
     trace = stats.pop("trace")
     log("last pass timeline (ms from CLI start): " +
         " ".join(f"{k}[{(a - t_pass) * 1e3:.0f},{(b - t_pass) * 1e3:.0f}]" for k, a, b in trace))
     stats["first_pass_s"] = cold        # the cold first pass (allocations included)
+    stats["passes_s"] = passes
+    return dt, stats
+
+
+def e2e_passes_sharded(path, params_args, steps, warmup, workdir, tdist, rank):
+    """--sharded: W untimed + K timed runs of the sharded CLI (cli.main with
+    one rank per GPU over ranges of whole families of ONE input,
+    cli._main_sharded) on all ranks at once; each pass is bracketed by
+    barriers, its time is this rank's view of the slowest rank.  Returns
+    (seconds of the K runs, this rank's stats of the last run)."""
+    from duplexumiconsensusreads_amd import cli
+    import contextlib
+    import io
+    os.environ["DCR_SHARD"] = "1"           # cli.main joins this process group (cli._shard_group)
+
+    def one(i, stats):
+        if rank == 0:
+            for f in os.listdir(workdir):
+                if f.startswith("cons"):
+                    os.remove(os.path.join(workdir, f))
+        out = os.path.join(workdir, f"cons{i}.bam")
+        argv = ["-i", path, "-o", out, "--device", "0", *params_args]
+        if tdist is not None:
+            tdist.barrier()
+        t = time.perf_counter()
+        with contextlib.redirect_stdout(io.StringIO()):
+            cli.main(argv, stats=stats)
+        if tdist is not None:
+            tdist.barrier()
+        return time.perf_counter() - t
+
+    for i in range(warmup):
+        one(i, {})
+    dt, passes, stats = 0.0, [], {}
+    for i in range(steps):
+        stats = {}
+        d = one(warmup + i, stats)
+        dt += d
+        passes.append(round(d, 4))
     stats["passes_s"] = passes
     return dt, stats
 
@@ -221,6 +278,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kernel-only", action="store_true", help="skip the whole-node CLI runs")
     ap.add_argument("--kernel-steps", type=int, default=10, help="device-resident passes for the roofline")
+    ap.add_argument("--sharded", action="store_true",
+                    help="strong scaling: ONE input BAM (rank 0's batch) through the sharded CLI, one process "
+                         "per GPU over ranges of whole families (cli._main_sharded), instead of one BAM per rank")
+    ap.add_argument("--in-level", type=int, default=1, help="BGZF compression level of the synthetic input BAM")
     args = ap.parse_args()
 
     import torch
@@ -229,10 +290,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
     dev = f"cuda:{local}"
+    tdist = None
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device(dev))
+        if args.sharded:      # the sharded CLI's control messages (no data-path collective) ride on gloo
+            tdist.init_process_group("gloo")
+        else:
+            tdist.init_process_group("nccl", device_id=torch.device(dev))
+    red_dev = None if args.sharded else dev
     from duplexumiconsensusreads_amd import _lib, shard, synth
     from duplexumiconsensusreads_amd.params import ConsensusParams
 
@@ -253,39 +319,60 @@ def main():
     log(f"[rank {rank}] device-resident step {dev_step * 1e3:.2f} ms")
 
     # -- whole node: the CLI over a BAM of the same families -------------------------
-    workdir = tempfile.mkdtemp(prefix=f"dcr_bench_r{rank}_", dir=os.environ.get("DCR_BENCH_DIR"))
+    workdir = None
+    if args.sharded:         # one shared directory (rank 0's) for the one input and the outputs
+        wd = [tempfile.mkdtemp(prefix="dcr_bench_sharded_", dir=os.environ.get("DCR_BENCH_DIR")) if rank == 0
+              else None]
+        if dist:
+            tdist.broadcast_object_list(wd, src=0)
+        workdir = wd[0]
+    else:
+        workdir = tempfile.mkdtemp(prefix=f"dcr_bench_r{rank}_", dir=os.environ.get("DCR_BENCH_DIR"))
     stats, e2e_s = {}, None
     try:
         if not args.kernel_only:
             bam_path = os.path.join(workdir, "in.bam")
             t0 = time.perf_counter()
-            synth.write_packed_bam(bam_path, packed, seed=args.seed + 1000 * rank, level=1)
-            log(f"[rank {rank}] wrote {os.path.getsize(bam_path) / 1e6:.0f} MB BAM in {time.perf_counter() - t0:.1f} s")
+            if rank == 0 or not args.sharded:
+                synth.write_packed_bam(bam_path, packed, seed=args.seed + 1000 * rank, level=args.in_level)
+                log(f"[rank {rank}] wrote {os.path.getsize(bam_path) / 1e6:.0f} MB BAM (level {args.in_level}) "
+                    f"in {time.perf_counter() - t0:.1f} s")
             if dist:
                 tdist.barrier()
             torch.cuda.synchronize()
-            e2e_s, stats = e2e_passes(bam_path, params_args, local, args.steps, args.warmup, workdir)
+            if args.sharded:
+                e2e_s, stats = e2e_passes_sharded(bam_path, params_args, args.steps, args.warmup, workdir,
+                                                  tdist if dist else None, rank)
+            else:
+                e2e_s, stats = e2e_passes(bam_path, params_args, local, args.steps, args.warmup, workdir)
             torch.cuda.synchronize()
             if dist:
                 tdist.barrier()
-            log(f"[rank {rank}] {args.steps} CLI passes in {e2e_s:.2f} s: {stats}")
+            log(f"[rank {rank}] {args.steps} CLI passes in {e2e_s:.2f} s: "
+                f"{ {k: v for k, v in stats.items() if k != 'ranks'} }")
     finally:
-        shutil.rmtree(workdir, ignore_errors=True)
+        if rank == 0 or not args.sharded:
+            shutil.rmtree(workdir, ignore_errors=True)
 
     e2e_bases = stats.get("consensus_bases", 0) * args.steps
     in_bases = int(packed.seq_len.astype(np.int64).sum()) * args.steps
+    if args.sharded and rank != 0:
+        in_bases = 0            # one input: rank 0's batch
     # per-rank busy time of the last CLI pass (whole pass, ingest thread, waits on the device)
     mine = {"rank": rank, "e2e_s_per_pass": (e2e_s or 0.0) / max(args.steps, 1),
             "device_resident_ms": dev_step * 1e3,
-            **{k: round(v, 4) for k, v in stats.items() if k in ("ingest_s", "wait_s", "idle_s", "write_s")}}
+            **{k: round(v, 4) for k, v in stats.items()
+               if k in ("ingest_s", "wait_s", "idle_s", "write_s", "run_s", "merge_s", "shard_rounds",
+                        "consensus_bases")}}
     per_rank = [mine]
     if dist:
         per_rank = [None] * world
         tdist.all_gather_object(per_rank, mine)
     if dist:
-        slowest = shard.max_over_ranks(e2e_s or 0.0, device=dev)
-        dev_slowest = shard.max_over_ranks(dev_step, device=dev)
-        e2e_bases, in_bases, dev_bases, n_bad = shard.sum_over_ranks([e2e_bases, in_bases, dev_bases, n_bad], device=dev)
+        slowest = shard.max_over_ranks(e2e_s or 0.0, device=red_dev)
+        dev_slowest = shard.max_over_ranks(dev_step, device=red_dev)
+        e2e_bases, in_bases, dev_bases, n_bad = shard.sum_over_ranks([e2e_bases, in_bases, dev_bases, n_bad],
+                                                                     device=red_dev)
     else:
         slowest, dev_slowest = e2e_s or 0.0, dev_step
 
@@ -297,7 +384,7 @@ def main():
             traffic, tsrc = load_traffic("k_consensus_fast<false, false>", packed.n_fam)
         else:
             dom_label = "single-strand stage (k_recmeta<ss> + k_consensus_fast<ss> + k_consensus_exact<ss> + k_consensus_general<ss>)"
-            dom_ms = sum(kavg[k] for k in _lib.KERNELS[1:5])
+            dom_ms = sum(kavg[k] for k in _lib.KERNELS[0:4])
             traffic, tsrc = None, None
         achieved = alg / (dom_ms / 1000.0) / 1e9
         if args.kernel_only:
@@ -310,9 +397,13 @@ def main():
         res = {
             "metric": METRIC, "value": value, "unit": "consensus bases/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": "strong" if args.sharded else "weak", "vs_baseline": None,
+            "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": WORKLOAD[args.config], "value_is": value_kind,
+            "config": {"workload": WORKLOAD[args.config] + (
+                           f"; --sharded: ONE input of {packed.n_reads} reads split over the {world} GPU(s) by "
+                           "the sharded CLI" if args.sharded else ""),
+                       "value_is": value_kind, "input_bgzf_level": args.in_level,
                        "families_per_gpu": packed.n_fam, "reads_per_gpu": packed.n_reads,
                        "input_bases_per_s": (in_bases / slowest) if slowest else None,
                        "consensus_records_per_pass": stats.get("consensus_records"),
@@ -320,8 +411,11 @@ def main():
                        "device_resident": {"consensus_bases_per_s": dev_bases / dev_slowest,
                                            "ms_per_step": dev_slowest * 1e3, "kernel_ms": kavg,
                                            "records_not_ok": n_bad},
-                       "single_strand_stage_GBps": alg / (sum(kavg[k] for k in _lib.KERNELS[1:5]) / 1e3) / 1e9,
-                       "parallelism": f"family-sharded x{world}, one process per GPU, no data-path collective",
+                       "single_strand_stage_GBps": alg / (sum(kavg[k] for k in _lib.KERNELS[0:4]) / 1e3) / 1e9,
+                       "parallelism": (f"one input sharded x{world} by ranges of whole families (cli --gpus), "
+                                       "one process per GPU, parallel part merge, no data-path collective"
+                                       if args.sharded else
+                                       f"family-sharded x{world}, one process per GPU, no data-path collective"),
                        "per_rank": per_rank, "shared_stream": shared},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

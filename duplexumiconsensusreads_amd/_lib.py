@@ -47,7 +47,7 @@ EXPORTS = {
 
 # HIP-event slots of dcr_last_kernel_timing: k_recmeta<ss> includes k_prep_big,
 # k_consensus_general<..> includes the k_decide pass that precedes it
-KERNELS = ("k_prep", "k_recmeta<ss>", "k_consensus_fast<ss>", "k_consensus_exact<ss>", "k_consensus_general<ss>",
+KERNELS = ("k_recmeta<ss>", "k_consensus_fast<ss>", "k_consensus_exact<ss>", "k_consensus_general<ss>",
            "k_recmeta<ds>", "k_consensus_fast<ds>", "k_consensus_exact<ds>", "k_consensus_general<ds>")
 
 _lib = None

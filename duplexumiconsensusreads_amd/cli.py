@@ -472,10 +472,9 @@ def main(argv: Optional[list] = None, backend=None, rng=random, stats: Optional[
               "valid .bam file. Include the format in the file name.")
         raise ReferenceExit(1)
     be = _as_backend(backend, params, args.device)
-    lvl, nt = args.compression_level, args.threads
-    cons = native_io.BgzfWriter(consensus_filename, ing.header, lvl, nt)
-    excl = native_io.BgzfWriter("%s_filteredreads.bam" % consensus_filename[:-4], ing.header, lvl, nt)
-    unproc = native_io.BgzfWriter("%s_filteredfamilies.bam" % consensus_filename[:-4], ing.header, lvl, nt)
+    cons, excl, unproc = _open_writers(
+        [consensus_filename, "%s_filteredreads.bam" % consensus_filename[:-4],
+         "%s_filteredfamilies.bam" % consensus_filename[:-4]], ing.header, args, ing)
     ing.set_rng_state(rng.getstate())
     t_open = time.perf_counter()
     try:
@@ -497,16 +496,44 @@ def main(argv: Optional[list] = None, backend=None, rng=random, stats: Optional[
         _print_summary(c)
     finally:
         t_close = time.perf_counter()
-        rng.setstate(ing.rng_state(rng.getstate()))
-        excl.close()
-        unproc.close()
-        cons.close()
-        t_wclose = time.perf_counter()
-        ing.close()
+        try:
+            rng.setstate(ing.rng_state(rng.getstate()))
+        finally:
+            try:
+                _close_all(excl.close, unproc.close, cons.close)
+            finally:
+                t_wclose = time.perf_counter()
+                ing.close()
         if stats is not None:
             stats["close_s"] = time.perf_counter() - t_close
             stats["close_writers_s"] = t_wclose - t_close
     return 0
+
+
+def _close_all(*closers):
+    """Call every closer even when one raises; re-raise the first error."""
+    err = None
+    for fn in closers:
+        try:
+            fn()
+        except BaseException as e:          # noqa: BLE001 - re-raised below
+            if err is None:
+                err = e
+    if err is not None:
+        raise err
+
+
+def _open_writers(paths, header, args, ing=None):
+    """BGZF writers for ``paths``; when one fails to open, the ones already
+    open are closed (and ``ing`` with them) before the error propagates."""
+    ws = []
+    try:
+        for p in paths:
+            ws.append(native_io.BgzfWriter(p, header, args.compression_level, args.threads))
+    except BaseException:
+        _close_all(*(w.close for w in ws), *((ing.close,) if ing is not None else ()))
+        raise
+    return ws
 
 
 def _print_summary(c):
@@ -611,15 +638,13 @@ def _launch_ranks(argv, n):
 def _run_range(args, params, backend, path, rng, rng_state, rng_range, parts, device):
     """The ordinary pipeline over one range of families into part files;
     stdout, outcome, counters and random.sample calls in a dict."""
-    res = {"status": "ok", "exc_args": (), "calls": [], "counters": None, "stdout": "", "stats": {}}
-    lvl, nt = args.compression_level, args.threads
+    res = {"status": "ok", "exc_args": (), "calls": [], "counters": None, "stdout": "", "stats": {},
+           "sizes": [0, 0, 0]}
     out = io.StringIO()
     ing = native_io.Ingest(path, params.min_map_quality, params.min_reads, params.max_reads,
                            params.min_base_quality, args.threads, rng_range[0], rng_range[1])
     be = _as_backend(backend, params, device)
-    cons = native_io.BgzfWriter(parts[0], b"", lvl, nt)
-    excl = native_io.BgzfWriter(parts[1], b"", lvl, nt)
-    unproc = native_io.BgzfWriter(parts[2], b"", lvl, nt)
+    cons, excl, unproc = _open_writers(parts, b"", args, ing)
     ing.set_rng_state(rng_state)
     drv = _Driver(args, params, be, ing, cons, excl, unproc)
     drv.ends_at_eof = rng_range[1] == -1
@@ -636,32 +661,72 @@ def _run_range(args, params, backend, path, rng, rng_state, rng_range, parts, de
         res["calls"] = ing.sample_calls()
         res["counters"] = ing.counters()
         res["stats"] = dict(drv.stats)
-        excl.close()
-        unproc.close()
-        cons.close()
-        ing.close()
         res["stdout"] = out.getvalue()
+        try:
+            _close_all(excl.close, unproc.close, cons.close)
+        finally:
+            ing.close()
+        res["sizes"] = [os.path.getsize(p) for p in parts]
     return res
 
 
-def _merge_parts(final, header, parts, lvl, nt):
-    """header + the parts' blocks (each without its end-of-file block) + EOF."""
-    w = native_io.BgzfWriter(final, header, lvl, nt)
-    w.close()
-    with open(final, "r+b") as f:
-        f.seek(-len(_BGZF_EOF), 2)
-        f.truncate()
-        for p in parts:
-            n = os.path.getsize(p) - len(_BGZF_EOF)
-            with open(p, "rb") as src:
-                left = n
-                while left > 0:
-                    chunk = src.read(min(left, 64 << 20))
-                    if not chunk:
-                        break
-                    f.write(chunk)
-                    left -= len(chunk)
-        f.write(_BGZF_EOF)
+def _copy_range(src, dst_fd, n, dst_off):
+    """Bytes [0, n) of the file ``src`` into ``dst_fd`` at ``dst_off``, in the
+    kernel (copy_file_range: no user-space round trip; a reflink where the
+    file system has one)."""
+    with open(src, "rb") as f:
+        fd, done = f.fileno(), 0
+        while done < n:
+            try:
+                k = os.copy_file_range(fd, dst_fd, n - done, done, dst_off + done)
+            except OSError:
+                k = 0
+            if k <= 0:                      # no copy_file_range here: pread / pwrite
+                chunk = os.pread(fd, min(n - done, 64 << 20), done)
+                if not chunk:
+                    raise IOError(f"{src}: short part file")
+                k = os.pwrite(dst_fd, chunk, dst_off + done)
+            done += k
+
+
+def _merge_parallel(dist, rank, finals, header, args, sizes, upto):
+    """The output files from the ranks' part files, every rank copying its own
+    parts in parallel: rank 0 writes the header (then the BGZF EOF block at
+    the end); part r lands at the header's length plus the sizes of parts
+    0..r-1 (each without its own EOF block), an exclusive scan of the part
+    sizes every rank already holds (``sizes[r][k]``)."""
+    eof = len(_BGZF_EOF)
+    hl = [0, 0, 0]
+    if rank == 0:
+        for k in range(3):
+            w = native_io.BgzfWriter(finals[k], header, args.compression_level, args.threads)
+            w.close()
+            hl[k] = os.path.getsize(finals[k]) - eof
+            os.truncate(finals[k], hl[k])
+    obj = [hl]
+    dist.broadcast_object_list(obj, src=0)
+    hl = obj[0]
+    ends = []
+    for k in range(3):
+        off = hl[k]
+        for r in range(upto):
+            n = max(sizes[r][k] - eof, 0)
+            if r == rank and n:
+                fd = os.open(finals[k], os.O_WRONLY)
+                try:
+                    _copy_range("%s.part%d" % (finals[k], r), fd, n, off)
+                finally:
+                    os.close(fd)
+            off += n
+        ends.append(off)
+    if rank == 0:
+        for k in range(3):
+            fd = os.open(finals[k], os.O_WRONLY)
+            try:
+                os.pwrite(fd, _BGZF_EOF, ends[k])
+            finally:
+                os.close(fd)
+    dist.barrier()
 
 
 def _main_sharded(args, params, backend, rng, stats, group):
@@ -700,7 +765,8 @@ def _main_sharded(args, params, backend, rng, stats, group):
     parts = ["%s.part%d" % (f, rank) for f in finals]
     local = int(os.environ.get("LOCAL_RANK", rank))
     device = _rank_device(args, local) if backend is None else args.device
-    empty = {"status": "ok", "exc_args": (), "calls": [], "counters": None, "stdout": "", "stats": {}}
+    empty = {"status": "ok", "exc_args": (), "calls": [], "counters": None, "stdout": "", "stats": {},
+             "sizes": [0, 0, 0]}
     result, used, rounds = empty, None, 0
     if mine is not None:
         result = _run_range(args, params, backend, path, rng, s0, mine, parts, device)
@@ -728,20 +794,21 @@ def _main_sharded(args, params, backend, rng, stats, group):
     if stats is not None:
         stats.update(result["stats"])
         stats["shard_rounds"] = rounds
+    # the first failing rank ends the output as the reference stops; later
+    # ranks are dropped (every rank derives the same cut from the results)
+    fail = next((r for r in range(world) if results[r]["status"] != "ok"), None)
+    upto = min((fail + 1) if fail is not None else world, len(ranges))
+    t_merge = time.perf_counter()
+    _merge_parallel(dist, rank, finals, header, args, [results[r]["sizes"] for r in range(world)], upto)
+    if stats is not None:
+        stats["merge_s"] = time.perf_counter() - t_merge
     if rank == 0:
-        fail = next((r for r in range(world) if results[r]["status"] != "ok"), None)
-        upto = (fail + 1) if fail is not None else world
-        lvl, nt = args.compression_level, args.threads
-        for k in range(3):
-            _merge_parts(finals[k], header, ["%s.part%d" % (finals[k], r) for r in range(min(upto, len(ranges)))],
-                         lvl, nt)
         sys.stdout.write("".join(results[r]["stdout"] for r in range(upto)))
         state = s0
         for r in range(upto):
             state = native_io.py_replay(state, results[r]["calls"])
         if stats is not None:
             stats["ranks"] = [results[r]["stats"] for r in range(world)]
-    dist.barrier()
     for p in parts:
         if os.path.exists(p):
             os.remove(p)

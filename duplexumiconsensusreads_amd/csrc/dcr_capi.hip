@@ -59,8 +59,8 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 struct dcr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    // ev[0] batch start, ev[1..9] after (fused) prep, k_recmeta<ss>, fast<ss>, exact<ss>,
-    // general<ss>, k_recmeta<ds>, fast<ds>, exact<ds>, general<ds>
+    // ev[0] batch start, ev[1..8] after k_recmeta<ss>, fast<ss>, exact<ss>, general<ss>,
+    // k_recmeta<ds>, fast<ds>, exact<ds>, general<ds>
     hipEvent_t ev[DCR_N_KERNEL_TIMES + 1] = {};
     dcr_params *d_params = nullptr;
     DevBuf ws;          // workspace
@@ -97,10 +97,7 @@ struct dcr_ctx {
     uint32_t *d_wtab = nullptr;    // device [DCR_LUT_N] (general kernel's decision pass)
     int n_cu = 256;     // compute units (persistent grid size)
     int dfl_blocks = 1; // resident k_deflate workgroups per CU (dynamic LDS = sizeof(dfl::Shared))
-    size_t rs_bytes = 0;  // the workspace's record-scalar rows
     int fast_blocks[4] = {1, 1, 1, 1};   // resident k_consensus_fast blocks per CU (ss, ds; exact ss, exact ds)
-    int pair_blocks = 1;                  // resident k_consensus_pair blocks per CU
-    int pair_env = 0;                     // DCR_PAIR=1 turns the pair kernel on (measured slower)
 };
 
 // The fast kernel's assumptions (dcr_kernels.hip, fast kernel v2): every
@@ -247,14 +244,6 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->fast_blocks[k], fk[k], dcr::kFastBlock, 0) != hipSuccess ||
             c->fast_blocks[k] < 1)
             c->fast_blocks[k] = 1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->pair_blocks, (const void *)dcr::k_consensus_pair,
-                                                     dcr::kWave * 4, 0) != hipSuccess ||
-        c->pair_blocks < 1)
-        c->pair_blocks = 1;
-    {
-        const char *e = std::getenv("DCR_PAIR");
-        c->pair_env = e && e[0] == '1';
-    }
     if (hipFuncSetAttribute((const void *)dcrw::k_deflate, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(dfl::Shared)) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->dfl_blocks, dcrw::k_deflate, dfl::kT, sizeof(dfl::Shared)) !=
@@ -334,7 +323,6 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     const size_t o_stamp = o; o = align_up(o + 32 * sizeof(unsigned long long));
     const size_t n_rec = (size_t)std::max<int64_t>(4LL * s->n_fam, 1);
     const size_t o_ovf = o;  o = align_up(o + sizeof(int) * n_rec);
-    const size_t o_rs = o;   o = align_up(o + 48 * n_rec);
     const size_t o_xl = o;   o = align_up(o + sizeof(int) * n_rec);
     const size_t o_deep = o; o = align_up(o + sizeof(int) * n_rec);
     const size_t o_meta = o; o = align_up(o + sizeof(dcr::RecMeta) * n_rec);
@@ -356,11 +344,8 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     c->w.xcount = (int *)(b + o_err) + 5;
     c->w.gen_next = (int *)(b + o_err) + 7;      // [2], in the same block: reset with it per batch
     c->w.deep_count = (int *)(b + o_err) + 9;    // [1], likewise
-    c->w.pair_count = (int *)(b + o_err) + 10;   // [1], likewise
     c->w.deep = (int *)(b + o_deep);
     c->w.xlist = (int *)(b + o_xl);
-    c->w.rs = (uint32_t *)(b + o_rs);
-    c->rs_bytes = 48 * n_rec;
     c->w.stamps = (unsigned long long *)(b + o_stamp);
     c->w.ovf = (int *)(b + o_ovf);
     c->w.meta = (dcr::RecMeta *)(b + o_meta);
@@ -375,16 +360,11 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemsetAsync(c->w.err, 0, 64, c->stream));
-    // record-scalar rows: their markers must read 0 (k_scatter_scalars clears
-    // the rows it uses; the region moves with the workspace layout)
-    if (in->n_fam > 0) HIP_TRY(hipMemsetAsync(c->w.rs, 0, (size_t)48 * 4 * (size_t)in->n_fam, c->stream));
     c->last_reads = in->n_reads;
-    HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     // per-read preprocessing (:191-325) is fused: k_recmeta<ss> analyses the
     // clips and fully preprocesses the reads of records the fast kernel does
-    // not take; the fast kernel does the 3' trim of its own records.  ev[1]
-    // (the former k_prep slot) directly follows ev[0].
-    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    // not take; the fast kernel does the 3' trim of its own records
+    HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     dcr::Args a;
     a.in = *in;
     a.P = c->d_params;
@@ -393,9 +373,6 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     a.ds = *ds;
     a.fast_ok = c->fast_ok;
     a.t16 = c->wide_ok ? c->fast_t16 : -1;     // -1: no decision pass
-    // the pair kernel: the fast kernel's default quality checks (no quality
-    // below fast_qlo left unmasked) and its decision constants
-    a.pair_ok = c->pair_env && c->fast_ok && c->host_params.min_base_quality >= c->fast_qlo;
     a.wtab = c->d_wtab;
     // per strand: k_recmeta classifies every record (fast list / general list /
     // status written), then the fast kernel (8 records per wave) drains the fast list and
@@ -407,9 +384,6 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     // ~8 records per wave
     auto fast_grid = [&](int64_t n_rec, int k) {
         return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_rec + 127) / 128, (int64_t)c->fast_blocks[k] * c->n_cu));
-    };
-    auto scatter_grid = [&](int64_t n_rec) {
-        return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_rec + 255) / 256, (int64_t)c->n_cu * 16));
     };
     auto fast_args = [&](bool duplex) {
         dcr::FastArgs f{};
@@ -438,9 +412,6 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         f.lo_check = duplex || c->host_params.min_base_quality < c->fast_qlo;
         f.llr16 = c->d_llr16;
         f.want_info = (c->options & DCR_OPT_READ_INFO) ? 1 : 0;
-        f.rs = c->w.rs;
-        f.pair_count = c->w.pair_count;
-        f.pair_top = a.n_rec - 1;
         return f;
     };
     auto strand = [&](bool duplex) -> int {
@@ -458,7 +429,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         const int64_t rpb = (int64_t)rm_waves * rpw;                // records per k_recmeta block
         const unsigned nb = (unsigned)((a.n_rec + rpb - 1) / rpb);
         const size_t rm_lds = dcr::recmeta_lds_bytes(rm_waves);
-        hipEvent_t *ev = c->ev + (duplex ? 6 : 2);
+        hipEvent_t *ev = c->ev + (duplex ? 5 : 1);
         // the exact queue is filled by the common kernel; its length is only
         // known on the device, so the exact kernel gets the resident grid
         const unsigned gx = (unsigned)((int64_t)c->fast_blocks[duplex ? 3 : 2] * c->n_cu);
@@ -469,8 +440,6 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
                                0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL((dcr::k_consensus_fast<true, true>), dim3(gx), dim3(dcr::kFastBlock), 0, c->stream, fa);
-            hipLaunchKernelGGL(dcr::k_scatter_scalars, dim3(scatter_grid(a.n_rec)), dim3(256), 0, c->stream,
-                               dcr::ScatterArgs{c->w.rs, c->w.rs, *ds, in->ds_col_off, a.n_rec});
             HIP_TRY(hipEventRecord(ev[2], c->stream));
             hipLaunchKernelGGL(dcr::k_decide<true>, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
             hipLaunchKernelGGL(dcr::k_consensus_general<true>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
@@ -479,19 +448,10 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
             hipLaunchKernelGGL(dcr::k_recmeta<false>, dim3(nb), dim3(rm_waves * dcr::kWave), rm_lds, c->stream, a);
             hipLaunchKernelGGL(dcr::k_prep_big, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
             HIP_TRY(hipEventRecord(ev[0], c->stream));
-            // the pair list (two records per wave) and the fast list: the
-            // single-strand consensus slot times both
-            if (a.pair_ok)
-                hipLaunchKernelGGL(dcr::k_consensus_pair,
-                                   dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((a.n_rec + 255) / 256,
-                                                                    (int64_t)c->pair_blocks * c->n_cu))),
-                                   dim3(dcr::kWave * 4), 0, c->stream, fa);
             hipLaunchKernelGGL((dcr::k_consensus_fast<false, false>), dim3(fast_grid(a.n_rec, 0)),
                                dim3(dcr::kFastBlock), 0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL((dcr::k_consensus_fast<false, true>), dim3(gx), dim3(dcr::kFastBlock), 0, c->stream, fa);
-            hipLaunchKernelGGL(dcr::k_scatter_scalars, dim3(scatter_grid(a.n_rec)), dim3(256), 0, c->stream,
-                               dcr::ScatterArgs{c->w.rs, c->w.rs, *ss, in->ss_col_off, a.n_rec});
             HIP_TRY(hipEventRecord(ev[2], c->stream));
             hipLaunchKernelGGL(dcr::k_decide<false>, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
             hipLaunchKernelGGL(dcr::k_decide_deep, dim3(2 * c->n_cu), dim3(dcr::kDeepWaves * dcr::kWave), 0, c->stream, a);
@@ -506,7 +466,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         if ((rc = strand(false))) return rc;
         if ((rc = strand(true))) return rc;
     } else {
-        for (int k = 2; k <= DCR_N_KERNEL_TIMES; ++k) HIP_TRY(hipEventRecord(c->ev[k], c->stream));
+        for (int k = 1; k <= DCR_N_KERNEL_TIMES; ++k) HIP_TRY(hipEventRecord(c->ev[k], c->stream));
     }
     c->timed = true;
     return DCR_OK;
@@ -529,9 +489,9 @@ int dcr_last_timing(dcr_ctx *c, float *ms4) {
     if (!c->timed) return fail(DCR_EARG, "no batch has run");
     const int last = DCR_N_KERNEL_TIMES;
     HIP_TRY(hipEventSynchronize(c->ev[last]));
-    HIP_TRY(hipEventElapsedTime(&ms4[0], c->ev[0], c->ev[1]));
-    HIP_TRY(hipEventElapsedTime(&ms4[1], c->ev[1], c->ev[5]));
-    HIP_TRY(hipEventElapsedTime(&ms4[2], c->ev[5], c->ev[last]));
+    ms4[0] = 0.0f;                       // preprocessing is fused into k_recmeta / the fast kernel
+    HIP_TRY(hipEventElapsedTime(&ms4[1], c->ev[0], c->ev[4]));
+    HIP_TRY(hipEventElapsedTime(&ms4[2], c->ev[4], c->ev[last]));
     HIP_TRY(hipEventElapsedTime(&ms4[3], c->ev[0], c->ev[last]));
     return DCR_OK;
 }

@@ -359,12 +359,10 @@ extern "C" {
 
 dcr_bgzw *dcr_bgzw_open(const char *path, int level, int n_threads) {
     if (!path || level < 0 || level > 12) { g_err = "bad arguments"; return nullptr; }
-    // Opened without O_TRUNC and cut to the written length at close: the same
-    // bytes as "wb", but rewriting a file that exists (a rerun, a bench pass)
-    // does not free its page-cache pages at open (7-70 ms per 150 MB here)
-    // nor, on ext4, start the writeback at close that a truncate-to-zero
-    // followed by a rewrite triggers (auto_da_alloc)
-    const int fd = ::open(path, O_WRONLY | O_CREAT | O_CLOEXEC, 0666);
+    // truncated at open, as fopen("wb"): works for any output (a FIFO,
+    // /dev/null) and a run that never reaches close leaves a short file with
+    // no BGZF EOF marker, never a new prefix over an old file's tail
+    const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
     FILE *f = fd >= 0 ? ::fdopen(fd, "wb") : nullptr;
     if (!f) {
         if (fd >= 0) ::close(fd);
@@ -405,8 +403,6 @@ int dcr_bgzw_close(dcr_bgzw *w) {
     if (!w->bad && w->n_in && !w->flush(w->n_in)) rc = DCR_IO_EFILE;
     if (std::fwrite(kEof, 1, sizeof kEof, w->f) != sizeof kEof) rc = fail(DCR_IO_EFILE, "write failed");
     if (std::fflush(w->f) != 0) rc = fail(DCR_IO_EFILE, "write failed");
-    const long end = std::ftell(w->f);
-    if (end < 0 || ::ftruncate(fileno(w->f), (off_t)end) != 0) rc = fail(DCR_IO_EFILE, "truncate failed");
     if (std::fclose(w->f) != 0) rc = fail(DCR_IO_EFILE, "close failed");
     delete w;
     return rc;

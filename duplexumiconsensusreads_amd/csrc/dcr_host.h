@@ -9,11 +9,15 @@
 #include <condition_variable>
 #include <cstddef>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
 #include <new>
+#include <sched.h>
 #include <sys/mman.h>
 #include <thread>
 #include <vector>
@@ -127,10 +131,44 @@ class HugeBuf {
     size_t cap_ = 0, n_ = 0;
 };
 
+// CPUs this process may use: the affinity mask, capped by the cgroup's CPU
+// quota (cgroup v2 cpu.max, or v1 cfs_quota / cfs_period), shared among the
+// processes of this node's local ranks (LOCAL_WORLD_SIZE, set by
+// torch.distributed.run).  hardware_concurrency() counts every CPU of the
+// machine, which on a GPU node is many times the share of one process.
+inline int available_cpus() {
+    int n = 0;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+    if (n <= 0) {
+        const unsigned hc = std::thread::hardware_concurrency();
+        n = hc ? (int)hc : 1;
+    }
+    long quota = -1, period = 0;
+    if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        if (std::fscanf(f, "%31s %ld", q, &period) == 2 && std::strcmp(q, "max") != 0) quota = std::atol(q);
+        std::fclose(f);
+    } else if (FILE *fq = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+        if (std::fscanf(fq, "%ld", &quota) != 1) quota = -1;
+        std::fclose(fq);
+        if (FILE *fp = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+            if (std::fscanf(fp, "%ld", &period) != 1) period = 0;
+            std::fclose(fp);
+        }
+    }
+    if (quota > 0 && period > 0) n = std::min<long>(n, std::max<long>(1, (quota + period - 1) / period));
+    int ranks = 1;
+    if (const char *e = std::getenv("LOCAL_WORLD_SIZE")) ranks = std::max(1, std::atoi(e));
+    return std::max(1, n / ranks);
+}
+
+// threads of a host pool: n when the caller asks (n > 0), else this
+// process's CPU share (available_cpus), at most 16
 inline int pick_threads(int n) {
     if (n > 0) return std::min(n, 64);
-    unsigned hc = std::thread::hardware_concurrency();
-    return (int)std::max(1u, std::min(hc ? hc : 1u, 16u));
+    static const int avail = available_cpus();
+    return std::max(1, std::min(avail, 16));
 }
 
 // Persistent workers; run(n, fn) calls fn(i) for i in [0, n) on the workers

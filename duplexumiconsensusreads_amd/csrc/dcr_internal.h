@@ -16,10 +16,6 @@ inline size_t recmeta_lds_bytes(int nw) { return (size_t)nw * (48 * 64 + 4 * 64 
 constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kFastWaves = 4;               // k_consensus_fast: five 4-wave blocks per CU (5 waves per SIMD)
 constexpr int kFastBlock = kWave * kFastWaves;
-// k_consensus_pair: two single-strand records per wave (32 lanes each)
-constexpr int kPairMaxR = 16;               // reads per record (the fixed-point mean's depth limit)
-constexpr int kPairMaxT = 160;              // columns: five 32-column half tiles
-constexpr int kPairMaxDw = 320;             // staged dwords per record (1,280 bytes)
 constexpr int kDeepReads = 64;              // k_decide: single-strand records of this many reads go to k_decide_deep
 constexpr int kDeepWaves = 8;               // k_decide_deep: waves per record (one 512-thread block, two per CU)
 
@@ -51,8 +47,6 @@ struct Workspace {
     int *gen_next;          // [2] next general-list entry to claim (k_consensus_general)
     int *deep;              // [n_rec] general-list indices of deep single-strand records (k_decide_deep)
     int *deep_count;        // [1] their number
-    int *pair_count;        // [1] single-strand records in the pair list (meta[n_rec - 1], downwards)
-    uint32_t *rs;           // [n_rec][12] record scalars of the fast kernel's records (k_scatter_scalars)
     int *xlist;             // [n_rec] exact queue: fast-list indices (k_consensus_fast<., true>)
     unsigned long long *stamps;   // [32] diagnostic phase cycles (DCR_STAMP builds only)
     RecMeta *meta;          // [n_rec] fast list
@@ -71,7 +65,6 @@ struct Args {
     int rpw;                // k_recmeta: records per wave (a power of two <= 64; fewer for deep records)
     int t16;                // decision margin in 1/16 nat (fast_constants)
     const uint32_t *wtab;   // [DCR_LUT_N] per LUT row: LLR term | -ln(p'/5) bound << 16 | not-a-call-row << 31
-    int pair_ok;            // single-strand records of the pair shape go to k_consensus_pair
 };
 
 // the fast kernel's compact arguments (one strand; fewer scalar registers than Args)
@@ -100,29 +93,13 @@ struct FastArgs {
     int lo_check;                   // some unmasked quality may lie below fast_qlo: check the bytes
     const uint16_t *llr16;          // [123] per-quality LLR term, 1/16 nat, rounded down
     int want_info;                  // single-strand: write every read's dcr_read_info (DCR_OPT_READ_INFO)
-    uint32_t *rs;                   // [n_rec][12] the record's scalar fields, [10] = 1 (k_scatter_scalars)
-    const int *pair_count;          // k_consensus_pair: records in the pair list ...
-    int64_t pair_top;               // ... at meta[pair_top - k], k = 0, 1, ...
 };
 
-// the fast kernels' record scalars, one contiguous 48-byte row per record,
-// scattered into the dcr_out arrays by one coalesced pass
-struct ScatterArgs {
-    const uint32_t *rs;
-    uint32_t *rs_clear;
-    dcr_out O;
-    const int64_t *col_off;
-    int64_t n_rec;
-};
-
-__global__ void k_prep(dcr_batch in, const dcr_params *P, Workspace ws);
 template <bool DUPLEX> __global__ void k_recmeta(Args a);
 __global__ void k_prep_big(Args a);
 template <bool DUPLEX, bool EXACT> __global__ void k_consensus_fast(FastArgs a);
-__global__ void k_consensus_pair(FastArgs a);
 template <bool DUPLEX> __global__ void k_consensus_general(Args a);
 template <bool DUPLEX> __global__ void k_decide(Args a);
 __global__ void k_decide_deep(Args a);
-__global__ void k_scatter_scalars(ScatterArgs s);
 
 }  // namespace dcr

@@ -2,9 +2,11 @@
 //
 // Reference: /root/reference/DuplexUMIConsensusReads.py (":line" below).
 //
-//   k_prep       one lane per read: remove_clipping / mask / trim_3prime_N
-//                (:191-325) -> kept sequence window + normalised M/I/D runs.
-//   k_consensus  one wavefront per consensus record (single-strand: one
+//   k_recmeta    one lane per record: classifies it (fast list / general list /
+//                status); prep_read (remove_clipping / mask / trim_3prime_N,
+//                :191-325) for the reads of general records.
+//   k_consensus_fast / _general
+//                one wavefront per consensus record (single-strand: one
 //                subfamily; duplex: one A1+B2 / B1+A2 pair).  Phases:
 //                  0. stage the record's bases/quals from HBM into LDS as
 //                     16-bit element codes (wide coalesced loads, one trip)
@@ -119,7 +121,7 @@ __device__ __forceinline__ void lds_fence() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// ------------------------------------------------------------------ k_prep
+// ------------------------------------------------------------------ prep_read
 // remove_clipping (:191-265): drop H; drop S with its bases (5'/3' ends);
 // mask_low_quality_bases (:268-289): base -> 'N' if qual < min_base_quality
 // (applied by the consumer); trim_3prime_N (:292-325): drop trailing 'N' and
@@ -191,11 +193,6 @@ __device__ __forceinline__ void prep_read(const dcr_batch &in, const dcr_params 
     inf.n_cig = nout;
     inf.has_ins = has_ins;
     ws.info[i] = inf;
-}
-
-__global__ __launch_bounds__(256) void k_prep(dcr_batch in, const dcr_params *P, Workspace ws) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < in.n_reads) prep_read(in, P, ws, i);
 }
 
 // Clip-only view of a read (remove_clipping :191-265 without the 3' N trim,
@@ -1966,7 +1963,7 @@ __device__ __forceinline__ double pairwise_et(const double *a, int n, int lane) 
 // ------------------------------------------------------------ k_recmeta
 // Classifies every record before any consensus work: the status the reference
 // reaches first (a read that failed preprocessing, or an empty read — :1291-1300
-// via the read statuses of k_prep), a fast record, or a general one.  For fast
+// via the read statuses of prep_read), a fast record, or a general one.  For fast
 // records it writes the launch metadata the fast kernel fetches with one scalar
 // load per record plus one 8-byte load per read.
 //
@@ -2260,11 +2257,7 @@ __global__ __launch_bounds__(kRecmetaWaves * kWave) void k_recmeta(Args a) {
                 !a.fast_ok || base_al + span >= 0xFFFFF000ll) {
                 kind = 1;
             } else {
-                // the pair shape (k_consensus_pair): few reads, short, in the batch's first 2 GiB
-                kind = !DUPLEX && a.pair_ok && R <= kPairMaxR && T <= kPairMaxT && span <= 4 * kPairMaxDw &&
-                               base_al + span < 0x7FFFF000ll
-                           ? 3
-                           : 0;
+                kind = 0;
                 m.base_al = (uint32_t)base_al;
                 // MAPQ = trunc(mean) of the reads' MAPQs (:874-889, :1377), here
                 // rather than a wave reduction per record in the fast kernel
@@ -2282,10 +2275,9 @@ __global__ __launch_bounds__(kRecmetaWaves * kWave) void k_recmeta(Args a) {
     }
     const uint64_t bf = __ballot(kind == 0);
     const uint64_t bg = __ballot(kind == 1);
-    const uint64_t bp = __ballot(kind == 3);
-    if (lane < 3) s_cnt[lane * nwb + wave] = __popcll(lane == 0 ? bf : (lane == 1 ? bg : bp));
+    if (lane < 2) s_cnt[lane * nwb + wave] = __popcll(lane == 0 ? bf : bg);
     __syncthreads();
-    if (threadIdx.x < 3) {                       // list t: the waves' exclusive prefix, one atomic
+    if (threadIdx.x < 2) {                       // list t: the waves' exclusive prefix, one atomic
         const int t = threadIdx.x;
         int tot = 0;
         for (int w = 0; w < nwb; ++w) {
@@ -2293,22 +2285,21 @@ __global__ __launch_bounds__(kRecmetaWaves * kWave) void k_recmeta(Args a) {
             s_cnt[t * nwb + w] = tot;
             tot += c;
         }
-        int *ctr = t == 0 ? &a.ws.fast_count[DUPLEX ? 1 : 0] : (t == 1 ? &a.ws.ovf_count[DUPLEX ? 1 : 0] : a.ws.pair_count);
+        int *ctr = t == 0 ? &a.ws.fast_count[DUPLEX ? 1 : 0] : &a.ws.ovf_count[DUPLEX ? 1 : 0];
         const int base = tot ? atomicAdd(ctr, tot) : 0;
         for (int w = 0; w < nwb; ++w) s_cnt[t * nwb + w] += base;
     }
     __syncthreads();
-    const int basef = s_cnt[wave], baseg = s_cnt[nwb + wave], basep = s_cnt[2 * nwb + wave];
+    const int basef = s_cnt[wave], baseg = s_cnt[nwb + wave];
     const uint64_t lt = lanemask_lt(lane);
     if (kind == 0) a.ws.meta[basef + __popcll(bf & lt)] = m;
-    if (kind == 3) a.ws.meta[a.n_rec - 1 - (basep + __popcll(bp & lt))] = m;   // the pair list, from the top
     if (kind == 1) a.ws.ovf[baseg + __popcll(bg & lt)] = (int)rk;
     // single-strand reads of records the fast kernel does not take need the full
     // preprocessing (3' trim included) for the general kernel and the host;
     // records of more than 64 reads are left to k_prep_big (a block per record,
     // not one wave walking every read of 64 records)
-    if (!DUPLEX) agg[lane].kind = (vk && R > kWave) ? 2 : (kind == 3 ? 0 : kind);
-    if (DUPLEX || __ballot(vk && kind != 0 && kind != 3 && R <= kWave) == 0) return;
+    if (!DUPLEX) agg[lane].kind = (vk && R > kWave) ? 2 : kind;
+    if (DUPLEX || __ballot(vk && kind != 0 && R <= kWave) == 0) return;
     lds_fence();
     carry = -1;
     for (int64_t c = gbeg; c < gend; c += kWave) {
@@ -2374,8 +2365,8 @@ constexpr int kTable = 5 * 0x800;                          // 5 class banks of 2
 constexpr int kStage0 = kTable;                            // 4 KiB per wave
 constexpr int kInvD = kStage0 + kWaves * 0x1000;           // f64 [64] 1 / d
 constexpr int kSent = kInvD + 64 * 8;                      // u16 pad code (out-of-read sentinel)
-constexpr int kPtrs = kSent + 16;                          // u64 [10] record-scalar destinations, [6] rare-path pointers
-constexpr int kRm = kPtrs + 16 * 8;                        // per wave: u64 [64] the current record's read words
+constexpr int kPtrs = kSent + 16;                          // u64 [24] pointers (kP* below)
+constexpr int kRm = kPtrs + 24 * 8;                        // per wave: u64 [64] the current record's read words
 constexpr int kMv = kRm + kWaves * kWave * 8;              // per wave: u32 [8] a later record's descriptor
 constexpr int kOv = kMv + kWaves * 32;                     // per wave: u16 [256] column words d | e << 6 | call << 12
 constexpr int kM720 = kOv + kWaves * 512;                  // u32 [64] 720720 / d for depths d <= 16, else 0
@@ -2388,6 +2379,12 @@ static_assert(16 * (kRowMax + 5) <= 0x800, "a class bank fits 2 KiB");
 static_assert(5 * kLdsBytes <= 160 * 1024, "five blocks (20 waves) per CU");
 
 __device__ __forceinline__ int stage_base(int wave) { return kStage0 + (wave << 12); }
+// pointer-cache slots: every pointer the record loop stores through is read
+// from LDS where it is used, so none is held in scalar registers across the
+// loop (the kernel's arguments no longer spill into VGPR lanes, whose
+// restores are VALU instructions)
+constexpr int kPNormCig = 10, kPCigOff = 11, kPOvf = 12, kPOvfCount = 13, kPXlist = 14, kPXcount = 15;
+constexpr int kPD = 16, kPE = 17, kPSeq = 18, kPQual = 19, kPStatus = 20, kPInfo = 21, kPParams = 22;
 }  // namespace fk
 
 constexpr int kStageDw = kStageElems / 4 / kWave;   // staged dwords per lane
@@ -2553,12 +2550,11 @@ __device__ __forceinline__ void run_evidence(Evidence<NT> &ev, const uint8_t *ld
 }
 
 // destination of record scalar k (lane k: field k of dcr_out) as one word:
-// pointer | rec_mul << 56 | off_mul << 60, address = pointer + rec * rec_mul +
-// off * off_mul.  Kept in LDS (read once per record) rather than in scalar
-// registers for the whole kernel.
+// pointer | shift << 56, address = pointer + (index << shift), index = the
+// record (the output column offset for k = 9, the CIGAR).  Kept in LDS (read
+// once per record) rather than in registers for the whole kernel.
 __device__ __forceinline__ uint64_t scalar_dest(const dcr_out &O, int k) {
-    const uint64_t rec_mul = k < 7 ? 4u : (k < 9 ? 8u : 0u);
-    const uint64_t off_mul = k == 9 ? 4u : 0u;
+    const uint64_t shift = (k == 7 || k == 8) ? 3u : 2u;
     const uint8_t *p;
     switch (k) {
     case 0: p = (const uint8_t *)O.pos; break;
@@ -2572,7 +2568,25 @@ __device__ __forceinline__ uint64_t scalar_dest(const dcr_out &O, int k) {
     case 8: p = (const uint8_t *)O.E + 4; break;
     default: p = (const uint8_t *)O.cigar; break;
     }
-    return (uint64_t)(uintptr_t)p | (rec_mul << 56) | (off_mul << 60);
+    return (uint64_t)(uintptr_t)p | (shift << 56);
+}
+
+// a pointer cached in LDS at kernel start, as a per-lane value (one
+// broadcast LDS read; stores through it take a 64-bit VGPR address)
+template <class Tp>
+__device__ __forceinline__ Tp *lds_vptr(const uint8_t *lds, int slot) {
+    return (Tp *)(uintptr_t)(*(const uint64_t *)(lds + fk::kPtrs + 8 * slot));
+}
+
+// a record's failure status from the fast kernel: status byte and zeroed
+// scalars as write_status_at writes them, lane k storing field k
+__device__ __forceinline__ void fast_status(const uint8_t *lds, int64_t rec, int st, int lane) {
+    if (lane < 9) {
+        const uint64_t pw = *(const uint64_t *)(lds + fk::kPtrs + 8 * lane);
+        *(uint32_t *)((pw & 0x00FFFFFFFFFFFFFFull) + ((uint64_t)rec << (pw >> 56))) = 0u;
+    } else if (lane == 10) {
+        lds_vptr<uint8_t>(lds, fk::kPStatus)[rec] = (uint8_t)st;
+    }
 }
 
 // a pointer cached in LDS at kernel start (rare paths), as a scalar
@@ -2624,12 +2638,12 @@ template <bool DUPLEX>
 __device__ __forceinline__ void send_to_general_(int rec, int g0, int R, uint32_t rmx, const uint8_t *lds, int lane) {
     if (!DUPLEX && lane < R) {
         const int tl = ((int)rmx >> 8) & 255;
-        uint32_t *norm_cig = lds_ptr<uint32_t>(lds, 10);
-        const int32_t *cig_off = lds_ptr<const int32_t>(lds, 11);
+        uint32_t *norm_cig = lds_ptr<uint32_t>(lds, fk::kPNormCig);
+        const int32_t *cig_off = lds_ptr<const int32_t>(lds, fk::kPCigOff);
         if (tl > 0) norm_cig[cig_off[g0 + lane]] = (uint32_t)tl << 4;   // one M run
     }
-    int *ovf = lds_ptr<int>(lds, 12);
-    int *ovf_count = lds_ptr<int>(lds, 13);
+    int *ovf = lds_ptr<int>(lds, fk::kPOvf);
+    int *ovf_count = lds_ptr<int>(lds, fk::kPOvfCount);
     if (lane == 0) {
         const int idx = atomicAdd(ovf_count, 1);
         ovf[idx] = rec;
@@ -2649,7 +2663,7 @@ __device__ __forceinline__ void send_to_general(const FastArgs &a, const RecMeta
         inf.n_cig = tl > 0 ? 1 : 0;
         inf.status = tl > 0 ? DCR_ST_OK : DCR_ST_INDEX_ERROR;
         inf.has_ins = 0;
-        a.info[m.g0 + lane] = inf;
+        lds_vptr<dcr_read_info>(lds, fk::kPInfo)[m.g0 + lane] = inf;
     }
     send_to_general_<DUPLEX>(m.rec, m.g0, R, rm.x, lds, lane);
 }
@@ -2661,7 +2675,21 @@ struct Staged {
 };
 
 // after the codes: 3' trim (single-strand), read info, T; invalid input -> general
-template <bool DUPLEX>
+//
+// QUICK (the common instantiation, read info not requested): the trim cannot
+// change a DECIDED column.  A trimmed base is an 'N' row either way (class N,
+// or a base masked below min_base_quality): its LLR term is 0 and it counts
+// as 'N' in d and e (:1001, :1011), exactly as the padding 'N' that replaces
+// it.  So the trim matters only when it empties a read (compress_cigarlist([])
+// :740 via :322), when it shrinks T (every read reaching the last column ends
+// in 'N'), or for the products of undecided columns (the pad quality is 2),
+// which the EXACT instantiation recomputes from scratch with the full trim.
+// QUICK therefore reads each read's first and last element only: a read
+// whose last element is a base keeps its length, one whose first element is
+// a base keeps at least one; when some read ending at T ends in a base, T
+// stays.  Anything else (and invalid input, whose record the general kernel
+// takes with the trimmed lengths) runs the full trim below.
+template <bool DUPLEX, bool QUICK>
 __device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &m, uint2 rm, uint32_t bad,
                                               const uint8_t *lds, int stage_addr, int lane) {
     Staged s;
@@ -2669,40 +2697,54 @@ __device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &
     s.T = (int)((m.w >> 7) & 255u);
     s.state = 0;
     lds_fence();
+    const bool any_bad = __ballot(bad != 0) != 0;
     if (!DUPLEX) {
         // trim_3prime_N (:292-325): drop each read's trailing 'N' (sequenced, or
         // masked below min_base_quality, :280): codes of class N, from the end
         const int x = (int)rm.x, y = (int)rm.y;
         const int col = x & 255;
         int tl = lane < R ? (x >> 8) & 255 : 0;
-        bool go = tl > 0;
-        while (__ballot(go)) {
-            if (go) {
-                const uint32_t code = *(const uint16_t *)(lds + stage_addr + 2 * (y + tl - 1));
-                // an 'N' row: sequenced 'N' or a masked quality (:280, folded into the table)
-                if (*(const uint32_t *)(lds + code + 8) & 63u) --tl; else go = false;
-                go = go && tl > 0;
+        bool full = true;
+        if (QUICK && !a.want_info && !any_bad) {
+            bool lastN = true, firstN = true;
+            if (tl > 0) {
+                const uint32_t cl = *(const uint16_t *)(lds + stage_addr + 2 * (y + tl - 1));
+                const uint32_t cf = *(const uint16_t *)(lds + stage_addr + 2 * y);
+                lastN = (*(const uint32_t *)(lds + cl + 8) & 63u) != 0;
+                firstN = (*(const uint32_t *)(lds + cf + 8) & 63u) != 0;
             }
+            full = __ballot(lane < R && lastN && firstN) != 0 || __ballot(lane < R && col + tl == s.T && !lastN) == 0;
         }
-        if (lane < R && (a.want_info || tl == 0)) {
-            dcr_read_info inf;
-            inf.seq_start = m.base_al + y;
-            inf.len = tl;
-            inf.n_cig = tl > 0 ? 1 : 0;
-            inf.status = tl > 0 ? DCR_ST_OK : DCR_ST_INDEX_ERROR;   // compress_cigarlist([]) :740 via :322
-            inf.has_ins = 0;
-            a.info[m.g0 + lane] = inf;
-        }
-        rm.x = (rm.x & ~0xFF00u) | ((uint32_t)tl << 8);
-        // T shrinks only when every read reaching the untrimmed end lost its tail
-        if (__ballot(lane < R && col + tl == s.T) == 0) s.T = wave_max(lane < R ? col + tl : 0);
-        if (__ballot(lane < R && tl == 0)) {
-            if (lane == 0) write_status_at(a.O, m.rec, DCR_ST_PREP | DCR_ST_INDEX_ERROR);
-            s.state = 2;
+        if (full) {
+            bool go = tl > 0;
+            while (__ballot(go)) {
+                if (go) {
+                    const uint32_t code = *(const uint16_t *)(lds + stage_addr + 2 * (y + tl - 1));
+                    // an 'N' row: sequenced 'N' or a masked quality (:280, folded into the table)
+                    if (*(const uint32_t *)(lds + code + 8) & 63u) --tl; else go = false;
+                    go = go && tl > 0;
+                }
+            }
+            if (lane < R && (a.want_info || tl == 0)) {
+                dcr_read_info inf;
+                inf.seq_start = m.base_al + y;
+                inf.len = tl;
+                inf.n_cig = tl > 0 ? 1 : 0;
+                inf.status = tl > 0 ? DCR_ST_OK : DCR_ST_INDEX_ERROR;   // compress_cigarlist([]) :740 via :322
+                inf.has_ins = 0;
+                lds_vptr<dcr_read_info>(lds, fk::kPInfo)[m.g0 + lane] = inf;
+            }
+            rm.x = (rm.x & ~0xFF00u) | ((uint32_t)tl << 8);
+            // T shrinks only when every read reaching the untrimmed end lost its tail
+            if (__ballot(lane < R && col + tl == s.T) == 0) s.T = wave_max(lane < R ? col + tl : 0);
+            if (__ballot(lane < R && tl == 0)) {
+                fast_status(lds, m.rec, DCR_ST_PREP | DCR_ST_INDEX_ERROR, lane);
+                s.state = 2;
+            }
         }
     }
     s.rm = rm;
-    if (s.state == 0 && __ballot(bad != 0)) s.state = 1;
+    if (s.state == 0 && any_bad) s.state = 1;
     return s;
 }
 
@@ -2723,7 +2765,6 @@ template <bool DUPLEX, int NT, bool EXACT>
 __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &m, const Staged &sg, uint8_t *lds,
                                               const int stage_addr, const int ov_addr, const int rm_addr, const int lane,
                                               Stamps &sp, const double2 *xt, const uint32_t *r1) {
-    const dcr_out &O = a.O;
     const int64_t rec = m.rec;
     const int64_t off = m.off;
     const int R = (int)(m.w & 127u);
@@ -2731,7 +2772,7 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     const int minpos = m.minpos;
     const uint2 rm = sg.rm;
     if (DCR_ABL == 1) {                 // diagnostic: staging only
-        if (lane == 0) O.pos[rec] = *(const uint16_t *)(lds + stage_addr + 2 * (int)(rm.y & 7)) + m.d0;
+        if (lane == 0) a.O.pos[rec] = *(const uint16_t *)(lds + stage_addr + 2 * (int)(rm.y & 7)) + m.d0;
         return true;
     }
     const int colr = (int)(rm.x & 255u), lenr = (int)((rm.x >> 8) & 255u);
@@ -2744,7 +2785,7 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         uint32_t x = 0;
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt) x += (uint32_t)ev.llr[tt] ^ (uint32_t)(ev.llr[tt] >> 32) ^ ev.cnt[tt];
-        if (lane == 0) O.pos[rec] = (int)x;
+        if (lane == 0) a.O.pos[rec] = (int)x;
         return true;
     }
 
@@ -2799,7 +2840,7 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     // read-word LDS (free once the read words are in registers)
     uint16_t *chq = (uint16_t *)(lds + rm_addr);
     if (exact) {
-        const dcr_params *P = a.P;
+        const dcr_params *P = lds_ptr<const dcr_params>(lds, fk::kPParams);
         const double *qthr = P->qthresh;
         bool fail = false;             // '+' / '-' call or int(-inf) quality: general kernel
 #pragma unroll 1
@@ -2909,8 +2950,9 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         const int c0 = 4 * lane;
         if (c0 < T16) {
             const uint2 w = *(const uint2 *)(ov + 8 * lane);
-            *(uint2 *)(O.d + off + c0) = make_uint2(w.x & 0x003F003Fu, w.y & 0x003F003Fu);
-            *(uint2 *)(O.e + off + c0) = make_uint2((w.x >> 6) & 0x003F003Fu, (w.y >> 6) & 0x003F003Fu);
+            *(uint2 *)(lds_vptr<uint16_t>(lds, fk::kPD) + off + c0) = make_uint2(w.x & 0x003F003Fu, w.y & 0x003F003Fu);
+            *(uint2 *)(lds_vptr<uint16_t>(lds, fk::kPE) + off + c0) =
+                make_uint2((w.x >> 6) & 0x003F003Fu, (w.y >> 6) & 0x003F003Fu);
             const int nl = min(max(klen - c0, 0), 4);                    // kept columns of the four
             const uint32_t keep = nl == 4 ? 0xFFFFFFFFu : (1u << (8 * nl)) - 1u;
             uint32_t letters, quals;
@@ -2924,8 +2966,8 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
                 letters = *(const uint32_t *)(sb + c0);
                 quals = *(const uint32_t *)(sb + 0x100 + c0);
             }
-            *(uint32_t *)(O.seq + off + c0) = (letters & keep) | (0x4E4E4E4Eu & ~keep);
-            *(uint32_t *)(O.qual + off + c0) = quals & keep;
+            *(uint32_t *)(lds_vptr<uint8_t>(lds, fk::kPSeq) + off + c0) = (letters & keep) | (0x4E4E4E4Eu & ~keep);
+            *(uint32_t *)(lds_vptr<uint8_t>(lds, fk::kPQual) + off + c0) = quals & keep;
         }
     }
     sp.mark(8);                          // [7] per-column stores
@@ -2998,28 +3040,33 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     }
     }
     sp.mark(9);                          // [8] mean
-    // the record's scalar fields in one dword store (lane k writes field k,
-    // lane 9 the single M run of the CIGAR) plus the status byte
+    // the record's scalar fields straight into the dcr_out arrays: lane k
+    // stores field k (pos :790, MAPQ, len, n_cig, n_de, D, M, E as two words,
+    // the single M run of the kept columns), lane 10 the status byte.  The
+    // waves of one XCD take consecutive records (k_consensus_fast), so the
+    // lines these 4-byte stores share fill up in one L2
     {
-        const int E_lo = (int)(uint32_t)__double_as_longlong(E);
-        const int E_hi = (int)(uint32_t)((uint64_t)__double_as_longlong(E) >> 32);
+        const uint32_t E_lo = (uint32_t)__double_as_longlong(E);
+        const uint32_t E_hi = (uint32_t)((uint64_t)__double_as_longlong(E) >> 32);
         const int mapq = (int)((uint32_t)m.d0 >> 16);                        // k_recmeta
-        // lane k takes field k through the wave's (now free) read-word LDS:
-        // pos (:790), MAPQ, len, n_cig, n_de, D, M, E (two words), one M run of the kept columns
-        uint8_t *sc = lds + rm_addr;
-        if (lane == 0) {
-            *(int4 *)sc = make_int4(minpos + first, mapq, klen, 1);
-            *(int4 *)(sc + 16) = make_int4(T, Dmax, Dmin, E_lo);
-            *(int2 *)(sc + 32) = make_int2(E_hi, (int)((uint32_t)klen << 4));
+        uint32_t v = (uint32_t)(minpos + first);
+        v = lane == 1 ? (uint32_t)mapq : v;
+        v = lane == 2 ? (uint32_t)klen : v;
+        v = lane == 3 ? 1u : v;
+        v = lane == 4 ? (uint32_t)T : v;
+        v = lane == 5 ? (uint32_t)Dmax : v;
+        v = lane == 6 ? (uint32_t)Dmin : v;
+        v = lane == 7 ? E_lo : v;
+        v = lane == 8 ? E_hi : v;
+        v = lane == 9 ? (uint32_t)klen << 4 : v;
+        if (lane < 10) {
+            // destination word of field k (scalar_dest), from the LDS cache
+            const uint64_t pw = *(const uint64_t *)(lds + fk::kPtrs + 8 * lane);
+            const uint64_t idx = lane == 9 ? (uint64_t)off : (uint64_t)rec;
+            *(uint32_t *)((pw & 0x00FFFFFFFFFFFFFFull) + (idx << (pw >> 56))) = v;
+        } else if (lane == 10) {
+            lds_vptr<uint8_t>(lds, fk::kPStatus)[rec] = DCR_ST_OK;
         }
-        lds_fence();
-        const int v = *(const int *)(sc + 4 * min(lane, 9));
-        // one contiguous 48-byte row (fields, then the marker) per record,
-        // scattered into the dcr_out arrays by k_scatter_scalars: ten 4-byte
-        // stores into ten arrays each landed in a line L2 evicted before its
-        // neighbours arrived (write amplification, PMC WRITE_SIZE)
-        (void)O;
-        if (DCR_ABL != 13 && lane < 11) a.rs[rec * 12 + lane] = lane < 10 ? (uint32_t)v : 1u;
     }
     sp.mark(10);                         // [9] record scalars
     return true;
@@ -3052,13 +3099,26 @@ __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
 template <bool DUPLEX, bool EXACT>
 __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[fk::kLdsBytes];
-    // a block none of whose waves has a record leaves before its tables are
-    // built (the EXACT grid is the resident one, its queue mostly short)
-    const int64_t n = EXACT ? *a.xcount : *a.fast_count;
-    const int64_t nw = (int64_t)gridDim.x * fk::kWaves;
+    // Record assignment, XCD-aware: the blocks of one group (blockIdx % 8,
+    // the blocks that share an XCD and its L2) take one contiguous range of
+    // the list, interleaved over the group's waves, so the records in flight
+    // on an XCD at any time are neighbours and the output lines they share
+    // (4-byte record scalars, 160-column regions) fill up in that XCD's L2.
+    // A block none of whose waves has a record leaves before its tables are
+    // built (the EXACT grid is the resident one, its queue mostly short).
+    const int n = EXACT ? *a.xcount : *a.fast_count;
+    int lo, hi, step, first_i;
     {
-        const int64_t b0 = (int64_t)blockIdx.x * fk::kWaves;
-        if (n * b0 / nw == n * (b0 + fk::kWaves) / nw) return;
+        const int nb = (int)gridDim.x, g = (int)(blockIdx.x & 7u);
+        int before = 0;                                      // blocks of the groups before g
+        for (int y = 0; y < g; ++y) before += (nb - y + 7) >> 3;
+        const int mine = (nb - g + 7) >> 3;                  // blocks of group g
+        const int64_t nw = (int64_t)nb * fk::kWaves;
+        lo = (int)((int64_t)n * (before * fk::kWaves) / nw);
+        hi = (int)((int64_t)n * ((before + mine) * fk::kWaves) / nw);
+        step = mine * fk::kWaves;
+        first_i = lo + (int)(blockIdx.x >> 3) * fk::kWaves;  // the block's wave 0
+        if (first_i >= hi) return;
     }
     // EXACT: the likelihood factors of quality rows 0..127 (the exact columns'
     // per-read products read them once per row; the common kernel keeps none)
@@ -3095,16 +3155,24 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
         const int t = threadIdx.x;
         ((uint32_t *)(lds + fk::kM720))[t] = t == 0 || t > 16 ? 0u : 720720u / (uint32_t)t;
     }
-    if (threadIdx.x < 16) {
+    if (threadIdx.x < 24) {
         const int k = threadIdx.x;
         uint64_t v;
         switch (k) {
-        case 10: v = (uint64_t)(uintptr_t)a.norm_cig; break;
-        case 11: v = (uint64_t)(uintptr_t)a.cig_off; break;
-        case 12: v = (uint64_t)(uintptr_t)a.ovf; break;
-        case 13: v = (uint64_t)(uintptr_t)a.ovf_count; break;
-        case 14: v = (uint64_t)(uintptr_t)a.xlist; break;
-        case 15: v = (uint64_t)(uintptr_t)a.xcount; break;
+        case fk::kPNormCig: v = (uint64_t)(uintptr_t)a.norm_cig; break;
+        case fk::kPCigOff: v = (uint64_t)(uintptr_t)a.cig_off; break;
+        case fk::kPOvf: v = (uint64_t)(uintptr_t)a.ovf; break;
+        case fk::kPOvfCount: v = (uint64_t)(uintptr_t)a.ovf_count; break;
+        case fk::kPXlist: v = (uint64_t)(uintptr_t)a.xlist; break;
+        case fk::kPXcount: v = (uint64_t)(uintptr_t)a.xcount; break;
+        case fk::kPD: v = (uint64_t)(uintptr_t)a.O.d; break;
+        case fk::kPE: v = (uint64_t)(uintptr_t)a.O.e; break;
+        case fk::kPSeq: v = (uint64_t)(uintptr_t)a.O.seq; break;
+        case fk::kPQual: v = (uint64_t)(uintptr_t)a.O.qual; break;
+        case fk::kPStatus: v = (uint64_t)(uintptr_t)a.O.status; break;
+        case fk::kPInfo: v = (uint64_t)(uintptr_t)a.info; break;
+        case fk::kPParams: v = (uint64_t)(uintptr_t)a.P; break;
+        case 23: v = 0; break;
         default: v = scalar_dest(a.O, k); break;
         }
         *(uint64_t *)(lds + fk::kPtrs + 8 * k) = v;
@@ -3115,24 +3183,23 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
     const int rm_addr = fk::kRm + wave * kWave * 8;
     const int ov_addr = fk::kOv + wave * 512;
     __syncthreads();
-    const int64_t gw = (int64_t)blockIdx.x * fk::kWaves + wave;
-    int i = (int)(n * gw / nw);
-    const int iend = (int)(n * (gw + 1) / nw);
-    if (i >= iend) return;
+    int i = first_i + wave;
+    if (i >= hi) return;
     const RecMeta *ML = a.meta;
-    const int ilast = iend - 1;
+    auto nxt = [&](int j) { return j + step < hi ? j + step : j; };   // the wave's next record (the last repeats)
     auto midx = [&](int j) { return EXACT ? a.xlist[j] : j; };   // EXACT: the queue holds fast-list indices
+    int i1 = nxt(i), i2 = nxt(i1);
     RecMeta m0 = ML[midx(i)];
-    RecMeta m1 = ML[midx(min(i + 1, ilast))];
+    RecMeta m1 = ML[midx(i1)];
     FastStage st;
-    fast_load<DUPLEX>(a, m0, ML + midx(min(i + 2, ilast)), lane0, st);
+    fast_load<DUPLEX>(a, m0, ML + midx(i2), lane0, st);
     Stamps sp;
     int pend = 0, npend = 0;           // !EXACT: queued fast-list indices (lane p holds the p-th)
     auto flush = [&](int ln) {         // queue pointers from the LDS cache (no scalar registers held)
         int base = 0;
-        if (ln == 0) base = atomicAdd(lds_ptr<int>(lds, 15), npend);
+        if (ln == 0) base = atomicAdd(lds_ptr<int>(lds, fk::kPXcount), npend);
         base = __builtin_amdgcn_readfirstlane(base);
-        if (ln < npend) lds_ptr<int>(lds, 14)[base + ln] = pend;
+        if (ln < npend) lds_ptr<int>(lds, fk::kPXlist)[base + ln] = pend;
         npend = 0;
     };
     for (;;) {
@@ -3151,41 +3218,20 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
         if (lane < 8) *(uint32_t *)(lds + fk::kMv + 32 * wave + 4 * lane) = st.mv;
         sp.mark(2);                    // [1] element codes into LDS
         __builtin_amdgcn_sched_barrier(0);
-        // record i + 1's bytes and record i + 3's descriptor; unconditional (the
-        // last record re-loads itself) so the registers have one definition
-        fast_load<DUPLEX>(a, m1, ML + midx(min(i + 3, ilast)), lane, st);
+        // the next record's bytes and the descriptor of the one after the
+        // next but one; unconditional (the last record re-loads itself) so the
+        // registers have one definition
+        const int i3 = nxt(i2);
+        fast_load<DUPLEX>(a, m1, ML + midx(i3), lane, st);
         sp.mark(3);                    // [2] prefetch issue
         lds_fence();
         const uint2 rw = *(const uint2 *)(lds + rm_addr + 8 * lane);
         // the read's word relative to this record: col | len << 8 | mapq << 16, stage offset
         const uint2 rm = make_uint2((uint32_t)(((int)rw.x >> 16) + (m0.d0 & 0xFFFF)) | (rw.x & 0xFFFFu) << 8,
                                     rw.y - m0.base_al);
-        const RecMeta m2 = meta_from_lanes(*(const uint32_t *)(lds + fk::kMv + 32 * wave + 4 * (lane & 7)));   // record i + 2
-        const Staged sg = trim_record<DUPLEX>(a, m0, rm, bad, lds, stage_addr, lane);
+        const RecMeta m2 = meta_from_lanes(*(const uint32_t *)(lds + fk::kMv + 32 * wave + 4 * (lane & 7)));   // record i2
+        const Staged sg = trim_record<DUPLEX, !EXACT>(a, m0, rm, bad, lds, stage_addr, lane);
         sp.mark(4);                    // [3] trim, fence
-        if (DCR_ABL == 6) {            // diagnostic: 128 extra independent VALU per record (issue-rate probe)
-            int d0 = lane, d1 = lane, d2 = lane, d3 = lane;
-#pragma unroll
-            for (int k = 0; k < 32; ++k)
-                asm volatile("v_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\tv_add_u32 %2, %2, 1\n\tv_add_u32 %3, %3, 1"
-                             : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
-            if ((d0 ^ d1 ^ d2 ^ d3) == 12345) a.O.status[0] = 9;
-        }
-        if (DCR_ABL == 7) {            // diagnostic: 128 extra SALU per record
-            int s0 = i, s1 = i;
-#pragma unroll
-            for (int k = 0; k < 64; ++k) asm volatile("s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 3" : "+s"(s0), "+s"(s1));
-            if ((s0 ^ s1) == 12345) a.O.status[0] = 9;
-        }
-        if (DCR_ABL == 8) {            // diagnostic: 24 extra ds_read_b128 of table rows per record
-            uint4 f[24];
-#pragma unroll
-            for (int k = 0; k < 24; ++k) f[k] = *(const uint4 *)(lds + 16 * ((lane + 7 * k) & 127) + 0x3000 * (k % 5));
-            uint32_t x = 0;
-#pragma unroll
-            for (int k = 0; k < 24; k += 3) x ^= f[k].x ^ f[k + 1].y ^ f[k + 2].z;
-            if (x == 12345u) a.O.status[0] = 9;
-        }
         if (sg.state == 1) {
             send_to_general<DUPLEX>(a, m0, sg.rm, lds, lane);
         } else if (sg.state == 0) {
@@ -3199,474 +3245,15 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
                 if (++npend == kWave) flush(lane);
             }
         }
-        if (++i >= iend) break;
+        i += step;
+        if (i >= hi) break;
         m0 = m1;
         m1 = m2;
+        i2 = i3;
     }
     if (!EXACT && npend) flush(lane0);
     if (DCR_STAMP && lane0 == 0)
         for (int k = 0; k < 10; ++k) atomicAdd(&a.stamps[k + (DUPLEX ? 16 : 0)], (unsigned long long)sp.acc[k]);
-}
-
-// ------------------------------------------------ pair kernel (two records per wave)
-// k_consensus_fast's records of the pair shape (single-strand, R <= 16,
-// T <= 160, <= 1,280 staged bytes, default quality checks): lanes 0-31 take
-// one record and lanes 32-63 the next, each half with its own LDS stage, read
-// words and column words.  The per-column work runs on five 32-column half
-// tiles per record (150 columns: 160 lanes instead of 192), and every
-// per-record step (descriptors, trim, reductions, mean, stores, scalars) is
-// shared by two records.  The arithmetic is k_consensus_fast's: the integer
-// decision over 1/16-nat LLR bounds, d / e / call words, the fixed-point mean
-// (R <= 16).  A record with a column the bound does not decide, a tie in the
-// mean, or R above r_safe goes to the EXACT queue (k_consensus_fast<., true>
-// recomputes it whole); invalid input goes to the general kernel.
-namespace pk {
-constexpr int kWaves = 4;
-constexpr int kBlockThreads = kWave * kWaves;
-constexpr int kNT = kPairMaxT / 32;                        // half tiles per record
-constexpr int kDw = kPairMaxDw / 32;                       // staged dwords per half lane
-constexpr int kStageB = 4 * kPairMaxDw * 2;                // codes of one record: 2,560 B
-constexpr int kZero = fk::kTable;                          // 16 zero bytes: a row that adds nothing
-constexpr int kSent = kZero + 16;                          // u16 fk::kPadCode: a column outside the read
-constexpr int kZSent = kSent + 2;                          // u16 kZero: a read the half's record does not have
-constexpr int kM720 = kSent + 16;                          // u32 [64] 720720 / d for d <= 16
-constexpr int kW0 = kM720 + 256;                           // per-wave regions
-constexpr int kRmO = 2 * kStageB;                          // uint2 [2][16] read words
-constexpr int kCrO = kRmO + 2 * 16 * 8;                    // int [2][16] LDS address of read r's column 0
-constexpr int kOvO = kCrO + 2 * 16 * 4;                    // u16 [2][160] column words d | e << 6 | call << 12
-constexpr int kScO = kOvO + 2 * kPairMaxT * 2;             // [2][48] record scalars
-constexpr int kPW = kScO + 2 * 48;
-constexpr int kLds = kW0 + kWaves * kPW;
-static_assert(kPW % 16 == 0, "16-byte aligned per-wave regions");
-static_assert(4 * kLds <= 160 * 1024, "four blocks per CU");
-}  // namespace pk
-
-// max / min / sum over each half of the wave: DPP inside rows, then the row
-// broadcast that folds row 0 into row 1 and row 2 into row 3 (no row_bcast:31);
-// .x = lanes 0-31, .y = lanes 32-63
-template <class F>
-__device__ __forceinline__ int2 half_reduce(int v, int ident, F op) {
-    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
-    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
-    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
-    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x140, 0xF, 0xF, false));  // row_mirror
-    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
-    return make_int2(__builtin_amdgcn_readlane(v, 31), __builtin_amdgcn_readlane(v, 63));
-}
-__device__ __forceinline__ int2 half_max(int v) {
-    return half_reduce(v, -0x7fffffff - 1, [](int x, int y) { return max(x, y); });
-}
-__device__ __forceinline__ int2 half_min(int v) {
-    return half_reduce(v, 0x7fffffff, [](int x, int y) { return min(x, y); });
-}
-__device__ __forceinline__ int2 half_sum(int v) {
-    return half_reduce(v, 0, [](int x, int y) { return x + y; });
-}
-__device__ __forceinline__ uint32_t half_bits(uint64_t b, int h) { return (uint32_t)(h ? b >> 32 : b); }
-
-// a pair's staged bytes (both halves) and read words, in flight during the
-// previous pair
-struct PairStage {
-    uint32_t vb[pk::kDw], vq[pk::kDw];   // dword 32 u + (lane & 31) of the half's record
-    uint2 rm;                            // read (lane & 31) of the half's record
-};
-
-__device__ __forceinline__ void pair_load(const FastArgs &a, const RecMeta &m, int R, int l, PairStage &st,
-                                          const __amdgpu_buffer_rsrc_t rb, const __amdgpu_buffer_rsrc_t rq,
-                                          int ndw_max) {
-#pragma unroll
-    for (int u = 0; u < pk::kDw; ++u) {
-        if (u * 32 < ndw_max) {
-            const int off = (int)m.base_al + 4 * (32 * u + l);
-            st.vb[u] = __builtin_amdgcn_raw_buffer_load_b32(rb, off, 0, 0);
-            st.vq[u] = __builtin_amdgcn_raw_buffer_load_b32(rq, off, 0, 0);
-        }
-    }
-    st.rm = a.rmeta[m.g0 + min(l, max(R - 1, 0))];
-}
-
-// the per-column state a record's half tiles leave behind
-struct PairCols {
-    uint32_t und;    // bit tt: the lane's live column of half tile tt is not decided
-    uint32_t fx;     // sum over its live columns of e * 720720 / d (the mean's numerator)
-    int dmax, dmin;
-};
-
-// evidence sums and the decision for half tiles [T0, T1) of both records of
-// the pair (k_consensus_fast's arithmetic): column words d | e << 6 | call << 12
-// into the half's LDS column words
-template <int T0, int T1>
-__device__ __forceinline__ void pair_tiles(const FastArgs &a, const uint8_t *lds, bool full, int Rmax, int R, int T,
-                                           int h, int l, int crv, int x0, int ov_h, PairCols &pc) {
-    constexpr int N = T1 - T0;
-    uint64_t llr[N];
-    uint32_t cnt[N];
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-        llr[k] = 0;
-        cnt[k] = 0;
-    }
-    // the LDS address of read r's column 32 T0 + l in this lane's half (lane r of
-    // each half holds its record's column-0 address: no LDS round trip per read)
-    auto addr0 = [&](int r) {
-        const int a0 = readlane(crv, r), a1 = readlane(crv, 32 + r);
-        return (h ? a1 : a0) + 2 * (32 * T0 + l);
-    };
-    auto row = [&](uint32_t code, uint2 &f, uint32_t &c) {   // 8-byte LLR increment, count increment (word 3)
-        const uint4 v = *(const uint4 *)(lds + code);           // one ds_read_b128 (word 2 is 0)
-        f = make_uint2(v.x, v.y);
-        c = v.z + v.w;
-    };
-    if (full) {
-        // two reads per step: the rows of reads r, r + 1 in flight while the codes
-        // of r + 2, r + 3 are read; no 16-bit field reaches 2^16 (16 rows of at
-        // most 1040), so the halves add without carries
-        uint32_t c0[N], c1[N];
-        {
-            const int a0 = addr0(0), a1 = addr0(min(1, Rmax - 1));
-#pragma unroll
-            for (int k = 0; k < N; ++k) {
-                c0[k] = *(const uint16_t *)(lds + a0 + 64 * k);
-                c1[k] = Rmax > 1 ? *(const uint16_t *)(lds + a1 + 64 * k) : (uint32_t)pk::kZero;
-            }
-        }
-        for (int r = 0; r < Rmax; r += 2) {
-            uint2 f0[N], f1[N];
-            uint32_t g0[N], g1[N];
-#pragma unroll
-            for (int k = 0; k < N; ++k) {
-                row(c0[k], f0[k], g0[k]);
-                row(c1[k], f1[k], g1[k]);
-            }
-            const int a0 = addr0(min(r + 2, Rmax - 1)), a1 = addr0(min(r + 3, Rmax - 1));
-            const bool n0 = r + 2 < Rmax, n1 = r + 3 < Rmax;
-#pragma unroll
-            for (int k = 0; k < N; ++k) {
-                c0[k] = n0 ? *(const uint16_t *)(lds + a0 + 64 * k) : (uint32_t)pk::kZero;
-                c1[k] = n1 ? *(const uint16_t *)(lds + a1 + 64 * k) : (uint32_t)pk::kZero;
-            }
-#pragma unroll
-            for (int k = 0; k < N; ++k) {
-                const uint32_t lo = (uint32_t)llr[k] + f0[k].x + f1[k].x;
-                const uint32_t hi = (uint32_t)(llr[k] >> 32) + f0[k].y + f1[k].y;
-                llr[k] = ((uint64_t)hi << 32) | lo;
-                cnt[k] += g0[k] + g1[k];
-            }
-        }
-    } else {
-        // one read per step; columns outside a read load the pad code (class
-        // 'N', :509-510, :543-544), reads the half's record lacks the zero row
-        auto codes = [&](int r, uint32_t (&cd)[N]) {
-            const int c0 = addr0(r) - 2 * (32 * T0 + l);
-            const int xa = readlane(x0, r), xb = readlane(x0, 32 + r);
-            const int x = h ? xb : xa;
-            const int rc = x & 255, rl = (x >> 8) & 255;
-            const int sent = r < R ? pk::kSent : pk::kZSent;
-#pragma unroll
-            for (int k = 0; k < N; ++k) {
-                const int t = 32 * (T0 + k) + l;
-                const int ad = r < R && (uint32_t)(t - rc) < (uint32_t)rl ? c0 + 2 * t : sent;
-                cd[k] = *(const uint16_t *)(lds + ad);
-            }
-        };
-        uint32_t c0[N];
-        codes(0, c0);
-        for (int r = 0; r < Rmax; ++r) {
-            uint2 f0[N];
-            uint32_t g0[N];
-#pragma unroll
-            for (int k = 0; k < N; ++k) row(c0[k], f0[k], g0[k]);
-            uint32_t n0[N];
-            codes(min(r + 1, Rmax - 1), n0);
-#pragma unroll
-            for (int k = 0; k < N; ++k) {
-                llr[k] += ((uint64_t)f0[k].y << 32) | f0[k].x;
-                cnt[k] += g0[k];
-                c0[k] = n0[k];
-            }
-        }
-    }
-    // the decision per column (as k_consensus_fast): call, d, e
-    const bool force = R > a.r_safe;
-    const uint32_t *m720 = (const uint32_t *)(lds + pk::kM720);
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-        const int t = 32 * (T0 + k) + l;
-        const bool live = t < T;
-        const uint32_t lo = (uint32_t)llr[k], hi = (uint32_t)(llr[k] >> 32);
-        const u16x2 P1 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi, lo, 0x05040100u));
-        const u16x2 P2 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi, lo, 0x07060302u));
-        const u16x2 Mx = __builtin_elementwise_max(P1, P2), Mn = __builtin_elementwise_min(P1, P2);
-        const uint32_t Lb = max((uint32_t)Mx.x, (uint32_t)Mx.y);
-        const uint32_t L2 = max(min((uint32_t)Mx.x, (uint32_t)Mx.y), max((uint32_t)Mn.x, (uint32_t)Mn.y));
-        uint32_t kb = (uint32_t)P1.y == Lb ? 2u : 3u;                        // the first largest ("ATCG")
-        kb = (uint32_t)P2.x == Lb ? 1u : kb;
-        kb = (uint32_t)P1.x == Lb ? 0u : kb;
-        const uint32_t cn = cnt[k];
-        const int d = R - (int)(cn & 63u);                                  // rows that are not 'N'
-        const int nb = (int)__builtin_amdgcn_ubfe(cn, 6u * kb + 6u, 6u);
-        const int e = R - nb;                                               // rows that differ from the call
-        const bool undecided = (int)(Lb - L2) - (d - nb) < a.t16 || force;
-        pc.und |= (uint32_t)(live && undecided) << (T0 + k);
-        *(uint16_t *)(lds + ov_h + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (kb << 12));
-        pc.fx += live ? __umul24((uint32_t)e, m720[max(d, 0)]) : 0u;
-        pc.dmax = max(pc.dmax, live ? d : -1);
-        pc.dmin = min(pc.dmin, live ? d : 0x7fffffff);
-    }
-}
-
-__global__ __launch_bounds__(pk::kBlockThreads, 3) void k_consensus_pair(FastArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[pk::kLds];
-    for (int i = threadIdx.x; i < 5 * (fk::kRowMax + 1); i += pk::kBlockThreads) {
-        const int k = i / (fk::kRowMax + 1), q = i % (fk::kRowMax + 1);
-        const bool nrow = k == 0 || q < a.minbq;          // 'N', or masked below min_base_quality (:280)
-        const uint64_t inc = nrow ? 0ull : (uint64_t)a.llr16[q] << (16 * (k - 1));
-        // the count increment in the row's last word (x, y, w: one ds_read_b128, not a b96)
-        *(uint4 *)(lds + 0x800 * k + 16 * (q + k)) = make_uint4((uint32_t)inc, (uint32_t)(inc >> 32), 0u, nrow ? 1u : 1u << (6 * k));
-    }
-    if (threadIdx.x < 4) ((uint32_t *)(lds + pk::kZero))[threadIdx.x] = 0u;
-    if (threadIdx.x == 0) {
-        *(uint16_t *)(lds + pk::kSent) = (uint16_t)fk::kPadCode;
-        *(uint16_t *)(lds + pk::kZSent) = (uint16_t)pk::kZero;
-    }
-    if (threadIdx.x < 64) {
-        const int t = threadIdx.x;
-        ((uint32_t *)(lds + pk::kM720))[t] = t == 0 || t > 16 ? 0u : 720720u / (uint32_t)t;
-    }
-    __syncthreads();
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int h = lane >> 5, l = lane & 31;
-    const int W = pk::kW0 + wave * pk::kPW;
-    const int stage_h = W + h * pk::kStageB;              // this half's stage
-    const int rm_h = W + pk::kRmO + h * 128;
-    const int cr_h = W + pk::kCrO + h * 64;
-    const int ov_h = W + pk::kOvO + h * (2 * kPairMaxT);
-    const int sc_h = W + pk::kScO + h * 48;
-
-    const int64_t np = *a.pair_count;                    // records in the pair list
-    const int64_t npairs = (np + 1) >> 1;
-    const int64_t nw = (int64_t)gridDim.x * pk::kWaves;
-    const int64_t gw = (int64_t)blockIdx.x * pk::kWaves + wave;
-    int64_t p = npairs * gw / nw;
-    const int64_t pend = npairs * (gw + 1) / nw;
-    if (p >= pend) return;
-    const RecMeta *ML = a.meta;
-    // record k of the list (k < np) and an empty stand-in past its end
-    auto meta_of = [&](int64_t k, RecMeta &m, int &R) {
-        if (k < np) {
-            m = ML[a.pair_top - k];
-            R = (int)(m.w & 127u);
-        } else {
-            m = ML[a.pair_top - (np - 1)];                 // any valid descriptor; R = 0 marks the half empty
-            R = 0;
-        }
-    };
-    const int64_t lim = ((a.nbytes + 3) & ~(int64_t)3);
-    const int nrec = (int)min(lim, (int64_t)0x7FFFFFF0);
-    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void *)a.gb, (short)0, nrec, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void *)a.gq, (short)0, nrec, 0x00020000);
-
-    RecMeta M0, M1;
-    int R0, R1;
-    meta_of(2 * p, M0, R0);
-    meta_of(2 * p + 1, M1, R1);
-    PairStage st;
-    {
-        const RecMeta &m = h ? M1 : M0;
-        pair_load(a, m, h ? R1 : R0, l, st, rb, rq, max((int)(M0.w >> 15), (int)(M1.w >> 15)));
-    }
-    for (;;) {
-        // ---- this pair's descriptors (wave-uniform) and the half's view
-        const RecMeta A0 = M0, A1 = M1;
-        const int AR0 = R0, AR1 = R1;
-        const int R = h ? AR1 : AR0;                        // this lane's record
-        const int ndw = (int)((h ? A1.w : A0.w) >> 15);
-        const uint32_t base_al = h ? A1.base_al : A0.base_al;
-        const int d0 = h ? A1.d0 : A0.d0;
-        // ---- element codes of the staged bytes into the half's stage
-        uint32_t bad = 0;
-#pragma unroll
-        for (int u = 0; u < pk::kDw; ++u) {
-            if (u * 32 < max((int)(A0.w >> 15), (int)(A1.w >> 15))) {
-                if (32 * u + l < ndw) {
-                    const uint2 c = make_codes4<false, false>(st.vb[u], st.vq[u], a.kq, a.kqlo, bad);
-                    *(uint2 *)(lds + stage_h + 8 * (32 * u + l)) = c;
-                }
-            }
-        }
-        *(uint2 *)(lds + rm_h + 8 * l) = l < 16 ? st.rm : make_uint2(0u, 0u);
-        // the next pair's descriptors and bytes, in flight during this pair
-        const bool more = p + 1 < pend;
-        if (more) {
-            meta_of(2 * (p + 1), M0, R0);
-            meta_of(2 * (p + 1) + 1, M1, R1);
-        }
-        {
-            __builtin_amdgcn_sched_barrier(0);
-            const RecMeta &m = h ? M1 : M0;
-            pair_load(a, m, h ? R1 : R0, l, st, rb, rq, max((int)(M0.w >> 15), (int)(M1.w >> 15)));
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        lds_fence();
-        const uint2 rw = *(const uint2 *)(lds + rm_h + 8 * l);
-        // the read's word relative to this record: col | len << 8, stage offset
-        const int col = (int)(((int)rw.x >> 16) + (d0 & 0xFFFF));
-        const int y = (int)(rw.y - base_al);
-        const bool rd = l < R;                              // lane = read of the half's record
-        int T = (int)(((h ? A1.w : A0.w) >> 7) & 255u);
-        int state = R > 0 ? 0 : 2;                          // 0 consensus here, 1 general, 2 finished, 3 exact queue
-        // ---- trim_3prime_N (:292-325): trailing 'N' rows (sequenced, or masked, :280)
-        int tl = rd ? (int)(rw.x & 255u) : 0;
-        {
-            bool go = tl > 0;
-            while (__ballot(go)) {
-                if (go) {
-                    const uint32_t code = *(const uint16_t *)(lds + stage_h + 2 * (y + tl - 1));
-                    if (*(const uint32_t *)(lds + code + 12) & 63u) --tl; else go = false;
-                    go = go && tl > 0;
-                }
-            }
-        }
-        const int64_t g0 = h ? A1.g0 : A0.g0;
-        if (rd && (a.want_info || tl == 0)) {
-            dcr_read_info inf;
-            inf.seq_start = (int64_t)base_al + y;
-            inf.len = tl;
-            inf.n_cig = tl > 0 ? 1 : 0;
-            inf.status = tl > 0 ? DCR_ST_OK : DCR_ST_INDEX_ERROR;   // compress_cigarlist([]) :740 via :322
-            inf.has_ins = 0;
-            a.info[g0 + l] = inf;
-        }
-        {
-            // T shrinks only when every read reaching the untrimmed end lost its tail
-            const uint32_t reach = half_bits(__ballot(rd && col + tl == T), h);
-            const int2 tm = half_max(rd ? col + tl : 0);
-            if (reach == 0) T = h ? tm.y : tm.x;
-            if (half_bits(__ballot(rd && tl == 0), h) != 0 && state == 0) {
-                if (l == 0) write_status_at(a.O, h ? A1.rec : A0.rec, DCR_ST_PREP | DCR_ST_INDEX_ERROR);
-                state = 2;
-            }
-            if (state == 0 && half_bits(__ballot(bad != 0), h) != 0) state = 1;
-        }
-        // the general kernel takes a record with invalid input (it reads the
-        // preprocessed reads: read info, one normalised M run)
-        if (state == 1) {
-            if (!a.want_info && rd) {
-                dcr_read_info inf;
-                inf.seq_start = (int64_t)base_al + y;
-                inf.len = tl;
-                inf.n_cig = tl > 0 ? 1 : 0;
-                inf.status = tl > 0 ? DCR_ST_OK : DCR_ST_INDEX_ERROR;
-                inf.has_ins = 0;
-                a.info[g0 + l] = inf;
-            }
-            if (rd && tl > 0) a.norm_cig[a.cig_off[g0 + l]] = (uint32_t)tl << 4;
-            if (l == 0) {
-                const int idx = atomicAdd(a.ovf_count, 1);
-                a.ovf[idx] = h ? A1.rec : A0.rec;
-            }
-        }
-        // read words for the column pass: LDS address of column 0, col | len << 8
-        if (rd) {
-            *(int *)(lds + cr_h + 4 * l) = stage_h + 2 * (y - col);
-            *(uint32_t *)(lds + rm_h + 8 * l) = (uint32_t)col | ((uint32_t)tl << 8);
-        }
-        lds_fence();
-        const uint64_t live_any = __ballot(state == 0);
-        if (live_any) {
-            // ---- evidence sums and the decision, lane = column t = 32 tt + l of
-            // the half's record, in two groups of half tiles (fewer rows in flight)
-            const int Rmax = max(AR0, AR1);
-            // every read of both records covers every column, and both have R reads
-            const bool full = AR0 == AR1 && __ballot(rd && (col != 0 || tl != T)) == 0;
-            const int crv = stage_h + 2 * (y - col);       // lane r of each half: read r's column 0
-            const int x0 = (int)((uint32_t)col | ((uint32_t)tl << 8));   // lane r: col | len << 8
-            PairCols pc;
-            pc.und = 0;
-            pc.fx = 0;
-            pc.dmax = -1;
-            pc.dmin = 0x7fffffff;
-            pair_tiles<0, 3>(a, lds, full, Rmax, R, T, h, l, crv, x0, ov_h, pc);
-            pair_tiles<3, pk::kNT>(a, lds, full, Rmax, R, T, h, l, crv, x0, ov_h, pc);
-            const uint32_t und = pc.und, fx = pc.fx;
-            const int dmax = pc.dmax, dmin = pc.dmin;
-            // ---- E = round(mean(e/d), 3) (:1015-1018), exactly: 25 fx / (18018 T)
-            const int2 S2 = half_sum((int)fx);
-            const int2 Dx = half_max(dmax), Dn = half_min(dmin);
-            const int2 Tp = make_int2(readlane(T, 0), readlane(T, 32));
-            double E2[2];
-            bool slow2[2];
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const uint32_t S = (uint32_t)(k ? S2.y : S2.x);
-                const int Tk = k ? Tp.y : Tp.x;
-                const int64_t num = 25 * (int64_t)S;
-                const int den = 18018 * max(Tk, 1);
-                const double dn = (double)den;
-                double rc = __builtin_amdgcn_rcp(dn);
-                rc = __builtin_fma(__builtin_fma(-dn, rc, 1.0), rc, rc);
-                const int kk = __builtin_amdgcn_readfirstlane((int)__builtin_rint((double)num * rc));
-                const int64_t rr = num - (int64_t)kk * den;
-                slow2[k] = 2 * (rr < 0 ? -rr : rr) >= den || kk > 1000 || kk < 0;   // a tie (or a bad estimate)
-                E2[k] = div1000(kk);
-            }
-            const bool slow = h ? slow2[1] : slow2[0];
-            // ---- an undecided column or a tie: the record goes to the exact pass
-            if (state == 0 && (half_bits(__ballot(und != 0), h) != 0 || slow)) {
-                if (l == 0) {
-                    const int idx = atomicAdd(a.xcount, 1);
-                    a.xlist[idx] = (int)(a.pair_top - (2 * p + h));
-                }
-                state = 3;
-            }
-            lds_fence();
-            // ---- d / e / seq / qual, eight columns per lane (one 16-, 16-, 8- and 8-byte store)
-            const int T16 = ((int)(((h ? A1.w : A0.w) >> 7) & 255u) + 15) & ~15;
-            const int64_t off = h ? A1.off : A0.off;
-            const int cb = 8 * l;
-            if (state == 0 && cb < T16) {
-                const uint4 w = *(const uint4 *)(lds + ov_h + 16 * l);
-                *(uint4 *)(a.O.d + off + cb) =
-                    make_uint4(w.x & 0x003F003Fu, w.y & 0x003F003Fu, w.z & 0x003F003Fu, w.w & 0x003F003Fu);
-                *(uint4 *)(a.O.e + off + cb) = make_uint4((w.x >> 6) & 0x003F003Fu, (w.y >> 6) & 0x003F003Fu,
-                                                          (w.z >> 6) & 0x003F003Fu, (w.w >> 6) & 0x003F003Fu);
-                auto letters4 = [](uint32_t u, uint32_t v) {
-                    const uint32_t sel = ((u >> 12) & 3u) | ((u >> 20) & 0x300u) | ((v << 4) & 0x30000u) |
-                                         ((v >> 4) & 0x3000000u);
-                    return __builtin_amdgcn_perm(0u, 0x47435441u, sel);        // "ATCG"[call]
-                };
-                const int nl0 = min(max(T - cb, 0), 4), nl1 = min(max(T - cb - 4, 0), 4);
-                const uint32_t k0 = nl0 == 4 ? 0xFFFFFFFFu : (1u << (8 * nl0)) - 1u;
-                const uint32_t k1 = nl1 == 4 ? 0xFFFFFFFFu : (1u << (8 * nl1)) - 1u;
-                const uint32_t q4 = (uint32_t)a.maxq * 0x01010101u;
-                *(uint2 *)(a.O.seq + off + cb) = make_uint2((letters4(w.x, w.y) & k0) | (0x4E4E4E4Eu & ~k0),
-                                                            (letters4(w.z, w.w) & k1) | (0x4E4E4E4Eu & ~k1));
-                *(uint2 *)(a.O.qual + off + cb) = make_uint2(q4 & k0, q4 & k1);
-            }
-            // ---- the record's scalar row (k_scatter_scalars): pos (:790), MAPQ,
-            // len, n_cig, n_de, D, M, E, one M run of the kept columns, marker
-            if (state == 0) {
-                const double E = h ? E2[1] : E2[0];
-                const int minpos = h ? A1.minpos : A0.minpos;
-                if (l == 0) {
-                    *(int4 *)(lds + sc_h) = make_int4(minpos, (int)((uint32_t)d0 >> 16), T, 1);
-                    *(int4 *)(lds + sc_h + 16) = make_int4(T, h ? Dx.y : Dx.x, h ? Dn.y : Dn.x,
-                                                           (int)(uint32_t)__double_as_longlong(E));
-                    *(int2 *)(lds + sc_h + 32) =
-                        make_int2((int)(uint32_t)((uint64_t)__double_as_longlong(E) >> 32), (int)((uint32_t)T << 4));
-                }
-            }
-            lds_fence();
-            if (state == 0 && l < 11) {
-                const int v = *(const int *)(lds + sc_h + 4 * min(l, 9));
-                const int64_t rec = h ? A1.rec : A0.rec;
-                a.rs[rec * 12 + l] = l < 10 ? (uint32_t)v : 1u;
-            }
-        }
-        if (!more) break;
-        ++p;
-    }
 }
 
 // persistent: drains the general list written by k_recmeta.  A wave takes
@@ -3697,43 +3284,6 @@ __global__ __launch_bounds__(kBlock, DCR_GEN_OCC) void k_consensus_general(Args 
     const int lane = threadIdx.x & 63;
     const int n = a.ws.ovf_count[DUPLEX ? 1 : 0];
     int *next = a.ws.gen_next + (DUPLEX ? 1 : 0);
-#if defined(DCR_GEN_VARIANT) && DCR_GEN_VARIANT == 1     // diagnostic: claim, at most one record per wave
-    {
-        int i = 0;
-        if (lane == 0) i = atomicAdd(next, 1);
-        i = __builtin_amdgcn_readfirstlane(__shfl(i, 0, kWave));
-        if (i < n) {
-            const int v = a.ws.ovf[i];
-            process_record<DUPLEX, false>(a, v & 0x7fffffff, s_wave[wave], s_lut, s_qthr, s_wtab, v < 0, lane);
-        }
-        return;
-    }
-#endif
-#if defined(DCR_GEN_VARIANT) && DCR_GEN_VARIANT == 2     // diagnostic: static stride, reversed order
-    for (int k = blockIdx.x * kWavesPerBlock + wave; k < n; k += gridDim.x * kWavesPerBlock) {
-        const int v = a.ws.ovf[n - 1 - k];
-        process_record<DUPLEX, false>(a, v & 0x7fffffff, s_wave[wave], s_lut, s_qthr, s_wtab, v < 0, lane);
-    }
-    (void)next;
-    return;
-#endif
-#if defined(DCR_GEN_VARIANT) && DCR_GEN_VARIANT == 3     // diagnostic: static stride over block 0's waves only
-    if (blockIdx.x == 0)
-        for (int k = wave; k < n; k += kWavesPerBlock) {
-            const int v = a.ws.ovf[k];
-            process_record<DUPLEX, false>(a, v & 0x7fffffff, s_wave[wave], s_lut, s_qthr, s_wtab, v < 0, lane);
-        }
-    (void)next;
-    return;
-#endif
-#ifdef DCR_GEN_STATIC     // diagnostic (tools/ablate.py): the round-1 static stride
-    for (int i = blockIdx.x * kWavesPerBlock + wave; i < n; i += gridDim.x * kWavesPerBlock) {
-        const int v = a.ws.ovf[i];
-        process_record<DUPLEX, false>(a, v & 0x7fffffff, s_wave[wave], s_lut, s_qthr, s_wtab, v < 0, lane);
-    }
-    (void)next;
-    return;
-#endif
     // the first record of each wave by position (no atomic on the way in: most
     // general lists are shorter than the grid), then claims past the grid
     // (one record per claim: claiming 4 or 8 at a time measured slower on C3,
@@ -3902,29 +3452,6 @@ __global__ __launch_bounds__(kDeepWaves * kWave, 2 * kDeepWaves / 4) void k_deci
     }
     if (DCR_STAMP && lane == 0)
         for (int q = 0; q < 3; ++q) atomicAdd(&a.ws.stamps[26 + q], (unsigned long long)st_acc[q]);
-}
-
-// the fast kernels' record scalars (finish_record, one 48-byte row per
-// record, marker [10]) into the dcr_out arrays; rows are cleared for the next
-// strand / batch.  Thread = record: every store is coalesced.
-__global__ __launch_bounds__(256) void k_scatter_scalars(ScatterArgs S) {
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < S.n_rec; r += (int64_t)gridDim.x * blockDim.x) {
-        const uint4 *row = (const uint4 *)(S.rs + 12 * r);
-        const uint4 c = row[2];
-        if (c.z != 1u) continue;
-        const uint4 a = row[0], b = row[1];
-        S.O.pos[r] = (int32_t)a.x;
-        S.O.mapq[r] = (int32_t)a.y;
-        S.O.len[r] = (int32_t)a.z;
-        S.O.n_cig[r] = (int32_t)a.w;
-        S.O.n_de[r] = (int32_t)b.x;
-        S.O.D[r] = (int32_t)b.y;
-        S.O.M[r] = (int32_t)b.z;
-        ((uint2 *)S.O.E)[r] = make_uint2(b.w, c.x);
-        S.O.cigar[S.col_off[r]] = c.y;
-        S.O.status[r] = DCR_ST_OK;
-        ((uint4 *)(S.rs_clear + 12 * r))[2] = make_uint4(0u, 0u, 0u, 0u);
-    }
 }
 
 template __global__ void k_recmeta<false>(Args);

@@ -288,7 +288,12 @@ class BgzfWriter:
         self._h = lib.dcr_bgzw_open(os.fsencode(path), level, n_threads)
         if not self._h:
             raise _err(f"cannot write {path}")
-        self.write(header)
+        try:
+            self.write(header)
+        except BaseException:
+            lib.dcr_bgzw_close(self._h)
+            self._h = None
+            raise
 
     def write(self, data):
         if isinstance(data, np.ndarray):

@@ -166,14 +166,14 @@ int dcr_sync(dcr_ctx *ctx);
    complete only with DCR_OPT_READ_INFO */
 int dcr_read_info_host(dcr_ctx *ctx, dcr_read_info *out, int64_t n_reads);
 /* timing of the last dcr_run_batch (HIP events on the context stream), ms:
-   [0] prep, [1] single-strand, [2] duplex, [3] whole batch */
+   [0] prep (always 0: fused into the consensus kernels), [1] single-strand,
+   [2] duplex, [3] whole batch */
 int dcr_last_timing(dcr_ctx *ctx, float *ms4);
 /* per-kernel timing of the last dcr_run_batch (HIP events between launches on
-   the context stream), ms: k_prep, then per strand (single-strand, duplex)
-   k_recmeta, k_consensus_fast, k_consensus_fast (exact queue),
-   k_consensus_general */
-#define DCR_N_KERNEL_TIMES 9
-int dcr_last_kernel_timing(dcr_ctx *ctx, float *ms9);
+   the context stream), ms: per strand (single-strand, duplex) k_recmeta,
+   k_consensus_fast, k_consensus_fast (exact queue), k_consensus_general */
+#define DCR_N_KERNEL_TIMES 8
+int dcr_last_kernel_timing(dcr_ctx *ctx, float *ms8);
 
 /* Streaming: a context has DCR_MAX_SLOTS slots of device buffers.
  * dcr_submit copies a host batch (pinned memory, dcr_host_alloc) into the

@@ -178,8 +178,9 @@ def test_ingest_rejects_non_bam(tmp_path):
 
 
 def test_bgzf_writer_rewrites_a_longer_file(tmp_path):
-    """The writer opens without truncation and cuts the file at close: a
-    rewrite over a longer file of the same name gives the bytes of a fresh one."""
+    """A rewrite over a longer file of the same name gives the bytes of a
+    fresh one; a writer dropped before close leaves no stale tail (the file
+    is truncated at open, so no old BGZF EOF marker survives)."""
     import gzip
     small, big = b"BAM\x01" + bytes(range(256)) * 4, os.urandom(3 << 20)
     fresh, reused = tmp_path / "fresh.bam", tmp_path / "reused.bam"
@@ -191,3 +192,30 @@ def test_bgzf_writer_rewrites_a_longer_file(tmp_path):
         w.close()
     assert reused.read_bytes() == fresh.read_bytes()
     assert gzip.decompress(reused.read_bytes()) == small
+    # dropped before close over the longer file: nothing of the old file left
+    w = native_io.BgzfWriter(str(reused), big, 1, 2)
+    w.close()
+    w = native_io.BgzfWriter(str(reused), small, 1, 2)
+    assert reused.stat().st_size < 1 << 20
+    assert not reused.read_bytes().endswith(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"))
+    w.close()
+
+
+def test_bgzf_writer_non_regular_outputs(tmp_path):
+    """Outputs that are not regular files: a symlink to /dev/null and a FIFO."""
+    import gzip
+    import threading
+    data = b"BAM\x01" + os.urandom(1 << 18)
+    link = tmp_path / "null.bam"
+    os.symlink("/dev/null", link)
+    w = native_io.BgzfWriter(str(link), data, 6, 2)
+    w.close()
+    fifo = tmp_path / "pipe.bam"
+    os.mkfifo(fifo)
+    got = []
+    th = threading.Thread(target=lambda: got.append(open(fifo, "rb").read()))
+    th.start()
+    w = native_io.BgzfWriter(str(fifo), data, 6, 2)
+    w.close()
+    th.join(30)
+    assert gzip.decompress(got[0]) == data
