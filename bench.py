@@ -208,6 +208,9 @@ def e2e_passes(path, params_args, device, steps, warmup, workdir):
     # passes reuse them, as a long-running converter would
     dt = 0.0
     passes = []
+    infl = cli._INFLATERS.get(device)
+    if infl is not None:
+        infl[0].totals(reset=True)
     for i in range(steps):
         argv = argv_of(warmup + i)
         stats = {"trace": []}
@@ -222,6 +225,13 @@ def e2e_passes(path, params_args, device, steps, warmup, workdir):
         " ".join(f"{k}[{(a - t_pass) * 1e3:.0f},{(b - t_pass) * 1e3:.0f}]" for k, a, b in trace))
     stats["first_pass_s"] = cold        # the cold first pass (allocations included)
     stats["passes_s"] = passes
+    if infl is not None:                # BGZF inflate on the device (cli.gpu_inflate)
+        t = infl[0].totals()
+        stats["gpu_inflate"] = {"kernel_ms_per_pass": t["kernel_ms"] / max(steps, 1),
+                                "launches_per_pass": t["runs"] / max(steps, 1),
+                                "GBps_of_output_in_kernel": (t["bytes"] / (t["kernel_ms"] * 1e6)) if t["kernel_ms"] else None}
+    else:
+        stats["gpu_inflate"] = None
     return dt, stats
 
 
@@ -394,6 +404,7 @@ def main():
             value, ms_step = e2e_bases / slowest, slowest * 1e3 / args.steps
             value_kind = "whole node: CLI from BAM open to output close"
         stage = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in stats.items() if k.endswith("_s")}
+        stage["gpu_inflate"] = stats.get("gpu_inflate")
         res = {
             "metric": METRIC, "value": value, "unit": "consensus bases/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,

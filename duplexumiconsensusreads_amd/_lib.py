@@ -43,6 +43,14 @@ EXPORTS = {
     "dcr_wait_write": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "dcr_slot_fetch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
                                       ctypes.c_void_p]),
+    # include/dcr_inflate.h: BGZF inflate on the device
+    "dcr_inflater_create": (ctypes.c_void_p, [ctypes.c_int]),
+    "dcr_inflater_destroy": (None, [ctypes.c_void_p]),
+    "dcr_inflater_hook": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "dcr_inflater_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                        ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64]),
+    "dcr_inflater_last": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "dcr_inflater_totals": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
 }
 
 # HIP-event slots of dcr_last_kernel_timing: k_recmeta<ss> includes k_prep_big,
@@ -166,6 +174,96 @@ class Context:
         ms = (ctypes.c_float * len(KERNELS))()
         _check(load().dcr_last_kernel_timing(self._ctx, ms))
         return dict(zip(KERNELS, ms))
+
+
+# include/dcr_inflate.h dcr_bgzf_member (32 bytes)
+BGZF_MEMBER_DTYPE = np.dtype([("in_off", "<i8"), ("out_off", "<i8"), ("in_len", "<u4"), ("isize", "<u4"),
+                              ("crc", "<u4"), ("pad", "<u4")])
+
+
+class InflateHook(ctypes.Structure):
+    """include/dcr_inflate.h dcr_inflate_hook (filled by dcr_inflater_hook)."""
+    _fields_ = [("user", ctypes.c_void_p), ("run", ctypes.c_void_p), ("host_alloc", ctypes.c_void_p),
+                ("host_free", ctypes.c_void_p)]
+
+
+def bgzf_members(data) -> tuple:
+    """(members, output bytes) of a buffer of whole BGZF blocks: the layout
+    dcr_inflater_run takes (the ingest builds the same table natively)."""
+    buf = memoryview(data)
+    out, p, o = [], 0, 0
+    while p < len(buf):
+        if bytes(buf[p:p + 4]) != b"\x1f\x8b\x08\x04":
+            raise ValueError(f"not a BGZF block at {p}")
+        xlen = int.from_bytes(buf[p + 10:p + 12], "little")
+        bsize, q = None, p + 12
+        while q + 4 <= p + 12 + xlen:
+            slen = int.from_bytes(buf[q + 2:q + 4], "little")
+            if bytes(buf[q:q + 2]) == b"BC" and slen == 2:
+                bsize = int.from_bytes(buf[q + 4:q + 6], "little") + 1
+            q += 4 + slen
+        if bsize is None:
+            raise ValueError("BGZF block without BC field")
+        crc = int.from_bytes(buf[p + bsize - 8:p + bsize - 4], "little")
+        isize = int.from_bytes(buf[p + bsize - 4:p + bsize], "little")
+        out.append((p + 12 + xlen, o, bsize - 12 - xlen - 8, isize, crc, 0))
+        o += isize
+        p += bsize
+    return np.array(out, dtype=BGZF_MEMBER_DTYPE), o
+
+
+class Inflater:
+    """A device BGZF inflater (``dcr_inflater``, include/dcr_inflate.h)."""
+
+    def __init__(self, device: int = 0):
+        lib = load()
+        self.device = device
+        self._h = lib.dcr_inflater_create(device)
+        if not self._h:
+            raise DcrError(f"dcr_inflater_create failed: {lib.dcr_last_error().decode()}")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def hook(self) -> InflateHook:
+        h = InflateHook()
+        _check(load().dcr_inflater_hook(self._h, ctypes.byref(h)))
+        return h
+
+    def run(self, data, members, out_bytes):
+        """Inflate ``members`` of ``data`` (bytes / uint8 array): returns
+        (0 or the index + 1 of the first failing member, output array)."""
+        src = np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray) else data
+        m = np.ascontiguousarray(members, dtype=BGZF_MEMBER_DTYPE)
+        out = np.zeros(max(out_bytes, 1), np.uint8)
+        rc = load().dcr_inflater_run(self._h, src.ctypes.data, src.nbytes, m.ctypes.data, len(m), out.ctypes.data,
+                                     out_bytes)
+        if rc < 0:
+            raise DcrError(f"dcr_inflater_run: {load().dcr_last_error().decode()}")
+        return rc, out[:out_bytes]
+
+    def last(self):
+        ms, n = ctypes.c_float(), ctypes.c_int32()
+        _check(load().dcr_inflater_last(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def totals(self, reset=False):
+        """Kernel ms, runs, members and output bytes since creation / the last reset."""
+        out = (ctypes.c_double * 4)()
+        _check(load().dcr_inflater_totals(self._h, out, int(reset)))
+        return {"kernel_ms": out[0], "runs": int(out[1]), "members": int(out[2]), "bytes": int(out[3])}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load().dcr_inflater_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def backend(ctx: Context):

@@ -179,6 +179,35 @@ def _close_backends():
     for be in _BACKENDS.values():
         be.close(final=True)
     _BACKENDS.clear()
+    if _INFLATERS:
+        native_io.set_inflate_hook(None)
+        for inf, _ in _INFLATERS.values():
+            inf.close()
+        _INFLATERS.clear()
+
+
+_INFLATERS = {}       # device -> (_lib.Inflater, its hook), kept for later runs in this process
+
+
+def gpu_inflate(device: int = 0):
+    """BGZF inflate on ``device`` for the ingests this process opens from now
+    on (include/dcr_inflate.h; the native ingest hands each chunk's members to
+    the device inflater and takes its chunk buffers page-locked from it).
+    One inflater per process and device, kept like the backend.
+    DCR_GPU_INFLATE=0 keeps the host pool (A/B runs)."""
+    if os.environ.get("DCR_GPU_INFLATE") == "0":
+        return None
+    got = _INFLATERS.get(device)
+    if got is None:
+        from . import _lib
+        inf = _lib.Inflater(device)
+        got = (inf, inf.hook())
+        _INFLATERS[device] = got
+        if len(_INFLATERS) == 1 and not _BACKENDS:
+            import atexit
+            atexit.register(_close_backends)
+    native_io.set_inflate_hook(got[1])
+    return got[0]
 
 
 def _as_backend(backend, params, device=0):
@@ -454,6 +483,8 @@ def main(argv: Optional[list] = None, backend=None, rng=random, stats: Optional[
         return _main_sharded(args, params, backend, rng, stats, group)
     if args.gpus > 1:
         return _launch_ranks(argv, args.gpus)
+    if backend is None:
+        gpu_inflate(args.device)       # the GPU path reads its input through the device inflater too
     try:
         ing = native_io.Ingest(args.input_file, params.min_map_quality, params.min_reads, params.max_reads,
                                params.min_base_quality, args.threads)
@@ -641,6 +672,8 @@ def _run_range(args, params, backend, path, rng, rng_state, rng_range, parts, de
     res = {"status": "ok", "exc_args": (), "calls": [], "counters": None, "stdout": "", "stats": {},
            "sizes": [0, 0, 0]}
     out = io.StringIO()
+    if backend is None:
+        gpu_inflate(device)
     ing = native_io.Ingest(path, params.min_map_quality, params.min_reads, params.max_reads,
                            params.min_base_quality, args.threads, rng_range[0], rng_range[1])
     be = _as_backend(backend, params, device)

@@ -56,6 +56,8 @@ struct DevBuf {
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 }  // namespace
 
+int dcr::set_error(int code, const std::string &msg) { return fail(code, msg); }
+
 struct dcr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;

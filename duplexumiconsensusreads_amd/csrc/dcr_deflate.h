@@ -153,21 +153,20 @@ DFL_HD inline uint32_t crc_byte(uint32_t c) {
 }
 DFL_HD inline uint32_t multmodp(uint32_t a, uint32_t b) {
     uint32_t m = 1u << 31, p = 0;
-    for (;;) {
+    for (; m; m >>= 1) {          // a = 0 (never passed) ends after 32 steps
         if (a & m) {
             p ^= b;
             if ((a & (m - 1)) == 0) break;
         }
-        m >>= 1;
         b = (b & 1) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
     }
     return p;
 }
-// x^(8 * 2^k) mod P, k = 0..15 (reflected), by repeated squaring of x^8
-DFL_CONST uint32_t kX8Pow2[16] = {0x00800000u, 0x00008000u, 0xedb88320u, 0xb1e6b092u, 0xa06a2517u, 0xed627daeu,
+// x^(8 * 2^k) mod P, k = 0..16 (reflected), by repeated squaring of x^8
+DFL_CONST uint32_t kX8Pow2[17] = {0x00800000u, 0x00008000u, 0xedb88320u, 0xb1e6b092u, 0xa06a2517u, 0xed627daeu,
                                   0x88d14467u, 0xd7bbfe6au, 0xec447f11u, 0x8e7ea170u, 0x6427800eu, 0x4d47bae0u,
-                                  0x09fe548fu, 0x83852d0fu, 0x30362f1au, 0x7b5a9cc3u};
-// x^(8n) mod P (n < 65536): the register shift of n zero bytes
+                                  0x09fe548fu, 0x83852d0fu, 0x30362f1au, 0x7b5a9cc3u, 0x31fec169u};
+// x^(8n) mod P (n <= 65536, a BGZF member's ISIZE at most): the register shift of n zero bytes
 DFL_HD inline uint32_t x8nmodp(uint32_t n) {
     uint32_t p = 1u << 31;         // 1
     for (int k = 0; n; ++k, n >>= 1)

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "../../include/dcr_io.h"
+#include "../../include/dcr_inflate.h"
 #include "dcr_host.h"
 
 using namespace dcrh;
@@ -395,12 +396,19 @@ struct RecParser {
 // its error messages) takes over.
 struct Chunk {
     HugeBuf buf;                    // [kHead headroom][len inflated bytes]
+    uint8_t *pin = nullptr;         // the same, page-locked (GPU inflate), instead of buf
+    uint8_t *data() { return pin ? pin : buf.data(); }
     size_t len = 0;
     bool eof = false;               // nothing follows this chunk
     std::string err;
     bool indexed = false;           // recs holds every record starting after the first
     std::vector<Rec> recs;          // boundary in this chunk and ending in it (off from buf start)
 };
+
+// the GPU inflate hook (dcr_io_set_inflate_hook), copied by each Inflater
+std::mutex g_hook_mu;
+dcr_inflate_hook g_hook{};
+bool g_hook_set = false;
 
 // override of a pool's size (A/B runs): the variable's value if set and positive
 inline int env_threads(const char *name, int dflt) {
@@ -413,6 +421,7 @@ class Inflater {
   public:
     static constexpr size_t kHead = (size_t)8 << 20;
     static constexpr size_t kWant = (size_t)32 << 20;
+    static constexpr size_t kWantGpu = (size_t)64 << 20;
 
     // ranged: start at the BGZF block at file offset start_coff, start_uoff
     // bytes into its data, on a record boundary (no header); end_coff >= 0:
@@ -450,9 +459,25 @@ class Inflater {
             }
             cbuf_.resize((size_t)48 << 20);
         }
+        {
+            std::lock_guard<std::mutex> g(g_hook_mu);
+            const char *e = std::getenv("DCR_GPU_INFLATE");
+            if (g_hook_set && !(e && std::strcmp(e, "0") == 0)) {
+                hook_ = g_hook;
+                gpu_ = true;
+            }
+        }
+        // GPU inflate: larger chunks (a launch needs ~1,000 members to fill the device)
+        want_max_ = gpu_ ? kWantGpu : kWant;
         for (auto &c : chunks_) {
-            c.buf.resize(kHead + kWant + 0x10000);
+            if (gpu_ && hook_.host_alloc) c.pin = (uint8_t *)hook_.host_alloc(hook_.user, kHead + want_max_ + 0x10000);
+            if (!c.pin) c.buf.resize(kHead + want_max_ + 0x10000);
             empty_.push_back(&c);
+        }
+        if (gpu_) {
+            stage_cap_ = want_max_ + ((size_t)1 << 20);
+            if (hook_.host_alloc) stage_pin_ = (uint8_t *)hook_.host_alloc(hook_.user, stage_cap_);
+            if (!stage_pin_) stage_.resize(stage_cap_);
         }
         th_ = std::thread([this] { loop(); });
         sth_ = std::thread([this] { scan_loop(); });
@@ -466,7 +491,13 @@ class Inflater {
         th_.join();
         sth_.join();
         if (map_) munmap((void *)map_, map_len_);
+        if (hook_.host_free) {
+            for (auto &c : chunks_)
+                if (c.pin) hook_.host_free(hook_.user, c.pin);
+            if (stage_pin_) hook_.host_free(hook_.user, stage_pin_);
+        }
     }
+    bool gpu() const { return gpu_; }
     Chunk *next() {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return !full_.empty(); });
@@ -532,7 +563,7 @@ class Inflater {
         c.indexed = false;
         if (dead_ || !c.err.empty()) { dead_ = true; return; }
         const double t0 = prof_ ? now() : 0;
-        const uint8_t *d = c.buf.data() + kHead;
+        const uint8_t *d = c.data() + kHead;
         const size_t n = c.len;
         size_t pos = 0;
         offs_.clear();
@@ -602,7 +633,7 @@ class Inflater {
         }
         const double t1 = prof_ ? now() : 0;
         c.recs.resize(offs_.size());
-        const uint8_t *base = c.buf.data();
+        const uint8_t *base = c.data();
         const size_t chunk = 512;
         spool_.run((offs_.size() + chunk - 1) / chunk, [&](size_t k) {
             const size_t e = std::min(offs_.size(), (k + 1) * chunk);
@@ -639,11 +670,13 @@ class Inflater {
         struct Blk { size_t coff, clen, doff; uint32_t isize, crc; };
         std::vector<Blk> blks;
         size_t total = 0, cut = SIZE_MAX;
+        size_t range0 = 0;              // the blocks' compressed bytes: [range0, cbeg_) of cdata()
         if (range_done_) { c.eof = true; return; }
         // compressed bytes are only moved while no parsed block points into them
         if (!file_eof_ && cend_ - cbeg_ < cbuf_.size() / 2) top_up();
         for (;;) {
             while (!range_done_ && cend_ - cbeg_ >= 18 && total + 0x10000 <= want_) {
+                if (blks.empty()) range0 = cbeg_;
                 if (end_coff_ >= 0 && cpos_ + cbeg_ >= (uint64_t)end_coff_) {
                     // the range's last block: only its first end_uoff bytes
                     range_done_ = true;
@@ -683,9 +716,35 @@ class Inflater {
             }
             top_up();
         }
-        uint8_t *dst = c.buf.data();
+        uint8_t *dst = c.data();
         const uint8_t *src = cdata();
-        const bool ok = pool_.run(blks.size(), [&](size_t i) {
+        if (gpu_ && !blks.empty()) {
+            // the members' compressed bytes to page-locked staging (pool-parallel
+            // copy out of the page cache), then inflate, CRC32 and ISIZE checks
+            // on the device, straight into the chunk buffer
+            const size_t nb = cbeg_ - range0;
+            uint8_t *stage = stage_pin_ ? stage_pin_ : stage_.data();
+            if (nb > stage_cap_) { c.err = "BGZF chunk larger than its staging buffer"; return; }
+            const size_t piece = (size_t)1 << 20;
+            pool_.run((nb + piece - 1) / piece, [&](size_t k) {
+                const size_t a = k * piece, n = std::min(piece, nb - a);
+                std::memcpy(stage + a, src + range0 + a, n);
+                return true;
+            });
+            mem_.resize(blks.size());
+            for (size_t i = 0; i < blks.size(); ++i) {
+                const Blk &b = blks[i];
+                mem_[i] = dcr_bgzf_member{(int64_t)(b.coff - range0), (int64_t)(b.doff - kHead), (uint32_t)b.clen,
+                                          b.isize, b.crc, 0};
+            }
+            const int rc = hook_.run(hook_.user, stage, (int64_t)nb, mem_.data(), (int32_t)blks.size(),
+                                     dst + kHead, (int64_t)total);
+            if (rc != 0) {
+                c.err = rc > 0 ? "BGZF block failed to inflate or CRC mismatch" : "GPU inflate failed";
+                return;
+            }
+        }
+        const bool ok = gpu_ || pool_.run(blks.size(), [&](size_t i) {
             const Blk &b = blks[i];
             if (b.isize == 0) return b.clen <= 2;      // empty block (the EOF marker)
             size_t got = 0;
@@ -697,7 +756,7 @@ class Inflater {
         if (!ok) { c.err = "BGZF block failed to inflate or CRC mismatch"; return; }
         c.len = total;
         if (blks.empty() && file_eof_ && cend_ == cbeg_) c.eof = true;
-        want_ = kWant;
+        want_ = want_max_;
         if (range_done_) {
             if (cut != SIZE_MAX) {
                 if (cut > total) { c.err = "range end past the end of its BGZF block"; return; }
@@ -718,6 +777,13 @@ class Inflater {
     const uint8_t *cdata() const { return map_ ? map_ : cbuf_.data(); }
     bool range_done_ = false;
     size_t want_ = (size_t)4 << 20;   // the first chunk is small: the walk starts sooner
+    size_t want_max_ = kWant;
+    bool gpu_ = false;                 // members inflated by hook_.run
+    dcr_inflate_hook hook_{};
+    uint8_t *stage_pin_ = nullptr;     // page-locked compressed staging (GPU inflate)
+    HugeBuf stage_;
+    size_t stage_cap_ = 0;
+    std::vector<dcr_bgzf_member> mem_;
     HugeBuf cbuf_;
     size_t cbeg_ = 0, cend_ = 0;
     bool file_eof_ = false;
@@ -812,14 +878,14 @@ struct dcr_ingest {
             const uint8_t *nbuf;
             if (left <= Inflater::kHead) {
                 base = Inflater::kHead - left;
-                if (left) std::memcpy(nx->buf.data() + base, wb + keep, left);
-                nbuf = nx->buf.data();
+                if (left) std::memcpy(nx->data() + base, wb + keep, left);
+                nbuf = nx->data();
             } else {                                 // a leftover larger than the headroom
                 HugeBuf &bg = big[big_i];
                 big_i ^= 1;
                 bg.resize(left + nx->len + 16);
                 std::memcpy(bg.data(), wb + keep, left);
-                std::memcpy(bg.data() + left, nx->buf.data() + Inflater::kHead, nx->len);
+                std::memcpy(bg.data() + left, nx->data() + Inflater::kHead, nx->len);
                 base = 0;
                 nbuf = bg.data();
             }
@@ -829,7 +895,7 @@ struct dcr_ingest {
             wb = nbuf;
             if (cur) infl->give_back(cur);
             ci = 0;
-            if (nbuf == nx->buf.data()) cur = nx;       // the chunk's record offsets hold in the window
+            if (nbuf == nx->data()) cur = nx;       // the chunk's record offsets hold in the window
             else { cur = nullptr; infl->give_back(nx); }
             if (nx->eof) data_eof = true;
         }
@@ -1374,6 +1440,20 @@ bool record_ok(SplitReader &rd, size_t o, int32_t n_ref, size_t &next) {
 extern "C" {
 
 int dcr_io_abi_version(void) { return DCR_IO_ABI_VERSION; }
+
+int dcr_io_set_inflate_hook(const dcr_inflate_hook *hook) {
+    std::lock_guard<std::mutex> g(g_hook_mu);
+    if (hook && hook->run) {
+        g_hook = *hook;
+        g_hook_set = true;
+    } else {
+        g_hook = dcr_inflate_hook{};
+        g_hook_set = false;
+    }
+    return DCR_IO_OK;
+}
+
+int dcr_ingest_gpu_inflate(dcr_ingest *ing) { return ing && ing->infl && ing->infl->gpu() ? 1 : 0; }
 const char *dcr_io_last_error(void) { return g_err.c_str(); }
 
 static dcr_ingest *open_impl(const char *path, const dcr_ingest_cfg *cfg, bool ranged, int64_t start_voff,

@@ -4,9 +4,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "../../include/dcr.h"
 
 namespace dcr {
+
+// sets dcr_last_error() (dcr_capi.hip) and returns code
+int set_error(int code, const std::string &msg);
 
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;

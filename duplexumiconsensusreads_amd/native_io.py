@@ -105,6 +105,8 @@ def load():
             "dcr_ingest_sample_calls": (_i64, [_vp, _vp, _i64]),
             "dcr_py_replay": (_i32, [_vp, _vp, _vp, _i64]),
             "dcr_bam_header": (_i64, [ctypes.c_char_p, _vp, _i64]),
+            "dcr_io_set_inflate_hook": (_i32, [_vp]),
+            "dcr_ingest_gpu_inflate": (_i32, [_vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -216,6 +218,19 @@ class HostBatch:
         return ERR_NAMES.get(self.s.err_kind), self.s.err_msg.decode(errors="replace")
 
 
+_HOOK = None    # the dcr_inflate_hook passed to the library (kept alive here)
+
+
+def set_inflate_hook(hook):
+    """Ingests opened after this inflate their BGZF members with ``hook``
+    (a ``_lib.InflateHook`` from ``_lib.Inflater.hook()``: the device
+    inflater); None goes back to the host pool (dcr_io_set_inflate_hook)."""
+    global _HOOK
+    if load().dcr_io_set_inflate_hook(ctypes.byref(hook) if hook is not None else None) != 0:
+        raise _err("set_inflate_hook")
+    _HOOK = hook
+
+
 class Ingest:
     """dcr_ingest: a BAM opened for batched reading."""
 
@@ -234,6 +249,11 @@ class Ingest:
         p = _vp()
         n = lib.dcr_ingest_header(self._h, ctypes.byref(p))
         self.header = ctypes.string_at(p.value, n) if n > 0 else b""
+
+    @property
+    def gpu_inflate(self) -> bool:
+        """True when this ingest inflates on the GPU (set_inflate_hook)."""
+        return bool(load().dcr_ingest_gpu_inflate(self._h))
 
     def sample_calls(self):
         """(population, sample size) of every random.sample call so far."""

@@ -145,6 +145,18 @@ int dcr_ingest_next(dcr_ingest *ing, dcr_host_batch *hb);
    families, [3] filtered families, [4] records read */
 int dcr_ingest_counters(dcr_ingest *ing, int64_t *out5);
 
+/* ---- BGZF inflate on the GPU (include/dcr_inflate.h) ----------------------
+ * With a hook set, ingests opened afterwards hand the BGZF members of every
+ * input chunk to hook->run (libdcr.so's device inflater: the members' CRC32
+ * and ISIZE are checked there) instead of inflating them on the host pool,
+ * and take their chunk buffers from hook->host_alloc (page-locked).  NULL
+ * clears it.  DCR_GPU_INFLATE=0 in the environment ignores a set hook (A/B
+ * runs).  The struct is copied; its functions must outlive the ingests. */
+struct dcr_inflate_hook;
+int dcr_io_set_inflate_hook(const struct dcr_inflate_hook *hook);
+/* 1 if the ingest inflates on the GPU */
+int dcr_ingest_gpu_inflate(dcr_ingest *ing);
+
 /* ---- family-range sharding (cli --gpus N: one process per GPU) ----------
  * Split points for n_parts ranges of whole families: part p (p >= 1) starts
  * at voff[p-1], the BGZF virtual offset (block file offset << 16 | offset in

@@ -10,11 +10,12 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "dcr.h")
+HEADERS = [HEADER, os.path.join(ROOT, "include", "dcr_inflate.h")]     # both implemented by libdcr.so
 LIB = os.path.join(ROOT, "duplexumiconsensusreads_amd", "libdcr.so")
 
 
 def header_functions():
-    txt = open(HEADER).read()
+    txt = "\n".join(open(h).read() for h in HEADERS)
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     names = re.findall(r"^[A-Za-z_][\w\s\*]*?\b(dcr_\w+)\s*\(", txt, flags=re.M)
     return sorted(set(names))
