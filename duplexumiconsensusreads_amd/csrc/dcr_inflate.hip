@@ -36,7 +36,31 @@
 #include "dcr_deflate.h"
 #include "dcr_internal.h"
 
+#ifndef DINF_STAMP
+#define DINF_STAMP 0      // diagnostic builds: per-phase s_memtime cycles and token counts in Args::dbg
+#endif
+
 namespace dinf {
+
+// diagnostic phase clock (DINF_STAMP builds): dbg[16 mi + k]
+struct IStamp {
+    uint64_t t = 0;
+    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    __device__ __forceinline__ void start() {
+        if (DINF_STAMP) t = __builtin_amdgcn_s_memtime();
+    }
+    __device__ __forceinline__ void lap(int k) {
+        if (DINF_STAMP) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            acc[k] += (uint32_t)(now - t);
+            t = now;
+        }
+    }
+    __device__ __forceinline__ void count(int k, uint32_t v = 1) {
+        if (DINF_STAMP) cnt[k] += v;
+    }
+};
 
 constexpr int kW = 64;
 constexpr int kLB = 10;                    // literal/length root table bits
@@ -100,7 +124,7 @@ __device__ __forceinline__ uint32_t dist_entry(uint32_t sym) {
 // Returns false for an over-subscribed code.  Entries of codes longer than
 // TB bits are 0; an incomplete code leaves K_BAD entries.
 template <int TB, int KIND>
-__device__ __forceinline__ bool build_table(const uint8_t *lens, int n, uint32_t *tab, uint16_t *cnt_out, uint16_t *sym_out) {
+__device__ __noinline__ bool build_table(const uint8_t *lens, int n, uint32_t *tab, uint16_t *cnt_out, uint16_t *sym_out) {
     const int lane = lane_id();
     const uint64_t lt = (1ull << lane) - 1;
     // codes per length: lane L holds cnt[L]
@@ -259,10 +283,10 @@ __device__ __forceinline__ int slow_decode(Dec &d, const uint16_t *cnt, const ui
     uint32_t code = 0, first = 0, index = 0;
     for (uint32_t L = 1; L <= 15; ++L) {
         code |= (uint32_t)(d.bb >> (L - 1)) & 1u;
-        const uint32_t c = cnt[L];
+        const uint32_t c = uni(cnt[L]);      // LDS reads stay wave-uniform (else the whole decoder turns divergent)
         if (code - first < c) {
             nbits = L;
-            return (int)sym[index + code - first];
+            return (int)uni(sym[index + code - first]);
         }
         index += c;
         first = (first + c) << 1;
@@ -287,11 +311,15 @@ __device__ __forceinline__ uint32_t crc_stripe(const WaveLds &s, uint32_t from, 
     return c;
 }
 
-// write ring bytes [gpos, gpos + m) to HBM (m <= 4096) and fold them into the CRC
-__device__ __forceinline__ void write_piece(WaveLds &s, Out &o, uint32_t m, const Args &a, uint32_t lane_shift) {
+extern __shared__ __align__(16) unsigned char smem[];
+
+// write ring bytes [g0, g0 + m) to HBM (m <= 4096) and fold them into the raw
+// CRC; one out-of-line copy (called every 4 KiB) keeps the decode loop small
+__device__ __noinline__ uint32_t write_piece(uint8_t *g, uint32_t g0, uint32_t m, uint32_t crc, uint32_t lane_shift,
+                                             uint32_t x8n_piece) {
+    const WaveLds &s = *reinterpret_cast<const WaveLds *>(smem);
     const int lane = lane_id();
-    const uint32_t g0 = o.gpos;
-    uint8_t *dst = o.g + g0;
+    uint8_t *dst = g + g0;
     if (((uintptr_t)dst & 3) == 0 && (g0 & 3) == 0) {
         const uint32_t *rw = reinterpret_cast<const uint32_t *>(s.ring);
         uint32_t *dw = reinterpret_cast<uint32_t *>(dst);
@@ -305,22 +333,31 @@ __device__ __forceinline__ void write_piece(WaveLds &s, Out &o, uint32_t m, cons
     uint32_t c = hi > lo ? crc_stripe(s, g0 + lo, hi - lo) : 0;
     if (hi > lo) c = dfl::multmodp(m == kPiece ? lane_shift : dfl::x8nmodp(m - hi), c);
     for (int d = 32; d >= 1; d >>= 1) c ^= __shfl_xor(c, d, kW);
-    const uint32_t shift = m == kPiece ? a.x8n_piece : dfl::x8nmodp(m);
-    o.crc = uni(dfl::multmodp(shift, o.crc) ^ c);
-    o.gpos = g0 + m;
+    const uint32_t shift = m == kPiece ? x8n_piece : dfl::x8nmodp(m);
+    return uni(dfl::multmodp(shift, crc) ^ c);
 }
 
+// Ring writes past the bytes produced are harmless: positions in
+// [opos, opos + 64) are rewritten before anything reads them, and their ring
+// slots alias bytes older than opos + 64 - 8 KiB, which no match reads
+// (distances from the ring stay <= kRingDist) and which are already in HBM
+// (gpos > opos - 4 KiB - 322).  So literal flushes and match copies store all
+// 64 lanes, with no exec masking.
+constexpr uint32_t kRingDist = kRing - kW;
+
 __device__ __forceinline__ void flush_lits(WaveLds &s, Out &o) {
-    if (lane_id() < (int)o.nlit) s.ring[(o.opos + lane_id()) & kRM] = (uint8_t)o.lbuf;
+    s.ring[(o.opos + lane_id()) & kRM] = (uint8_t)o.lbuf;
     o.opos += o.nlit;
     o.nlit = 0;
 }
-__device__ __forceinline__ void keep_room(WaveLds &s, Out &o, const Args &a, uint32_t lane_shift) {
-    while (o.gpos + kPiece <= o.opos) write_piece(s, o, kPiece, a, lane_shift);
+__device__ __forceinline__ void keep_room(Out &o, const Args &a, uint32_t lane_shift) {
+    while (o.gpos + kPiece <= o.opos) {
+        o.crc = uni(write_piece(o.g, o.gpos, kPiece, o.crc, lane_shift, a.x8n_piece));   // call results count as divergent
+        o.gpos += kPiece;
+    }
 }
 
 __global__ __launch_bounds__(64) void k_inflate(Args a) {
-    extern __shared__ __align__(16) unsigned char smem[];
     WaveLds &s = *reinterpret_cast<WaveLds *>(smem);
     const int lane = lane_id();
     const int mi = blockIdx.x;
@@ -344,6 +381,8 @@ __global__ __launch_bounds__(64) void k_inflate(Args a) {
 
     bool last = false;
     uint32_t guard = 0, where = 0;
+    IStamp sp;
+    sp.start();
     while (!last && st == ST_OK) {
         if (++guard > kGuard) { st = ST_GUARD; where = 1; break; }
         if (bits_used(d) > (M.in_len + 4) * 8) { st = ST_STREAM; break; }
@@ -362,7 +401,7 @@ __global__ __launch_bounds__(64) void k_inflate(Args a) {
                 const uint32_t m = min((uint32_t)kW, len - c0);
                 if (lane < (int)m) s.ring[(o.opos + lane) & kRM] = src[c0 + lane];
                 o.opos += m;
-                keep_room(s, o, a, lsh);
+                keep_room(o, a, lsh);
             }
             // the bit reader restarts after the stored bytes
             dec_start(d, src + len, mend, (uint32_t)(src + len - mstart) * 8);
@@ -384,7 +423,7 @@ __global__ __launch_bounds__(64) void k_inflate(Args a) {
                 if (lane == 0) s.cl_lens[dfl::kClOrder[i]] = (uint8_t)v;
             }
             // the code-length table lives in dist[] while the lengths are read
-            if (!build_table<kCB, 2>(s.cl_lens, 19, s.dist, s.dcnt, s.dsym)) { st = ST_STREAM; break; }
+            if (!uni(build_table<kCB, 2>(s.cl_lens, 19, s.dist, s.dcnt, s.dsym))) { st = ST_STREAM; break; }
             const uint32_t total = hlit + hdist;
             uint32_t i = 0;
             while (i < total) {
@@ -399,7 +438,7 @@ __global__ __launch_bounds__(64) void k_inflate(Args a) {
                 uint32_t rep = 1, val = sym;
                 if (sym == 16) {
                     if (i == 0) { st = ST_STREAM; break; }
-                    val = s.lens[i - 1];
+                    val = uni(s.lens[i - 1]);
                     rep = 3 + getbits(d, 2);
                 } else if (sym == 17) {
                     val = 0;
@@ -413,10 +452,11 @@ __global__ __launch_bounds__(64) void k_inflate(Args a) {
                 i += rep;
             }
             if (st != ST_OK) break;
-            if (s.lens[256] == 0) { st = ST_STREAM; break; }
-            if (!build_table<kLB, 0>(s.lens, (int)hlit, s.lit, s.lcnt, s.lsym)) { st = ST_STREAM; break; }
-            if (!build_table<kDB, 1>(s.lens + hlit, (int)hdist, s.dist, s.dcnt, s.dsym)) { st = ST_STREAM; break; }
+            if (uni(s.lens[256]) == 0) { st = ST_STREAM; break; }
+            if (!uni(build_table<kLB, 0>(s.lens, (int)hlit, s.lit, s.lcnt, s.lsym))) { st = ST_STREAM; break; }
+            if (!uni(build_table<kDB, 1>(s.lens + hlit, (int)hdist, s.dist, s.dcnt, s.dsym))) { st = ST_STREAM; break; }
         }
+        sp.lap(0);                                        // block header, tables
         // Huffman-coded data
         for (;;) {
             if (++guard > kGuard) { st = ST_GUARD; where = 3; break; }
@@ -432,6 +472,7 @@ __global__ __launch_bounds__(64) void k_inflate(Args a) {
             d.nb -= n;
             const uint32_t kind = (e >> 5) & 7;
             if (kind == K_LIT || kind == K_PAIR) {
+                sp.count(kind == K_PAIR ? 1 : 0);
                 o.lbuf = lane == (int)o.nlit ? (e >> 8) & 0xff : o.lbuf;
                 ++o.nlit;
                 if (kind == K_PAIR) {
@@ -440,8 +481,10 @@ __global__ __launch_bounds__(64) void k_inflate(Args a) {
                 }
                 if (o.nlit >= kW - 1) {
                     if (o.opos + o.nlit > o.isize) { st = ST_SIZE; break; }
+                    sp.lap(1);
                     flush_lits(s, o);
-                    keep_room(s, o, a, lsh);
+                    keep_room(o, a, lsh);
+                    sp.lap(4);
                 }
                 continue;
             }
@@ -467,15 +510,24 @@ __global__ __launch_bounds__(64) void k_inflate(Args a) {
             d.bb >>= dex;
             d.nb -= dex;
             if (o.opos + o.nlit + len > o.isize) { st = ST_SIZE; break; }
+            sp.lap(2);
+            sp.count(2);
+            sp.count(3, len);
             flush_lits(s, o);
             if (dist > o.opos) { st = ST_STREAM; break; }
-            if (dist <= kRing) {
+            if (dist >= kW && dist <= kRingDist) {
+                // no overlap inside a 64-byte step: sources precede the step
                 for (uint32_t c0 = 0; c0 < len; c0 += kW) {
                     const uint32_t i = c0 + lane;
-                    uint8_t v = 0;
-                    if (i < len) v = s.ring[(o.opos - dist + (dist < kW ? i % dist : i)) & kRM];
-                    if (i < len) s.ring[(o.opos + i) & kRM] = v;
+                    const uint8_t v = s.ring[(o.opos - dist + i) & kRM];
+                    s.ring[(o.opos + i) & kRM] = v;
                 }
+            } else if (dist < kW) {
+                // a period below the wave: byte i repeats byte i mod dist
+                const uint32_t rep = (uint32_t)lane % dist;      // then + dist steps of the period
+                const uint32_t step = kW - kW % dist;            // a multiple of dist
+                const uint8_t v = s.ring[(o.opos - dist + rep) & kRM];
+                for (uint32_t c0 = 0; c0 < len; c0 += step) s.ring[(o.opos + c0 + lane) & kRM] = v;
             } else {
                 // older than the ring: already in HBM (written by this wave)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -485,17 +537,24 @@ __global__ __launch_bounds__(64) void k_inflate(Args a) {
                 }
             }
             o.opos += len;
-            keep_room(s, o, a, lsh);
+            sp.lap(3);
+            keep_room(o, a, lsh);
+            sp.lap(4);
         }
+        sp.lap(1);
         if (st != ST_OK) break;
         if (o.opos + o.nlit > o.isize) { st = ST_SIZE; break; }
         flush_lits(s, o);
-        keep_room(s, o, a, lsh);
+        keep_room(o, a, lsh);
     }
     if (st == ST_OK && (bits_used(d) + 7) / 8 > M.in_len) st = ST_STREAM;
     if (st == ST_OK && o.opos != o.isize) st = ST_SIZE;
     if (st == ST_OK) {
-        while (o.gpos < o.opos) write_piece(s, o, min(kPiece, o.opos - o.gpos), a, lsh);
+        while (o.gpos < o.opos) {
+            const uint32_t m = min(kPiece, o.opos - o.gpos);
+            o.crc = uni(write_piece(o.g, o.gpos, m, o.crc, lsh, a.x8n_piece));
+            o.gpos += m;
+        }
         const uint32_t crc = ~(dfl::multmodp(dfl::x8nmodp(o.isize), 0xffffffffu) ^ o.crc);
         if (o.isize == 0) {
             if (M.crc != 0) st = ST_CRC;
@@ -503,9 +562,16 @@ __global__ __launch_bounds__(64) void k_inflate(Args a) {
             st = ST_CRC;
         }
     }
+    sp.lap(5);
+    if (DINF_STAMP && lane == 0 && a.dbg) {
+        for (int k = 0; k < 6; ++k) a.dbg[16 * mi + k] = sp.acc[k];
+        for (int k = 0; k < 4; ++k) a.dbg[16 * mi + 8 + k] = sp.cnt[k];
+        a.dbg[16 * mi + 12] = guard;
+        a.dbg[16 * mi + 13] = o.opos;
+    }
     if (lane == 0) {
         a.status[mi] = st;
-        if (a.dbg) {
+        if (a.dbg && !DINF_STAMP) {
             a.dbg[4 * mi] = st | where << 8;
             a.dbg[4 * mi + 1] = bits_used(d);
             a.dbg[4 * mi + 2] = o.opos;
@@ -530,6 +596,7 @@ struct dcr_inflater {
     float last_ms = 0;
     int32_t last_n = 0;
     double tot[4] = {0, 0, 0, 0};     // kernel ms, runs, members, output bytes
+    double stamp[16] = {};            // DINF_STAMP builds: summed dbg words
     std::mutex mu;
     std::unordered_multimap<size_t, void *> free_host;   // page-locked buffers kept for later ingests
     std::unordered_map<void *, size_t> live_host;
@@ -611,7 +678,7 @@ int dcr_inflater_run(dcr_inflater *h, const uint8_t *in, int64_t in_bytes, const
         (e = grow(h->d_out, h->cap_out, (size_t)out_bytes + 16)) != hipSuccess ||
         (e = grow(h->d_m, h->cap_m, (size_t)n)) != hipSuccess ||
         (e = grow(h->d_st, h->cap_st, (size_t)n)) != hipSuccess ||
-        (e = grow(h->d_dbg, h->cap_dbg, (size_t)n * 4)) != hipSuccess)
+        (e = grow(h->d_dbg, h->cap_dbg, (size_t)n * (DINF_STAMP ? 16 : 4))) != hipSuccess)
         return -hip_fail(e, "dcr_inflater_run: device buffers");
     std::vector<uint8_t> st((size_t)n);
     hipStream_t s = h->stream;
@@ -639,6 +706,12 @@ int dcr_inflater_run(dcr_inflater *h, const uint8_t *in, int64_t in_bytes, const
     h->tot[1] += 1;
     h->tot[2] += n;
     h->tot[3] += (double)out_bytes;
+    if (DINF_STAMP) {
+        std::vector<uint32_t> dbg((size_t)n * 16);
+        (void)hipMemcpy(dbg.data(), h->d_dbg, dbg.size() * 4, hipMemcpyDeviceToHost);
+        for (int32_t i = 0; i < n; ++i)
+            for (int k = 0; k < 16; ++k) h->stamp[k] += dbg[(size_t)i * 16 + k];
+    }
     for (int32_t i = 0; i < n; ++i)
         if (st[(size_t)i] != dinf::ST_OK) {
             uint32_t dbg[4] = {0, 0, 0, 0};
@@ -671,6 +744,17 @@ int dcr_inflater_totals(dcr_inflater *h, double *out4, int reset) {
     if (reset)
         for (double &t : h->tot) t = 0;
     return 0;
+}
+
+// diagnostic (not in include/dcr_inflate.h): the summed phase stamps of a
+// DINF_STAMP build (0 otherwise)
+extern "C" int dcr_inflater_stamps(dcr_inflater *h, double *out16, int reset) {
+    if (!h || !out16) return dcr::set_error(DCR_EARG, "dcr_inflater_stamps: null argument");
+    std::lock_guard<std::mutex> g(h->mu);
+    for (int i = 0; i < 16; ++i) out16[i] = h->stamp[i];
+    if (reset)
+        for (double &t : h->stamp) t = 0;
+    return DINF_STAMP;
 }
 
 static int hook_run(void *u, const uint8_t *in, int64_t in_bytes, const dcr_bgzf_member *m, int32_t n, uint8_t *out,

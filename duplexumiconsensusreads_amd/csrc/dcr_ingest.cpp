@@ -469,6 +469,10 @@ class Inflater {
         }
         // GPU inflate: larger chunks (a launch needs ~1,000 members to fill the device)
         want_max_ = gpu_ ? kWantGpu : kWant;
+        if (const char *fr = std::getenv("DCR_GPU_INFLATE_FRAC")) {
+            frac_ = std::min(1.0, std::max(0.0, std::atof(fr)));
+            frac_fixed_ = true;
+        }
         for (auto &c : chunks_) {
             if (gpu_ && hook_.host_alloc) c.pin = (uint8_t *)hook_.host_alloc(hook_.user, kHead + want_max_ + 0x10000);
             if (!c.pin) c.buf.resize(kHead + want_max_ + 0x10000);
@@ -718,33 +722,7 @@ class Inflater {
         }
         uint8_t *dst = c.data();
         const uint8_t *src = cdata();
-        if (gpu_ && !blks.empty()) {
-            // the members' compressed bytes to page-locked staging (pool-parallel
-            // copy out of the page cache), then inflate, CRC32 and ISIZE checks
-            // on the device, straight into the chunk buffer
-            const size_t nb = cbeg_ - range0;
-            uint8_t *stage = stage_pin_ ? stage_pin_ : stage_.data();
-            if (nb > stage_cap_) { c.err = "BGZF chunk larger than its staging buffer"; return; }
-            const size_t piece = (size_t)1 << 20;
-            pool_.run((nb + piece - 1) / piece, [&](size_t k) {
-                const size_t a = k * piece, n = std::min(piece, nb - a);
-                std::memcpy(stage + a, src + range0 + a, n);
-                return true;
-            });
-            mem_.resize(blks.size());
-            for (size_t i = 0; i < blks.size(); ++i) {
-                const Blk &b = blks[i];
-                mem_[i] = dcr_bgzf_member{(int64_t)(b.coff - range0), (int64_t)(b.doff - kHead), (uint32_t)b.clen,
-                                          b.isize, b.crc, 0};
-            }
-            const int rc = hook_.run(hook_.user, stage, (int64_t)nb, mem_.data(), (int32_t)blks.size(),
-                                     dst + kHead, (int64_t)total);
-            if (rc != 0) {
-                c.err = rc > 0 ? "BGZF block failed to inflate or CRC mismatch" : "GPU inflate failed";
-                return;
-            }
-        }
-        const bool ok = gpu_ || pool_.run(blks.size(), [&](size_t i) {
+        auto host_inflate = [&](size_t i) {
             const Blk &b = blks[i];
             if (b.isize == 0) return b.clen <= 2;      // empty block (the EOF marker)
             size_t got = 0;
@@ -752,7 +730,57 @@ class Inflater {
                 got != b.isize)
                 return false;
             return libdeflate_crc32(0, dst + b.doff, b.isize) == b.crc;
-        });
+        };
+        bool ok = true;
+        if (gpu_ && !blks.empty()) {
+            // the chunk's first k members inflate on the GPU (their compressed
+            // bytes copied to page-locked staging by the pool first; CRC32 and
+            // ISIZE checked on the device; output straight into the chunk
+            // buffer) while the host pool inflates the rest; k follows the
+            // measured times of both sides (their finish times meet)
+            const size_t n = blks.size();
+            const size_t k = std::min(n, std::max<size_t>(1, (size_t)(frac_ * (double)n + 0.5)));
+            const size_t g0 = blks[0].coff, g1 = blks[k - 1].coff + blks[k - 1].clen;
+            const size_t nb = g1 - g0;
+            uint8_t *stage = stage_pin_ ? stage_pin_ : stage_.data();
+            if (nb > stage_cap_) { c.err = "BGZF chunk larger than its staging buffer"; return; }
+            const size_t piece = (size_t)1 << 20;
+            pool_.run((nb + piece - 1) / piece, [&](size_t q) {
+                const size_t a = q * piece, m = std::min(piece, nb - a);
+                std::memcpy(stage + a, src + g0 + a, m);
+                return true;
+            });
+            mem_.resize(k);
+            for (size_t i = 0; i < k; ++i) {
+                const Blk &b = blks[i];
+                mem_[i] = dcr_bgzf_member{(int64_t)(b.coff - g0), (int64_t)(b.doff - kHead), (uint32_t)b.clen,
+                                          b.isize, b.crc, 0};
+            }
+            const size_t out_k = blks[k - 1].doff + blks[k - 1].isize - kHead;
+            int rc = 0;
+            double t_gpu = 0, t_host = 0;
+            std::thread gt([&] {
+                const double t0 = now();
+                rc = hook_.run(hook_.user, stage, (int64_t)nb, mem_.data(), (int32_t)k, dst + kHead, (int64_t)out_k);
+                t_gpu = now() - t0;
+            });
+            const double th = now();
+            if (k < n) ok = pool_.run(n - k, [&](size_t i) { return host_inflate(k + i); });
+            t_host = now() - th;
+            gt.join();
+            if (rc != 0) {
+                c.err = rc > 0 ? "BGZF block failed to inflate or CRC mismatch" : "GPU inflate failed";
+                return;
+            }
+            if (!frac_fixed_ && k < n && t_gpu > 0 && t_host > 0) {
+                frac_ *= std::sqrt(t_host / t_gpu);
+                frac_ = std::min(0.95, std::max(0.05, frac_));
+            } else if (!frac_fixed_ && k == n && t_gpu > 0) {
+                frac_ = 0.95;
+            }
+        } else {
+            ok = pool_.run(blks.size(), host_inflate);
+        }
         if (!ok) { c.err = "BGZF block failed to inflate or CRC mismatch"; return; }
         c.len = total;
         if (blks.empty() && file_eof_ && cend_ == cbeg_) c.eof = true;
@@ -784,6 +812,8 @@ class Inflater {
     HugeBuf stage_;
     size_t stage_cap_ = 0;
     std::vector<dcr_bgzf_member> mem_;
+    double frac_ = 0.5;                // share of a chunk's members inflated on the GPU
+    bool frac_fixed_ = false;          // DCR_GPU_INFLATE_FRAC set: no adaptation
     HugeBuf cbuf_;
     size_t cbeg_ = 0, cend_ = 0;
     bool file_eof_ = false;

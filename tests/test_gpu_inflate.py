@@ -171,11 +171,15 @@ def test_ingest_gpu_inflate_same_outputs_as_host_inflate(tmp_path, level):
     from duplexumiconsensusreads_amd import bam, cli, native_io
     inp = str(tmp_path / "in.bam")
     synth.write_packed_bam(inp, synth.packed_config(synth.CONFIGS["C5"], 60_000, seed=5), seed=5, level=level)
-    cli.gpu_inflate(0)
+    os.environ["DCR_GPU_INFLATE"] = "1"
+    try:
+        cli.gpu_inflate(0)
+    finally:
+        os.environ.pop("DCR_GPU_INFLATE", None)
     ing = native_io.Ingest(inp)
     assert ing.gpu_inflate
     ing.close()
-    so_gpu = _cli(inp, str(tmp_path / "g.bam"), None)
+    so_gpu = _cli(inp, str(tmp_path / "g.bam"), "1")
     so_host = _cli(inp, str(tmp_path / "h.bam"), "0")
     assert so_gpu == so_host
     for suf in (".bam", "_filteredreads.bam", "_filteredfamilies.bam"):
@@ -194,7 +198,11 @@ def test_ingest_gpu_inflate_corrupt_block(tmp_path):
     x = m[len(m) // 2]
     blob[int(x["in_off"]) + 100] ^= 0xff
     open(inp, "wb").write(bytes(blob))
-    cli.gpu_inflate(0)
+    os.environ["DCR_GPU_INFLATE"] = "1"
+    try:
+        cli.gpu_inflate(0)
+    finally:
+        os.environ.pop("DCR_GPU_INFLATE", None)
     ing = native_io.Ingest(inp)
     assert ing.gpu_inflate
     hb = native_io.HostBatch(reads=1 << 20)

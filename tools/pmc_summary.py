@@ -13,7 +13,7 @@ for f in glob.glob(f"{out}/p*/*counter_collection.csv"):
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[(k, r["Counter_Name"])].add(r["Dispatch_Id"])
 for k, d in agg.items():
-    if "dcr" not in k:
+    if "dcr" not in k and "dinf" not in k:
         continue
     w = d.get("SQ_WAVES", 0) or 1
     print(f"== {k}  (dispatches {len(disp[(k, 'SQ_WAVES')])}, waves {w:.0f})")
