@@ -69,11 +69,11 @@ WORKLOAD = {
 }
 
 
-def make_batch(config, families, seed):
+def make_batch(config, families, seed, max_reads=1000):
     from duplexumiconsensusreads_amd import synth
     if config == "C2":
         return synth.packed_fixed_size(families, seed=seed)
-    return synth.packed_config(synth.CONFIGS[config], families, seed=seed, max_reads=1000)
+    return synth.packed_config(synth.CONFIGS[config], families, seed=seed, max_reads=max_reads)
 
 
 def shared_share(config, families, seed, rank, world):
@@ -195,9 +195,11 @@ def e2e_passes(path, params_args, device, steps, warmup, workdir):
         out = os.path.join(workdir, f"cons{i}.bam")
         return ["-i", path, "-o", out, "--device", str(device), *params_args]
 
+    import random
     cold = None
     for i in range(warmup):
         argv = argv_of(i)
+        random.seed(4)                  # downsampling draws from random.seed(4)
         tw = time.perf_counter()
         with contextlib.redirect_stdout(io.StringIO()):
             cli.main(argv)
@@ -214,6 +216,7 @@ def e2e_passes(path, params_args, device, steps, warmup, workdir):
     for i in range(steps):
         argv = argv_of(warmup + i)
         stats = {"trace": []}
+        random.seed(4)
         t_pass = time.perf_counter()
         with contextlib.redirect_stdout(io.StringIO()):
             cli.main(argv, stats=stats)
@@ -292,6 +295,10 @@ def main():
                     help="strong scaling: ONE input BAM (rank 0's batch) through the sharded CLI, one process "
                          "per GPU over ranges of whole families (cli._main_sharded), instead of one BAM per rank")
     ap.add_argument("--in-level", type=int, default=1, help="BGZF compression level of the synthetic input BAM")
+    ap.add_argument("--max-reads", type=int, default=None,
+                    help="--max_reads of the CLI runs (default: the reference's 100; C4: 1000, the whole deep "
+                         "subfamilies).  Below a config's subfamily sizes the CLI downsamples (random.seed(4)); "
+                         "the device-resident batch is then capped at the same size")
     args = ap.parse_args()
 
     import torch
@@ -315,14 +322,18 @@ def main():
     t0 = time.perf_counter()
     families = args.families or CONFIG_FAMILIES[args.config]
     shared = None
+    max_reads = args.max_reads if args.max_reads is not None else (1000 if args.config == "C4" else 100)
+    bam_packed = None            # the BAM's families when the CLI downsamples them (C4 at --max-reads 100)
     if args.config == "C4" and dist:
         packed, shared = shared_share(args.config, families, args.seed, rank, world)
     else:
-        packed = make_batch(args.config, families, args.seed + 1000 * rank)
+        packed = make_batch(args.config, families, args.seed + 1000 * rank, max_reads=min(max_reads, 1000))
+        if args.config != "C2" and max_reads < 1000:
+            bam_packed = make_batch(args.config, families, args.seed + 1000 * rank, max_reads=1000)
     log(f"[rank {rank}] generated {packed.n_reads} reads in {time.perf_counter() - t0:.1f} s")
-    # C4 runs with --max_reads 1000; the batch is already downsampled
-    params = ConsensusParams(max_reads=1000) if args.config == "C4" else ConsensusParams()
-    params_args = ["--max_reads", "1000"] if args.config == "C4" else []
+    # C4 runs with --max_reads 1000 by default (the deep families whole)
+    params = ConsensusParams(max_reads=max_reads)
+    params_args = ["--max_reads", str(max_reads)] if max_reads != 100 else []
 
     # -- SSCS kernel roofline: device-resident passes ------------------------------
     kavg, dev_bases, n_bad, dev_step = device_resident(packed, params, local, args.kernel_steps, 2)
@@ -344,7 +355,8 @@ def main():
             bam_path = os.path.join(workdir, "in.bam")
             t0 = time.perf_counter()
             if rank == 0 or not args.sharded:
-                synth.write_packed_bam(bam_path, packed, seed=args.seed + 1000 * rank, level=args.in_level)
+                synth.write_packed_bam(bam_path, bam_packed if bam_packed is not None else packed,
+                                       seed=args.seed + 1000 * rank, level=args.in_level)
                 log(f"[rank {rank}] wrote {os.path.getsize(bam_path) / 1e6:.0f} MB BAM (level {args.in_level}) "
                     f"in {time.perf_counter() - t0:.1f} s")
             if dist:
@@ -365,7 +377,7 @@ def main():
             shutil.rmtree(workdir, ignore_errors=True)
 
     e2e_bases = stats.get("consensus_bases", 0) * args.steps
-    in_bases = int(packed.seq_len.astype(np.int64).sum()) * args.steps
+    in_bases = int((bam_packed if bam_packed is not None else packed).seq_len.astype(np.int64).sum()) * args.steps
     if args.sharded and rank != 0:
         in_bases = 0            # one input: rank 0's batch
     # per-rank busy time of the last CLI pass (whole pass, ingest thread, waits on the device)
@@ -414,7 +426,8 @@ def main():
             "config": {"workload": WORKLOAD[args.config] + (
                            f"; --sharded: ONE input of {packed.n_reads} reads split over the {world} GPU(s) by "
                            "the sharded CLI" if args.sharded else ""),
-                       "value_is": value_kind, "input_bgzf_level": args.in_level,
+                       "value_is": value_kind, "input_bgzf_level": args.in_level, "max_reads": max_reads,
+                       "input_reads_per_gpu": (bam_packed if bam_packed is not None else packed).n_reads,
                        "families_per_gpu": packed.n_fam, "reads_per_gpu": packed.n_reads,
                        "input_bases_per_s": (in_bases / slowest) if slowest else None,
                        "consensus_records_per_pass": stats.get("consensus_records"),
