@@ -2573,9 +2573,17 @@ __device__ __forceinline__ uint64_t scalar_dest(const dcr_out &O, int k) {
 
 // a pointer cached in LDS at kernel start, as a per-lane value (one
 // broadcast LDS read; stores through it take a 64-bit VGPR address)
+// (global address space: stores through a pointer read back from LDS would
+// otherwise be flat stores, which count in lgkmcnt too, so every later LDS
+// wait of the record loop also waited for them)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DCR_G __attribute__((address_space(1)))
+#else
+#define DCR_G                  // the host pass only parses device functions
+#endif
 template <class Tp>
-__device__ __forceinline__ Tp *lds_vptr(const uint8_t *lds, int slot) {
-    return (Tp *)(uintptr_t)(*(const uint64_t *)(lds + fk::kPtrs + 8 * slot));
+__device__ __forceinline__ DCR_G Tp *lds_vptr(const uint8_t *lds, int slot) {
+    return (DCR_G Tp *)(uintptr_t)(*(const uint64_t *)(lds + fk::kPtrs + 8 * slot));
 }
 
 // a record's failure status from the fast kernel: status byte and zeroed
@@ -2583,7 +2591,7 @@ __device__ __forceinline__ Tp *lds_vptr(const uint8_t *lds, int slot) {
 __device__ __forceinline__ void fast_status(const uint8_t *lds, int64_t rec, int st, int lane) {
     if (lane < 9) {
         const uint64_t pw = *(const uint64_t *)(lds + fk::kPtrs + 8 * lane);
-        *(uint32_t *)((pw & 0x00FFFFFFFFFFFFFFull) + ((uint64_t)rec << (pw >> 56))) = 0u;
+        *(DCR_G uint32_t *)((pw & 0x00FFFFFFFFFFFFFFull) + ((uint64_t)rec << (pw >> 56))) = 0u;
     } else if (lane == 10) {
         lds_vptr<uint8_t>(lds, fk::kPStatus)[rec] = (uint8_t)st;
     }
@@ -2950,8 +2958,8 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         const int c0 = 4 * lane;
         if (c0 < T16) {
             const uint2 w = *(const uint2 *)(ov + 8 * lane);
-            *(uint2 *)(lds_vptr<uint16_t>(lds, fk::kPD) + off + c0) = make_uint2(w.x & 0x003F003Fu, w.y & 0x003F003Fu);
-            *(uint2 *)(lds_vptr<uint16_t>(lds, fk::kPE) + off + c0) =
+            *(DCR_G uint2 *)(lds_vptr<uint16_t>(lds, fk::kPD) + off + c0) = make_uint2(w.x & 0x003F003Fu, w.y & 0x003F003Fu);
+            *(DCR_G uint2 *)(lds_vptr<uint16_t>(lds, fk::kPE) + off + c0) =
                 make_uint2((w.x >> 6) & 0x003F003Fu, (w.y >> 6) & 0x003F003Fu);
             const int nl = min(max(klen - c0, 0), 4);                    // kept columns of the four
             const uint32_t keep = nl == 4 ? 0xFFFFFFFFu : (1u << (8 * nl)) - 1u;
@@ -2966,8 +2974,8 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
                 letters = *(const uint32_t *)(sb + c0);
                 quals = *(const uint32_t *)(sb + 0x100 + c0);
             }
-            *(uint32_t *)(lds_vptr<uint8_t>(lds, fk::kPSeq) + off + c0) = (letters & keep) | (0x4E4E4E4Eu & ~keep);
-            *(uint32_t *)(lds_vptr<uint8_t>(lds, fk::kPQual) + off + c0) = quals & keep;
+            *(DCR_G uint32_t *)(lds_vptr<uint8_t>(lds, fk::kPSeq) + off + c0) = (letters & keep) | (0x4E4E4E4Eu & ~keep);
+            *(DCR_G uint32_t *)(lds_vptr<uint8_t>(lds, fk::kPQual) + off + c0) = quals & keep;
         }
     }
     sp.mark(8);                          // [7] per-column stores
@@ -3063,7 +3071,7 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
             // destination word of field k (scalar_dest), from the LDS cache
             const uint64_t pw = *(const uint64_t *)(lds + fk::kPtrs + 8 * lane);
             const uint64_t idx = lane == 9 ? (uint64_t)off : (uint64_t)rec;
-            *(uint32_t *)((pw & 0x00FFFFFFFFFFFFFFull) + (idx << (pw >> 56))) = v;
+            *(DCR_G uint32_t *)((pw & 0x00FFFFFFFFFFFFFFull) + (idx << (pw >> 56))) = v;
         } else if (lane == 10) {
             lds_vptr<uint8_t>(lds, fk::kPStatus)[rec] = DCR_ST_OK;
         }
