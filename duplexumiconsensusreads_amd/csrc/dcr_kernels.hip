@@ -2597,6 +2597,23 @@ __device__ __forceinline__ void fast_status(const uint8_t *lds, int64_t rec, int
     }
 }
 
+// a pointer cached in LDS, as a wave-uniform global pointer (stores through
+// it take an SGPR base and a per-lane 32-bit offset: no 64-bit address VALU)
+template <class Tp>
+__device__ __forceinline__ DCR_G Tp *lds_sgptr(const uint8_t *lds, int slot) {
+    const uint64_t v = *(const uint64_t *)(lds + fk::kPtrs + 8 * slot);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const int hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return (DCR_G Tp *)(uintptr_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// v_writelane: an SGPR value into one lane of a VGPR (one VALU, no compare)
+template <int L>
+__device__ __forceinline__ uint32_t write_lane(uint32_t v, uint32_t x) {
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(L));
+    return v;
+}
+
 // a pointer cached in LDS at kernel start (rare paths), as a scalar
 template <class Tp>
 __device__ __forceinline__ Tp *lds_ptr(const uint8_t *lds, int slot) {
@@ -2802,6 +2819,22 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     const double *invd = (const double *)(lds + fk::kInvD);
     uint8_t *ov = lds + ov_addr;
     uint32_t und = 0;                  // bit tt: the lane's live column is not decided
+    // the common instantiation stores every column as it is decided (lane =
+    // column, uniform bases + 32-bit lane offsets, no LDS round trip): 'N' /
+    // quality 0 past T up to the region's end (the untrimmed T rounded to 16
+    // columns; d / e there are don't-care).  A record that turns out to have
+    // an undecided column is queued and the EXACT kernel rewrites all of it.
+    // The column words go to ov only where they are read again: EXACT, and
+    // the double mean of records of more than 16 reads.
+    const int T16 = ((int)((m.w >> 7) & 255u) + 15) & ~15;
+    DCR_G uint16_t *pd = nullptr, *pe = nullptr;
+    DCR_G uint8_t *ps = nullptr, *pq = nullptr;
+    if (!EXACT) {
+        pd = lds_sgptr<uint16_t>(lds, fk::kPD) + off;
+        pe = lds_sgptr<uint16_t>(lds, fk::kPE) + off;
+        ps = lds_sgptr<uint8_t>(lds, fk::kPSeq) + off;
+        pq = lds_sgptr<uint8_t>(lds, fk::kPQual) + off;
+    }
     // more reads than r_safe: L_b may underflow (fast_constants), no column is decided here
     const bool force = R > a.r_safe;
     int dmax = -1, dmin = 0x7fffffff;
@@ -2831,7 +2864,13 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         // decided: LLR_b - max(LLR_k, 0) >= (Lb - L2 - (d - nb)) / 16 >= T16 / 16
         const bool undecided = (int)(Lb - L2) - (d - nb) < a.t16 || force;
         und |= (uint32_t)(live && undecided) << tt;
-        *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (kb << 12));
+        if (EXACT || R > 16) *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (kb << 12));
+        if (!EXACT && DCR_ABL != 5 && t < T16) {
+            pd[t] = (uint16_t)d;
+            pe[t] = (uint16_t)e;
+            ps[t] = (uint8_t)(t < T ? __builtin_amdgcn_perm(0u, 0x47435441u, kb) : 0x4Eu);   // "ATCG"[call]
+            pq[t] = (uint8_t)(t < T ? (uint32_t)a.maxq : 0u);
+        }
         fx += live ? __umul24((uint32_t)e, m720[d]) : 0u;
         dmax = max(dmax, live ? d : -1);
         dmin = min(dmin, live ? d : 0x7fffffff);
@@ -2952,9 +2991,7 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     // columns gets 'N' / quality 0 so a duplex record staging this region never
     // reads a byte that is not a valid letter (d / e there are don't-care)
     lds_fence();
-    if (DCR_ABL != 5) {                 // diagnostic 5: no per-column stores
-        // up to the region's end: the untrimmed T (k_recmeta) rounded to 16 columns
-        const int T16 = ((int)((m.w >> 7) & 255u) + 15) & ~15;
+    if (EXACT && DCR_ABL != 5) {        // diagnostic 5: no per-column stores
         const int c0 = 4 * lane;
         if (c0 < T16) {
             const uint2 w = *(const uint2 *)(ov + 8 * lane);
@@ -3004,6 +3041,9 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         const int64_t r = num - (int64_t)k * den;
         slow = 2 * (r < 0 ? -r : r) >= den || k > 1000;                   // a tie (or a bad estimate)
         E = div1000(k);
+        // the common kernel kept no column words for the double walk: the
+        // EXACT kernel takes the record (a tie is rare)
+        if (!EXACT && slow) return false;
     }
     if (slow) {
     double sum = 0.0;
@@ -3057,16 +3097,17 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         const uint32_t E_lo = (uint32_t)__double_as_longlong(E);
         const uint32_t E_hi = (uint32_t)((uint64_t)__double_as_longlong(E) >> 32);
         const int mapq = (int)((uint32_t)m.d0 >> 16);                        // k_recmeta
-        uint32_t v = (uint32_t)(minpos + first);
-        v = lane == 1 ? (uint32_t)mapq : v;
-        v = lane == 2 ? (uint32_t)klen : v;
-        v = lane == 3 ? 1u : v;
-        v = lane == 4 ? (uint32_t)T : v;
-        v = lane == 5 ? (uint32_t)Dmax : v;
-        v = lane == 6 ? (uint32_t)Dmin : v;
-        v = lane == 7 ? E_lo : v;
-        v = lane == 8 ? E_hi : v;
-        v = lane == 9 ? (uint32_t)klen << 4 : v;
+        uint32_t v = 0;
+        v = write_lane<0>(v, __builtin_amdgcn_readfirstlane((uint32_t)(minpos + first)));
+        v = write_lane<1>(v, __builtin_amdgcn_readfirstlane((uint32_t)mapq));
+        v = write_lane<2>(v, __builtin_amdgcn_readfirstlane((uint32_t)klen));
+        v = write_lane<3>(v, 1u);
+        v = write_lane<4>(v, __builtin_amdgcn_readfirstlane((uint32_t)T));
+        v = write_lane<5>(v, __builtin_amdgcn_readfirstlane((uint32_t)Dmax));
+        v = write_lane<6>(v, __builtin_amdgcn_readfirstlane((uint32_t)Dmin));
+        v = write_lane<7>(v, __builtin_amdgcn_readfirstlane(E_lo));
+        v = write_lane<8>(v, __builtin_amdgcn_readfirstlane(E_hi));
+        v = write_lane<9>(v, __builtin_amdgcn_readfirstlane((uint32_t)klen << 4));
         if (lane < 10) {
             // destination word of field k (scalar_dest), from the LDS cache
             const uint64_t pw = *(const uint64_t *)(lds + fk::kPtrs + 8 * lane);
