@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstddef>
 #include <cstring>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -95,6 +96,9 @@ struct dcr_ctx {
     // fast-kernel constants (fast_constants)
     uint32_t fast_kq = 0, fast_kqlo = 0;
     int fast_maxq = 0, fast_t16 = 0, fast_r_safe = 0, fast_qlo = 0;
+    // single-strand records of at most this many reads skip the common fast
+    // pass (the exact pass takes them whole); DCR_EXACT_DIRECT_R overrides
+    int direct_r = 3;
     uint16_t *d_llr16 = nullptr;   // device [128]
     uint32_t *d_wtab = nullptr;    // device [DCR_LUT_N] (general kernel's decision pass)
     int n_cu = 256;     // compute units (persistent grid size)
@@ -227,6 +231,7 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
     }
     dcr_ctx *c = new dcr_ctx();
     c->device = device;
+    if (const char *e = std::getenv("DCR_EXACT_DIRECT_R")) c->direct_r = std::atoi(e);   // A/B runs
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_params, sizeof(dcr_params)) != hipSuccess ||
@@ -414,6 +419,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         f.lo_check = duplex || c->host_params.min_base_quality < c->fast_qlo;
         f.llr16 = c->d_llr16;
         f.want_info = (c->options & DCR_OPT_READ_INFO) ? 1 : 0;
+        f.direct_r = duplex ? 0 : c->direct_r;
         return f;
     };
     auto strand = [&](bool duplex) -> int {

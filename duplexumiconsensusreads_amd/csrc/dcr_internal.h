@@ -98,6 +98,7 @@ struct FastArgs {
     int lo_check;                   // some unmasked quality may lie below fast_qlo: check the bytes
     const uint16_t *llr16;          // [123] per-quality LLR term, 1/16 nat, rounded down
     int want_info;                  // single-strand: write every read's dcr_read_info (DCR_OPT_READ_INFO)
+    int direct_r;                   // single-strand records of at most this many reads go to the exact queue unstaged
 };
 
 template <bool DUPLEX> __global__ void k_recmeta(Args a);

@@ -3258,12 +3258,20 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
         sp.mark(0);
         if (DCR_STAMP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         sp.mark(1);                    // [0] wait for this record's prefetched bytes
-        const uint32_t bad = a.lo_check ? stage_codes<DUPLEX, true>(a, m0, st, lds, stage_addr, lane)
-                                        : stage_codes<DUPLEX, false>(a, m0, st, lds, stage_addr, lane);
-        // the read words go through LDS: a register copy of them would live
-        // across the prefetch's refill of st and force a wait for it at the
-        // loop's back edge
-        *(uint2 *)(lds + rm_addr + 8 * lane) = st.rm;
+        // single-strand records of at most direct_r reads almost never have
+        // every column decided by the bound (one to three reads stay below
+        // maxQ wherever a read is masked or disagrees): they go to the exact
+        // queue untouched instead of being staged here and again there
+        const bool direct = !EXACT && !DUPLEX && (int)(m0.w & 127u) <= a.direct_r;
+        uint32_t bad = 0;
+        if (!direct) {
+            bad = a.lo_check ? stage_codes<DUPLEX, true>(a, m0, st, lds, stage_addr, lane)
+                             : stage_codes<DUPLEX, false>(a, m0, st, lds, stage_addr, lane);
+            // the read words go through LDS: a register copy of them would live
+            // across the prefetch's refill of st and force a wait for it at the
+            // loop's back edge
+            *(uint2 *)(lds + rm_addr + 8 * lane) = st.rm;
+        }
         if (lane < 8) *(uint32_t *)(lds + fk::kMv + 32 * wave + 4 * lane) = st.mv;
         sp.mark(2);                    // [1] element codes into LDS
         __builtin_amdgcn_sched_barrier(0);
@@ -3279,6 +3287,16 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
         const uint2 rm = make_uint2((uint32_t)(((int)rw.x >> 16) + (m0.d0 & 0xFFFF)) | (rw.x & 0xFFFFu) << 8,
                                     rw.y - m0.base_al);
         const RecMeta m2 = meta_from_lanes(*(const uint32_t *)(lds + fk::kMv + 32 * wave + 4 * (lane & 7)));   // record i2
+        if (direct) {
+            if (lane == npend) pend = i;
+            if (++npend == kWave) flush(lane);
+            i += step;
+            if (i >= hi) break;
+            m0 = m1;
+            m1 = m2;
+            i2 = i3;
+            continue;
+        }
         const Staged sg = trim_record<DUPLEX, !EXACT>(a, m0, rm, bad, lds, stage_addr, lane);
         sp.mark(4);                    // [3] trim, fence
         if (sg.state == 1) {
