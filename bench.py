@@ -304,7 +304,9 @@ def main():
     import torch
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # ranks beyond the visible GPUs share them (the sharded CLI's rehearsal
+    # on a one-GPU box); counting devices does not initialise the GPU
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     dist = world > 1
     dev = f"cuda:{local}"
     tdist = None

@@ -51,6 +51,10 @@ EXPORTS = {
                                         ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64]),
     "dcr_inflater_last": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "dcr_inflater_totals": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "dcr_inflate_stream_open": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_void_p]),
+    "dcr_inflate_stream_add": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]),
+    "dcr_inflate_stream_fetch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]),
+    "dcr_inflate_stream_close": (None, [ctypes.c_void_p]),
 }
 
 # HIP-event slots of dcr_last_kernel_timing: k_recmeta<ss> includes k_prep_big,
@@ -184,7 +188,8 @@ BGZF_MEMBER_DTYPE = np.dtype([("in_off", "<i8"), ("out_off", "<i8"), ("in_len", 
 class InflateHook(ctypes.Structure):
     """include/dcr_inflate.h dcr_inflate_hook (filled by dcr_inflater_hook)."""
     _fields_ = [("user", ctypes.c_void_p), ("run", ctypes.c_void_p), ("host_alloc", ctypes.c_void_p),
-                ("host_free", ctypes.c_void_p)]
+                ("host_free", ctypes.c_void_p), ("stream_open", ctypes.c_void_p), ("stream_add", ctypes.c_void_p),
+                ("stream_fetch", ctypes.c_void_p), ("stream_close", ctypes.c_void_p)]
 
 
 def bgzf_members(data) -> tuple:

@@ -195,13 +195,13 @@ def gpu_inflate(device: int = 0):
     the device inflater and takes its chunk buffers page-locked from it).
     One inflater per process and device, kept like the backend.
 
-    Opt-in (DCR_GPU_INFLATE=1): measured on C2 it loses to the host pool
-    (profiles/r03g, r03h): a member takes ~4 ms of serial
-    decode on one wavefront, so a chunk's launch costs that much whatever its
-    size, and the whole-node pass got slower (180-193 vs 217-242 M consensus
-    bases/s with every member on the GPU; 210-232 vs 226-245 with the
-    adaptive GPU/host split)."""
-    if os.environ.get("DCR_GPU_INFLATE") != "1":
+    On by default, DCR_GPU_INFLATE=0 keeps the host inflate pool.  The
+    ingest streams the input's members to the device in spans launched ahead
+    of the reader: measured whole-node on C2 it beats the host
+    pool at input levels 1 and 6 (profiles/r03m).  A member is still ~4 ms of
+    serial decode on one wavefront, so the per-chunk launches tried first
+    lost (profiles/r03g, r03h)."""
+    if os.environ.get("DCR_GPU_INFLATE") == "0":
         if native_io._HOOK is not None:
             native_io.set_inflate_hook(None)
         return None

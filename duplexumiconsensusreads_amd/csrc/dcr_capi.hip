@@ -59,6 +59,15 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 int dcr::set_error(int code, const std::string &msg) { return fail(code, msg); }
 
+// The batch streams run at the device's highest priority: the input
+// inflater's long launches (include/dcr_inflate.h) share the GPU and a
+// batch's kernels should not queue behind spans inflated far ahead.
+static hipError_t hi_prio_stream(hipStream_t *s) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+}
+
 struct dcr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -233,7 +242,7 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
     c->device = device;
     if (const char *e = std::getenv("DCR_EXACT_DIRECT_R")) c->direct_r = std::atoi(e);   // A/B runs
     if (hipSetDevice(device) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hi_prio_stream(&c->stream) != hipSuccess ||
         hipMalloc(&c->d_params, sizeof(dcr_params)) != hipSuccess ||
         hipMalloc(&c->d_llr16, 128 * sizeof(uint16_t)) != hipSuccess ||
         hipMalloc(&c->d_wtab, DCR_LUT_N * sizeof(uint32_t)) != hipSuccess) {
@@ -678,9 +687,9 @@ int dcr_submit(dcr_ctx *c, int slot, const dcr_batch *h, dcr_out *hss, dcr_out *
     if (slot < 0 || slot >= DCR_MAX_SLOTS) return fail(DCR_EARG, "slot out of range");
     HIP_TRY(hipSetDevice(c->device));
     if (!c->s_h2d) {
-        HIP_TRY(hipStreamCreateWithFlags(&c->s_h2d, hipStreamNonBlocking));
-        HIP_TRY(hipStreamCreateWithFlags(&c->s_d2h, hipStreamNonBlocking));
-        HIP_TRY(hipStreamCreateWithFlags(&c->s_fetch, hipStreamNonBlocking));
+        HIP_TRY(hi_prio_stream(&c->s_h2d));
+        HIP_TRY(hi_prio_stream(&c->s_d2h));
+        HIP_TRY(hi_prio_stream(&c->s_fetch));
     }
     dcr_ctx::Slot &S = c->slots[slot];
     if (!S.ev_h2d) {
@@ -759,9 +768,9 @@ int dcr_submit_write(dcr_ctx *c, int slot, const dcr_batch *h, const dcr_wmeta *
     if (slot < 0 || slot >= DCR_MAX_SLOTS) return fail(DCR_EARG, "slot out of range");
     HIP_TRY(hipSetDevice(c->device));
     if (!c->s_h2d) {
-        HIP_TRY(hipStreamCreateWithFlags(&c->s_h2d, hipStreamNonBlocking));
-        HIP_TRY(hipStreamCreateWithFlags(&c->s_d2h, hipStreamNonBlocking));
-        HIP_TRY(hipStreamCreateWithFlags(&c->s_fetch, hipStreamNonBlocking));
+        HIP_TRY(hi_prio_stream(&c->s_h2d));
+        HIP_TRY(hi_prio_stream(&c->s_d2h));
+        HIP_TRY(hi_prio_stream(&c->s_fetch));
     }
     dcr_ctx::Slot &S = c->slots[slot];
     if (!S.ev_h2d) {

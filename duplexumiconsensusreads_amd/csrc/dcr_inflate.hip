@@ -14,8 +14,8 @@
 //     first codes by a lane scan, symbols sorted by (length, symbol), every
 //     10-bit root entry resolved by its own lane); literal/length root
 //     entries hold two literals when both codes fit the 10 bits;
-//   - the input read as 256-byte windows, one dword per lane, the next window
-//     prefetched; the bit buffer refilled by v_readlane;
+//   - the input read as 256-byte windows, one dword per lane (loaded when the
+//     bit buffer reaches them); the bit buffer refilled by v_readlane;
 //   - literals collected one per lane and written 64 at a time, matches
 //     copied by all lanes (a distance below 64 by its period);
 //   - the last 8 KiB of output kept in an LDS ring, the source of every match
@@ -26,8 +26,11 @@
 //   - ISIZE and CRC32 checked against the member trailer on the device.
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -222,7 +225,7 @@ __device__ __noinline__ bool build_table(const uint8_t *lens, int n, uint32_t *t
 // the wave's decoder state (all wave-uniform)
 struct Dec {
     __amdgpu_buffer_rsrc_t rs; // member input from a dword-aligned base; loads past its end read 0
-    uint32_t win, winn;       // this lane's dword of the current / next 256-byte window
+    uint32_t win;             // this lane's dword of the current 256-byte window
     uint32_t wbase;           // dword index of the current window
     uint32_t wi;              // next dword to enter the bit buffer
     uint64_t bb;
@@ -243,7 +246,6 @@ __device__ __forceinline__ void dec_start(Dec &d, const uint8_t *p, const uint8_
     d.rs = __builtin_amdgcn_make_buffer_rsrc((void *)d.base, (short)0, (int)extent, 0x00020000);
     const int lane = lane_id();
     d.win = __builtin_amdgcn_raw_buffer_load_b32(d.rs, 4 * lane, 0, 0);
-    d.winn = __builtin_amdgcn_raw_buffer_load_b32(d.rs, 4 * (kW + lane), 0, 0);
     d.wbase = 0;
     d.wi = 0;
     d.bb = 0;
@@ -256,9 +258,11 @@ __device__ __forceinline__ void refill(Dec &d) {
         d.nb += 32;
         ++d.wi;
         if (d.wi - d.wbase == kW) {
-            d.win = d.winn;
+            // the next window on demand (~300 tokens per window): a
+            // prefetched register would be copied at every loop back edge
+            // while in flight, i.e. a vmcnt(0) wait per token
             d.wbase += kW;
-            d.winn = __builtin_amdgcn_raw_buffer_load_b32(d.rs, 4 * (d.wbase + kW + lane_id()), 0, 0);
+            d.win = __builtin_amdgcn_raw_buffer_load_b32(d.rs, 4 * (d.wbase + lane_id()), 0, 0);
         }
     }
 }
@@ -458,8 +462,9 @@ __global__ __launch_bounds__(64) void k_inflate(Args a) {
         }
         sp.lap(0);                                        // block header, tables
         // Huffman-coded data
+        // (bounded without a guard: every symbol emits output, checked
+        // against ISIZE at least every 63 literals and at every match)
         for (;;) {
-            if (++guard > kGuard) { st = ST_GUARD; where = 3; break; }
             if (d.nb < 32) refill(d);
             uint32_t e = uni(s.lit[(uint32_t)d.bb & ((1u << kLB) - 1)]);
             uint32_t n = e & 31;
@@ -583,6 +588,29 @@ __global__ __launch_bounds__(64) void k_inflate(Args a) {
 }  // namespace dinf
 
 // ---- host side ---------------------------------------------------------------
+struct InflSlots {
+    static constexpr int kSlots = 4;
+    uint8_t *d_in[kSlots] = {}, *d_out[kSlots] = {}, *d_st[kSlots] = {};
+    dcr_bgzf_member *d_m[kSlots] = {};
+    size_t cap_in[kSlots] = {}, cap_out[kSlots] = {}, cap_m[kSlots] = {}, cap_dst[kSlots] = {};
+    uint8_t *h_stage[kSlots] = {}, *h_st[kSlots] = {};
+    size_t cap_stage[kSlots] = {}, cap_hst[kSlots] = {};
+    hipStream_t s_k = nullptr, s_out = nullptr;
+    bool busy = false;
+    void release() {
+        for (int i = 0; i < kSlots; ++i) {
+            if (d_in[i]) (void)hipFree(d_in[i]);
+            if (d_out[i]) (void)hipFree(d_out[i]);
+            if (d_st[i]) (void)hipFree(d_st[i]);
+            if (d_m[i]) (void)hipFree(d_m[i]);
+            if (h_stage[i]) (void)hipHostFree(h_stage[i]);
+            if (h_st[i]) (void)hipHostFree(h_st[i]);
+        }
+        if (s_k) (void)hipStreamDestroy(s_k);
+        if (s_out) (void)hipStreamDestroy(s_out);
+    }
+};
+
 struct dcr_inflater {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -597,6 +625,7 @@ struct dcr_inflater {
     int32_t last_n = 0;
     double tot[4] = {0, 0, 0, 0};     // kernel ms, runs, members, output bytes
     double stamp[16] = {};            // DINF_STAMP builds: summed dbg words
+    struct InflSlots *slots = nullptr;  // the streaming buffers (kept across streams)
     std::mutex mu;
     std::unordered_multimap<size_t, void *> free_host;   // page-locked buffers kept for later ingests
     std::unordered_map<void *, size_t> live_host;
@@ -656,6 +685,10 @@ void dcr_inflater_destroy(dcr_inflater *h) {
     if (h->d_dbg) (void)hipFree(h->d_dbg);
     for (auto &kv : h->free_host) (void)hipHostFree(kv.second);
     for (auto &kv : h->live_host) (void)hipHostFree(kv.first);
+    if (h->slots) {
+        h->slots->release();
+        delete h->slots;
+    }
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -757,6 +790,279 @@ extern "C" int dcr_inflater_stamps(dcr_inflater *h, double *out16, int reset) {
     return DINF_STAMP;
 }
 
+// ---- streaming: spans of members launched ahead of the reader ---------------
+// The reader's helper thread appends the input's members as it walks the
+// BGZF headers (stream_add).  The producer thread forms spans of them, copies
+// a span's compressed bytes out of the caller's mapping into page-locked
+// staging, uploads them and launches k_inflate into one of kSlots device
+// output slots; fetch waits for the spans that cover a range, checks their
+// members' statuses and copies the range out (DMA into the caller's
+// page-locked chunk buffer).  A slot is reused once every byte of its span
+// has been fetched.  The first spans are small (the reader starts early:
+// a member takes ~4 ms of serial decode whatever the launch size), the
+// others hold 4,096 members, enough to fill the device.  The slots' device
+// and page-locked buffers belong to the inflater and outlive the stream.
+struct dcr_inflate_stream {
+    static constexpr int kSlots = InflSlots::kSlots;
+    dcr_inflater *h = nullptr;
+    InflSlots *sl = nullptr;
+    const uint8_t *file = nullptr;
+    std::vector<dcr_bgzf_member> m;      // appended by stream_add
+    bool m_done = false;
+    struct Span {
+        int32_t m0 = 0, m1 = 0;
+        int64_t out0 = 0, out1 = 0, in0 = 0, in1 = 0;
+        bool launched = false, checked = false;
+        int rc = 0;
+        hipEvent_t start = nullptr, done = nullptr;
+    };
+    std::deque<Span> spans;             // formed by the producer (stable references)
+    std::vector<dcr_bgzf_member> mrel[kSlots];
+    std::thread producer;
+    std::mutex mu;
+    std::condition_variable cv;
+    int64_t fetched = 0;                // output bytes handed to the reader (monotonic)
+    bool stop = false, produced = false;
+    int err = 0;                        // producer-side runtime error
+};
+
+namespace {
+hipError_t pinned_grow(uint8_t *&p, size_t &cap, size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipHostMalloc((void **)&p, n, hipHostMallocDefault);
+    if (e == hipSuccess) cap = n;
+    return e;
+}
+
+void stream_produce(dcr_inflate_stream *st) {
+    dcr_inflater *h = st->h;
+    InflSlots &S = *st->sl;
+    (void)hipSetDevice(h->device);
+    int32_t mnext = 0;
+    for (size_t k = 0;; ++k) {
+        const int32_t want = k == 0 ? 128 : k == 1 ? 1024 : 4096;
+        dcr_inflate_stream::Span *spp;
+        {
+            std::unique_lock<std::mutex> lk(st->mu);
+            st->cv.wait(lk, [&] { return st->stop || st->m_done || (int32_t)st->m.size() - mnext >= want; });
+            if (st->stop || (st->m_done && mnext == (int32_t)st->m.size())) break;
+            dcr_inflate_stream::Span sp;
+            sp.m0 = mnext;
+            sp.m1 = std::min((int32_t)st->m.size(), mnext + want);
+            sp.out0 = st->m[sp.m0].out_off;
+            sp.out1 = st->m[sp.m1 - 1].out_off + st->m[sp.m1 - 1].isize;
+            sp.in0 = st->m[sp.m0].in_off;
+            sp.in1 = sp.in0;
+            for (int32_t i = sp.m0; i < sp.m1; ++i)
+                sp.in1 = std::max<int64_t>(sp.in1, st->m[i].in_off + st->m[i].in_len);
+            if (hipEventCreateWithFlags(&sp.done, hipEventBlockingSync) != hipSuccess ||
+                hipEventCreate(&sp.start) != hipSuccess) {
+                st->err = -1;
+                st->cv.notify_all();
+                return;
+            }
+            st->spans.push_back(sp);
+            spp = &st->spans.back();
+            // the slot's previous span must be fully read
+            st->cv.wait(lk, [&] {
+                return st->stop || k < (size_t)dcr_inflate_stream::kSlots ||
+                       st->fetched >= st->spans[k - dcr_inflate_stream::kSlots].out1;
+            });
+            if (st->stop) break;
+        }
+        auto &sp = *spp;
+        mnext = sp.m1;
+        const int slot = (int)(k % dcr_inflate_stream::kSlots);
+        const int32_t n = sp.m1 - sp.m0;
+        const size_t nin = (size_t)(sp.in1 - sp.in0), nout = (size_t)(sp.out1 - sp.out0);
+        if (pinned_grow(S.h_stage[slot], S.cap_stage[slot], nin + 16) != hipSuccess ||
+            pinned_grow(S.h_st[slot], S.cap_hst[slot], (size_t)n) != hipSuccess ||
+            grow(S.d_in[slot], S.cap_in[slot], nin + dinf::kPad) != hipSuccess ||
+            grow(S.d_out[slot], S.cap_out[slot], nout + 16) != hipSuccess ||
+            grow(S.d_m[slot], S.cap_m[slot], (size_t)n) != hipSuccess ||
+            grow(S.d_st[slot], S.cap_dst[slot], (size_t)n) != hipSuccess) {
+            std::lock_guard<std::mutex> g(st->mu);
+            st->err = -1;
+            st->cv.notify_all();
+            return;
+        }
+        std::memcpy(S.h_stage[slot], st->file + sp.in0, nin);
+        auto &mr = st->mrel[slot];
+        {
+            std::lock_guard<std::mutex> g(st->mu);
+            mr.assign(st->m.begin() + sp.m0, st->m.begin() + sp.m1);
+        }
+        for (auto &x : mr) {
+            x.in_off -= sp.in0;
+            x.out_off -= sp.out0;
+        }
+        dinf::Args a = h->base;
+        a.in = S.d_in[slot];
+        a.out = S.d_out[slot];
+        a.m = S.d_m[slot];
+        a.status = S.d_st[slot];
+        a.dbg = nullptr;
+        a.n = n;
+        (void)hipMemcpyAsync(S.d_in[slot], S.h_stage[slot], nin, hipMemcpyHostToDevice, S.s_k);
+        (void)hipMemcpyAsync(S.d_m[slot], mr.data(), (size_t)n * sizeof(dcr_bgzf_member), hipMemcpyHostToDevice, S.s_k);
+        (void)hipEventRecord(sp.start, S.s_k);
+        hipLaunchKernelGGL(dinf::k_inflate, dim3((unsigned)n), dim3(64), sizeof(dinf::WaveLds), S.s_k, a);
+        (void)hipMemcpyAsync(S.h_st[slot], S.d_st[slot], (size_t)n, hipMemcpyDeviceToHost, S.s_k);
+        (void)hipEventRecord(sp.done, S.s_k);
+        {
+            // the slot's staging and mrel are reused kSlots spans later,
+            // after the reader has fetched this span (its event done)
+            std::lock_guard<std::mutex> g(st->mu);
+            sp.launched = true;
+        }
+        st->cv.notify_all();
+    }
+    std::lock_guard<std::mutex> g(st->mu);
+    st->produced = true;
+    st->cv.notify_all();
+}
+}  // namespace
+
+extern "C" dcr_inflate_stream *dcr_inflate_stream_open(dcr_inflater *h, const uint8_t *file) {
+    if (!h || !file) {
+        dcr::set_error(DCR_EARG, "dcr_inflate_stream_open: bad arguments");
+        return nullptr;
+    }
+    {
+        std::lock_guard<std::mutex> g(h->mu);
+        if (!h->slots) h->slots = new InflSlots;
+        if (h->slots->busy) {            // one stream per inflater at a time
+            dcr::set_error(DCR_EARG, "dcr_inflate_stream_open: the inflater's stream is in use");
+            return nullptr;
+        }
+        h->slots->busy = true;
+    }
+    auto *st = new dcr_inflate_stream;
+    st->h = h;
+    st->sl = h->slots;
+    st->file = file;
+    (void)hipSetDevice(h->device);
+    if ((!st->sl->s_k && hipStreamCreateWithFlags(&st->sl->s_k, hipStreamNonBlocking) != hipSuccess) ||
+        (!st->sl->s_out && hipStreamCreateWithFlags(&st->sl->s_out, hipStreamNonBlocking) != hipSuccess)) {
+        dcr_inflate_stream_close(st);
+        dcr::set_error(DCR_EHIP, "dcr_inflate_stream_open: HIP setup failed");
+        return nullptr;
+    }
+    st->producer = std::thread(stream_produce, st);
+    return st;
+}
+
+extern "C" int dcr_inflate_stream_add(dcr_inflate_stream *st, const dcr_bgzf_member *m, int32_t n, int32_t last) {
+    if (!st || n < 0 || (n && !m)) return dcr::set_error(DCR_EARG, "dcr_inflate_stream_add: bad arguments");
+    for (int32_t i = 0; i < n; ++i)
+        if (m[i].isize > 65536 || m[i].in_off < 0 || m[i].out_off < 0)
+            return dcr::set_error(DCR_EARG, "dcr_inflate_stream_add: member out of range");
+    {
+        std::lock_guard<std::mutex> g(st->mu);
+        st->m.insert(st->m.end(), m, m + n);
+        if (last) st->m_done = true;
+    }
+    st->cv.notify_all();
+    return 0;
+}
+
+extern "C" int dcr_inflate_stream_fetch(dcr_inflate_stream *st, int64_t out_off, int64_t n, uint8_t *dst) {
+    if (!st || n < 0 || (n && !dst)) return -1;
+    if (n == 0) return 0;
+    (void)hipSetDevice(st->h->device);
+    InflSlots &S = *st->sl;
+    const int64_t end = out_off + n;
+    for (size_t k = 0;; ++k) {
+        dcr_inflate_stream::Span *spp;
+        {
+            std::unique_lock<std::mutex> lk(st->mu);
+            st->cv.wait(lk, [&] { return st->spans.size() > k || st->produced || st->err; });
+            if (st->spans.size() <= k) {
+                if (st->err) return -1;
+                dcr::set_error(DCR_EARG, "dcr_inflate_stream_fetch: range past the stream's members");
+                return -1;
+            }
+            spp = &st->spans[k];
+            if (spp->out0 >= end) break;
+            if (spp->out1 <= out_off) continue;
+            st->cv.wait(lk, [&] { return spp->launched || st->err; });
+            if (!spp->launched) return -1;
+        }
+        auto &sp = *spp;
+        const int slot = (int)(k % dcr_inflate_stream::kSlots);
+        if (!sp.checked) {
+            if (hipEventSynchronize(sp.done) != hipSuccess) return -1;
+            for (int32_t i = 0; i < sp.m1 - sp.m0; ++i)
+                if (S.h_st[slot][i] != dinf::ST_OK) {
+                    sp.rc = sp.m0 + i + 1;
+                    break;
+                }
+            sp.checked = true;
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, sp.start, sp.done);
+            std::lock_guard<std::mutex> g(st->h->mu);
+            st->h->tot[0] += ms;
+            st->h->tot[1] += 1;
+            st->h->tot[2] += sp.m1 - sp.m0;
+        }
+        if (sp.rc) {
+            dcr::set_error(DCR_EARG, "BGZF member " + std::to_string(sp.rc - 1) + " failed to inflate or CRC mismatch");
+            return sp.rc;
+        }
+        const int64_t a = std::max(out_off, sp.out0), b = std::min(end, sp.out1);
+        if (hipMemcpyAsync(dst + (a - out_off), S.d_out[slot] + (a - sp.out0), (size_t)(b - a), hipMemcpyDeviceToHost,
+                           S.s_out) != hipSuccess)
+            return -1;
+        if (sp.out1 >= end) break;
+    }
+    if (hipStreamSynchronize(S.s_out) != hipSuccess) return -1;
+    {
+        std::lock_guard<std::mutex> g(st->mu);
+        st->fetched = std::max(st->fetched, end);
+    }
+    st->cv.notify_all();
+    std::lock_guard<std::mutex> g(st->h->mu);
+    st->h->tot[3] += (double)n;
+    return 0;
+}
+
+extern "C" void dcr_inflate_stream_close(dcr_inflate_stream *st) {
+    if (!st) return;
+    {
+        std::lock_guard<std::mutex> g(st->mu);
+        st->stop = true;
+    }
+    st->cv.notify_all();
+    if (st->producer.joinable()) st->producer.join();
+    (void)hipSetDevice(st->h->device);
+    if (st->sl->s_k) (void)hipStreamSynchronize(st->sl->s_k);
+    if (st->sl->s_out) (void)hipStreamSynchronize(st->sl->s_out);
+    for (auto &sp : st->spans)
+    {
+        if (sp.start) (void)hipEventDestroy(sp.start);
+        if (sp.done) (void)hipEventDestroy(sp.done);
+    }
+    {
+        std::lock_guard<std::mutex> g(st->h->mu);
+        st->sl->busy = false;
+    }
+    delete st;
+}
+
+static void *hook_stream_open(void *u, const uint8_t *file) {
+    return dcr_inflate_stream_open((dcr_inflater *)u, file);
+}
+static int hook_stream_add(void *s, const dcr_bgzf_member *m, int32_t n, int32_t last) {
+    return dcr_inflate_stream_add((dcr_inflate_stream *)s, m, n, last);
+}
+static int hook_stream_fetch(void *s, int64_t off, int64_t n, uint8_t *dst) {
+    return dcr_inflate_stream_fetch((dcr_inflate_stream *)s, off, n, dst);
+}
+static void hook_stream_close(void *s) { dcr_inflate_stream_close((dcr_inflate_stream *)s); }
+
 static int hook_run(void *u, const uint8_t *in, int64_t in_bytes, const dcr_bgzf_member *m, int32_t n, uint8_t *out,
                     int64_t out_bytes) {
     const int r = dcr_inflater_run((dcr_inflater *)u, in, in_bytes, m, n, out, out_bytes);
@@ -792,6 +1098,10 @@ int dcr_inflater_hook(dcr_inflater *h, dcr_inflate_hook *hook) {
     hook->run = hook_run;
     hook->host_alloc = hook_alloc;
     hook->host_free = hook_free;
+    hook->stream_open = hook_stream_open;
+    hook->stream_add = hook_stream_add;
+    hook->stream_fetch = hook_stream_fetch;
+    hook->stream_close = hook_stream_close;
     return 0;
 }
 

@@ -478,7 +478,8 @@ class Inflater {
             if (!c.pin) c.buf.resize(kHead + want_max_ + 0x10000);
             empty_.push_back(&c);
         }
-        if (gpu_) {
+        if (gpu_ && map_ && hook_.stream_open) open_stream();
+        if (gpu_ && !stream_) {
             stage_cap_ = want_max_ + ((size_t)1 << 20);
             if (hook_.host_alloc) stage_pin_ = (uint8_t *)hook_.host_alloc(hook_.user, stage_cap_);
             if (!stage_pin_) stage_.resize(stage_cap_);
@@ -494,6 +495,9 @@ class Inflater {
         cv_.notify_all();
         th_.join();
         sth_.join();
+        stop_members_ = true;
+        if (mth_.joinable()) mth_.join();
+        if (stream_) hook_.stream_close(stream_);          // before the mapping it reads goes away
         if (map_) munmap((void *)map_, map_len_);
         if (hook_.host_free) {
             for (auto &c : chunks_)
@@ -502,6 +506,61 @@ class Inflater {
         }
     }
     bool gpu() const { return gpu_; }
+
+    // A mapped input's members for the device inflater's stream
+    // (dcr_inflate_hook.stream_*): a helper thread walks the BGZF headers
+    // (the walk fill() makes chunk by chunk) and appends them in batches, the
+    // first small so the first launch starts at once.  On anything
+    // unexpected it stops appending; fill()'s own walk then reports it.
+    void open_stream() {
+        stream_ = hook_.stream_open(hook_.user, map_);
+        if (!stream_) return;
+        stream_out_ = 0;
+        mth_ = std::thread([this] { scan_members(); });
+    }
+    void scan_members() {
+        std::vector<dcr_bgzf_member> ms;
+        size_t p = cbeg_;
+        int64_t out = 0;
+        size_t batch = 128;
+        auto flush = [&](bool last) {
+            hook_.stream_add(stream_, ms.data(), (int32_t)ms.size(), last ? 1 : 0);
+            ms.clear();
+        };
+        while (p + 18 <= cend_ && !stop_members_.load(std::memory_order_relaxed)) {
+            if (end_coff_ >= 0 && p >= (uint64_t)end_coff_) {
+                if (p != (uint64_t)end_coff_ || end_uoff_ == 0) break;
+            }
+            const uint8_t *h = map_ + p;
+            if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) break;
+            const size_t xlen = rd16(h + 10);
+            if (cend_ - p < 12 + xlen) break;
+            long bsize = -1;
+            for (size_t i = 0; i + 4 <= xlen;) {
+                const uint8_t *sf = h + 12 + i;
+                const size_t slen = rd16(sf + 2);
+                if (sf[0] == 66 && sf[1] == 67 && slen == 2) bsize = rd16(sf + 4);
+                i += 4 + slen;
+            }
+            if (bsize < 0) break;
+            const size_t blen = (size_t)bsize + 1;
+            if (blen < 12 + xlen + 8 || cend_ - p < blen) break;
+            const uint32_t isize = rd32(h + blen - 4);
+            if (isize > 0x10000) break;
+            ms.push_back(dcr_bgzf_member{(int64_t)(p + 12 + xlen), out, (uint32_t)(blen - 12 - xlen - 8), isize,
+                                         rd32(h + blen - 8), 0});
+            out += isize;
+            const bool last_of_range = end_coff_ >= 0 && p == (uint64_t)end_coff_;
+            p += blen;
+            if (last_of_range) break;
+            if (ms.size() >= batch) {
+                flush(false);
+                batch = 1024;
+            }
+        }
+        flush(true);
+    }
+
     Chunk *next() {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return !full_.empty(); });
@@ -674,13 +733,11 @@ class Inflater {
         struct Blk { size_t coff, clen, doff; uint32_t isize, crc; };
         std::vector<Blk> blks;
         size_t total = 0, cut = SIZE_MAX;
-        size_t range0 = 0;              // the blocks' compressed bytes: [range0, cbeg_) of cdata()
         if (range_done_) { c.eof = true; return; }
         // compressed bytes are only moved while no parsed block points into them
         if (!file_eof_ && cend_ - cbeg_ < cbuf_.size() / 2) top_up();
         for (;;) {
             while (!range_done_ && cend_ - cbeg_ >= 18 && total + 0x10000 <= want_) {
-                if (blks.empty()) range0 = cbeg_;
                 if (end_coff_ >= 0 && cpos_ + cbeg_ >= (uint64_t)end_coff_) {
                     // the range's last block: only its first end_uoff bytes
                     range_done_ = true;
@@ -732,7 +789,16 @@ class Inflater {
             return libdeflate_crc32(0, dst + b.doff, b.isize) == b.crc;
         };
         bool ok = true;
-        if (gpu_ && !blks.empty()) {
+        if (stream_ && !blks.empty()) {
+            // inflated ahead by the device: copy this chunk's bytes out
+            const size_t out_blocks = blks.back().doff + blks.back().isize - kHead;
+            const int rc = hook_.stream_fetch(stream_, stream_out_, (int64_t)out_blocks, dst + kHead);
+            if (rc != 0) {
+                c.err = rc > 0 ? "BGZF block failed to inflate or CRC mismatch" : "GPU inflate failed";
+                return;
+            }
+            stream_out_ += (int64_t)out_blocks;
+        } else if (gpu_ && !blks.empty()) {
             // the chunk's first k members inflate on the GPU (their compressed
             // bytes copied to page-locked staging by the pool first; CRC32 and
             // ISIZE checked on the device; output straight into the chunk
@@ -812,6 +878,10 @@ class Inflater {
     HugeBuf stage_;
     size_t stage_cap_ = 0;
     std::vector<dcr_bgzf_member> mem_;
+    void *stream_ = nullptr;           // the device inflater's stream over the whole mapped input
+    std::thread mth_;                  // appends the input's members to stream_
+    std::atomic<bool> stop_members_{false};
+    int64_t stream_out_ = 0;           // output bytes fetched from it so far
     double frac_ = 0.5;                // share of a chunk's members inflated on the GPU
     bool frac_fixed_ = false;          // DCR_GPU_INFLATE_FRAC set: no adaptation
     HugeBuf cbuf_;

@@ -47,6 +47,18 @@ typedef struct dcr_inflate_hook {
                int64_t out_bytes);
     void *(*host_alloc)(void *user, size_t bytes);
     void (*host_free)(void *user, void *p);
+    /* streaming (a mapped input): stream_open starts a stream over `file`;
+     * stream_add appends members in input order (in_off from `file`, out_off
+     * from the first member's output; last != 0 after the final ones), which
+     * the device inflates ahead of the reader in large launches on its own
+     * thread; stream_fetch blocks until output bytes [out_off, out_off + n)
+     * are inflated and copies them to dst (page-locked: a DMA), returning 0,
+     * the index + 1 of a failed member, or -1; stream_close stops and frees.
+     * NULL stream_open: chunks go through run. */
+    void *(*stream_open)(void *user, const uint8_t *file);
+    int (*stream_add)(void *stream, const dcr_bgzf_member *m, int32_t n, int32_t last);
+    int (*stream_fetch)(void *stream, int64_t out_off, int64_t n, uint8_t *dst);
+    void (*stream_close)(void *stream);
 } dcr_inflate_hook;
 
 /* libdcr.so: a device inflater (one per process and device; its streams,
@@ -62,6 +74,12 @@ int dcr_inflater_hook(dcr_inflater *h, dcr_inflate_hook *hook);
  * it), or -DCR_E* for bad arguments or a runtime error */
 int dcr_inflater_run(dcr_inflater *h, const uint8_t *in, int64_t in_bytes, const dcr_bgzf_member *m, int32_t n,
                      uint8_t *out, int64_t out_bytes);
+/* the streaming entry points behind dcr_inflate_hook.stream_* */
+typedef struct dcr_inflate_stream dcr_inflate_stream;
+dcr_inflate_stream *dcr_inflate_stream_open(dcr_inflater *h, const uint8_t *file);
+int dcr_inflate_stream_add(dcr_inflate_stream *st, const dcr_bgzf_member *m, int32_t n, int32_t last);
+int dcr_inflate_stream_fetch(dcr_inflate_stream *st, int64_t out_off, int64_t n, uint8_t *dst);
+void dcr_inflate_stream_close(dcr_inflate_stream *st);
 /* device time of the last run's kernel (ms) and its member count */
 int dcr_inflater_last(dcr_inflater *h, float *kernel_ms, int32_t *n_members);
 /* totals since creation or the last reset: out4 = {kernel ms, runs, members,

@@ -19,7 +19,7 @@ for lvl in $LEVELS; do
 done
 timeout -k 10 200 python3 -u -m pytest tests/test_gpu_inflate.py -x -q --timeout 60 --timeout-method thread > "$O/pytest.log" 2>&1 || { tail -20 "$O/pytest.log"; exit 1; }
 tail -1 "$O/pytest.log"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/kt" -o kt --output-format csv -- python3 bench.py --no-cpu --kernel-steps 2 --steps 2 --warmup 1 > "$O/prof.json" 2> "$O/prof.log" || { echo "prof failed"; tail -20 "$O/prof.log"; exit 1; }
+DCR_GPU_INFLATE=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/kt" -o kt --output-format csv -- python3 bench.py --no-cpu --kernel-steps 2 --steps 2 --warmup 1 > "$O/prof.json" 2> "$O/prof.log" || { echo "prof failed"; tail -20 "$O/prof.log"; exit 1; }
 find "$O/kt" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats.csv" \;
 find "$O/kt" -name "*kernel_trace.csv" -exec python3 tools/kt_grid.py {} k_inflate k_deflate k_consensus_fast \; > "$O/kernel_grid.csv"
 rm -rf "$O/kt"
