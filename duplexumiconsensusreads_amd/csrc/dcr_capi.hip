@@ -931,10 +931,12 @@ int dcr_slot_fetch(dcr_ctx *c, int slot, int what, int64_t off, int64_t n, void 
 
 // diagnostic (not in include/dcr.h): k_deflate alone over n host bytes with
 // per-phase s_memtime cycle totals (summed over workgroups) and the HIP-event
-// time; returns the compressed bytes in *comp_bytes
-int dcr_deflate_probe(dcr_ctx *c, const uint8_t *host, int64_t n, unsigned long long *stamps10, float *ms,
-                      int64_t *comp_bytes) {
-    if (!c || !host || n <= 0 || !stamps10 || !ms || !comp_bytes) return fail(DCR_EARG, "bad argument");
+// time; returns the compressed bytes in *comp_bytes and, when slots_out is
+// given (ceil(n / 0xff00) * 65536 bytes), each block's BGZF member at the
+// start of its 64 KiB slot, the member sizes in sizes_out
+int dcr_deflate_probe(dcr_ctx *c, const uint8_t *host, int64_t n, unsigned long long *stamps12, float *ms,
+                      int64_t *comp_bytes, uint8_t *slots_out, int64_t *sizes_out) {
+    if (!c || !host || n <= 0 || !stamps12 || !ms || !comp_bytes) return fail(DCR_EARG, "bad argument");
     HIP_TRY(hipSetDevice(c->device));
     const int64_t nb = (n + dfl::kMaxIn - 1) / dfl::kMaxIn;
     uint8_t *d_in = nullptr, *d_slots = nullptr;
@@ -945,12 +947,12 @@ int dcr_deflate_probe(dcr_ctx *c, const uint8_t *host, int64_t n, unsigned long 
     HIP_TRY(hipMalloc(&d_slots, (size_t)nb * dfl::kSlot));
     HIP_TRY(hipMalloc(&d_n, 8));
     HIP_TRY(hipMalloc(&d_sizes, 8 * (size_t)nb));
-    HIP_TRY(hipMalloc(&d_st, 8 * 10));
+    HIP_TRY(hipMalloc(&d_st, 8 * 12));
     const unsigned gd = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nb, (int64_t)c->n_cu * c->dfl_blocks));
     HIP_TRY(hipMalloc(&d_tok, (size_t)gd * dfl::kTokWords * 4));
     HIP_TRY(hipMemcpy(d_in, host, (size_t)n, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(d_n, &n, 8, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemset(d_st, 0, 80));
+    HIP_TRY(hipMemset(d_st, 0, 96));
     dcrw::DflArgs D{d_in, d_n, d_slots, d_sizes, d_tok, d_st};
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
@@ -961,12 +963,14 @@ int dcr_deflate_probe(dcr_ctx *c, const uint8_t *host, int64_t n, unsigned long 
     HIP_TRY(hipEventRecord(e1, c->stream));
     HIP_TRY(hipEventSynchronize(e1));
     HIP_TRY(hipEventElapsedTime(ms, e0, e1));
-    HIP_TRY(hipMemcpy(stamps10, d_st, 80, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(stamps12, d_st, 96, hipMemcpyDeviceToHost));
     std::vector<int64_t> sz((size_t)nb);
     HIP_TRY(hipMemcpy(sz.data(), d_sizes, 8 * (size_t)nb, hipMemcpyDeviceToHost));
     int64_t tot = 0;
     for (int64_t v : sz) tot += v;
     *comp_bytes = tot;
+    if (sizes_out) std::memcpy(sizes_out, sz.data(), 8 * (size_t)nb);
+    if (slots_out) HIP_TRY(hipMemcpy(slots_out, d_slots, (size_t)nb * dfl::kSlot, hipMemcpyDeviceToHost));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipFree(d_in);

@@ -52,14 +52,26 @@
 
 namespace dfl {
 
-constexpr int kT = 256;                   // lanes per block
+#ifndef DFL_T
+#define DFL_T 256
+#endif
+#ifndef DFL_LS
+#define DFL_LS 32
+#endif
+#ifndef DFL_MW
+#define DFL_MW 4                           // dwords per side per match-extension step
+#endif
+constexpr int kT = DFL_T;                 // lanes per block
 constexpr uint32_t kMaxIn = 0xff00;       // input bytes per BGZF block
-constexpr int kHB = 11;
+#ifndef DFL_HB
+#define DFL_HB 11
+#endif
+constexpr int kHB = DFL_HB;
 constexpr int kHN = 1 << kHB;
 constexpr uint32_t kNone = 0xffffffffu;
 constexpr uint32_t kSlot = 65536;         // output slot bytes (one BGZF block at most)
 constexpr uint32_t kMaxDeflate = kSlot - 26;
-constexpr int kLS = 32;                   // lane-private recency table: sets x 2 ways
+constexpr int kLS = DFL_LS;               // lane-private recency table: sets x 2 ways
 // tokens per lane: <= 63 matches (>= 4 bytes each in <= 255 bytes) and the
 // tail literal run; entry e of lane l at tok[e * kT + l]:
 //   bit 31 tail | bits 23..30 literal run before | 15..22 length - 4 | 0..14 distance - 1
@@ -67,7 +79,7 @@ constexpr int kTokE = 64;
 constexpr uint32_t kTokWords = (uint32_t)kTokE * kT;
 
 struct alignas(16) Shared {
-    uint8_t in[kMaxIn + 32];              // zero padding: match_len reads past the end
+    uint8_t in[kMaxIn + 4 * DFL_MW + 32];   // zero padding: match_len reads past the end
     union {
         struct {
             uint32_t a_min[kHN], a_max[kHN], b_min[kHN];   // positions (a_max: position + 1, 0 none)
@@ -78,6 +90,7 @@ struct alignas(16) Shared {
     uint32_t lit_freq[288], dist_freq[32];
     uint8_t lit_len[288], dist_len[32], cl_len[19];
     uint16_t lit_code[288], dist_code[32], cl_code[19];   // bit-reversed (LSB-first) codes
+    uint32_t lit_cl[288], dist_cl[32];    // code | length << 16: one LDS load per symbol in P4 / P5
     uint32_t lane_bits[kT];
     uint32_t lane_off[kT];
     uint32_t lane_crc[kT];
@@ -196,34 +209,44 @@ DFL_HD inline void lane_range(uint32_t n, int lane, uint32_t &lo, uint32_t &hi) 
 }
 
 // length of the common prefix of in[c..] and in[p..], at most lim (reads
-// stay below p + lim + 20 <= n + 20, inside the zero padding of in[])
+// stay below p + lim + 4 * kMW + 4 <= n + 4 * kMW + 4, inside the zero padding of in[])
 DFL_HD inline uint32_t match_len(const Shared &s, uint32_t c, uint32_t p, uint32_t lim) {
 #if DFL_DEVICE
-    // 16 bytes per step: four new aligned LDS dwords per side issued
+    // kMW * 4 bytes per step: kMW new aligned LDS dwords per side issued
     // together (one LDS round trip), byte funnel shifts, the first
-    // differing byte from the lowest set bit of the xor
+    // differing byte from the lowest set bit of the xor.  The workgroup is
+    // alone on its CU (LDS), so registers are plentiful and a wide step
+    // shortens the longest match of a wave, which every lane waits for.
+    constexpr int kMW = DFL_MW;
     const uint32_t *w = reinterpret_cast<const uint32_t *>(s.in);
     uint32_t ia = c >> 2, ib = p >> 2;
     const uint32_t sa = c & 3, sb = p & 3;
     uint32_t a0 = w[ia], b0 = w[ib], l = 0;
     while (l < lim) {
-        const uint32_t a1 = w[ia + 1], a2 = w[ia + 2], a3 = w[ia + 3], a4 = w[ia + 4];
-        const uint32_t b1 = w[ib + 1], b2 = w[ib + 2], b3 = w[ib + 3], b4 = w[ib + 4];
-        const uint32_t x0 = __builtin_amdgcn_alignbyte(a1, a0, sa) ^ __builtin_amdgcn_alignbyte(b1, b0, sb);
-        const uint32_t x1 = __builtin_amdgcn_alignbyte(a2, a1, sa) ^ __builtin_amdgcn_alignbyte(b2, b1, sb);
-        const uint32_t x2 = __builtin_amdgcn_alignbyte(a3, a2, sa) ^ __builtin_amdgcn_alignbyte(b3, b2, sb);
-        const uint32_t x3 = __builtin_amdgcn_alignbyte(a4, a3, sa) ^ __builtin_amdgcn_alignbyte(b4, b3, sb);
-        if (x0 | x1 | x2 | x3) {
-            const uint32_t k = x0 ? 0 : x1 ? 4 : x2 ? 8 : 12;
-            const uint32_t x = x0 ? x0 : x1 ? x1 : x2 ? x2 : x3;
-            l += k + ((uint32_t)__builtin_ctz(x) >> 3);
+        uint32_t a[kMW + 1], b[kMW + 1], x[kMW];
+        a[0] = a0;
+        b[0] = b0;
+DFL_UNROLL
+        for (int k = 1; k <= kMW; ++k) { a[k] = w[ia + k]; b[k] = w[ib + k]; }
+        uint32_t any = 0;
+DFL_UNROLL
+        for (int k = 0; k < kMW; ++k) {
+            x[k] = __builtin_amdgcn_alignbyte(a[k + 1], a[k], sa) ^ __builtin_amdgcn_alignbyte(b[k + 1], b[k], sb);
+            any |= x[k];
+        }
+        if (any) {
+            uint32_t kk = kMW - 1, xx = x[kMW - 1];
+DFL_UNROLL
+            for (int k = kMW - 2; k >= 0; --k)
+                if (x[k]) { kk = (uint32_t)k; xx = x[k]; }
+            l += 4 * kk + ((uint32_t)__builtin_ctz(xx) >> 3);
             break;
         }
-        l += 16;
-        ia += 4;
-        ib += 4;
-        a0 = a4;
-        b0 = b4;
+        l += 4 * kMW;
+        ia += kMW;
+        ib += kMW;
+        a0 = a[kMW];
+        b0 = b[kMW];
     }
     return l < lim ? l : lim;
 #else
@@ -233,21 +256,26 @@ DFL_HD inline uint32_t match_len(const Shared &s, uint32_t c, uint32_t p, uint32
 #endif
 }
 
-DFL_HD inline int len_sym(uint32_t len) {   // 0..28 (symbol 257 + i)
-    int lo = 0, hi = 28;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (kLenBase[mid] <= len) lo = mid; else hi = mid - 1;
-    }
-    return lo;
+// Length / distance symbols by arithmetic (RFC 1951 3.2.5; the tables above
+// are its listing): the tables are in global memory on the device, and a
+// binary search over them was a chain of dependent loads per match in each
+// of the three passes over the tokens.
+struct Sym {
+    uint32_t sym, nb, ev;   // symbol (0-based), extra bits, extra value
+};
+DFL_HD inline uint32_t log2u(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
+DFL_HD inline Sym len_code(uint32_t len) {     // len 3..258 -> symbol 257 + sym
+    const uint32_t x = len - 3;
+    if (x < 8) return {x, 0, 0};
+    if (len == 258) return {28, 0, 0};
+    const uint32_t e = log2u(x);               // 3..7
+    return {4 * (e - 1) + ((x >> (e - 2)) & 3), e - 2, x & ((1u << (e - 2)) - 1)};
 }
-DFL_HD inline int dist_sym(uint32_t d) {    // 0..29
-    int lo = 0, hi = 29;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (kDistBase[mid] <= d) lo = mid; else hi = mid - 1;
-    }
-    return lo;
+DFL_HD inline Sym dist_code(uint32_t d) {      // d 1..32768
+    const uint32_t x = d - 1;
+    if (x < 4) return {x, 0, 0};
+    const uint32_t e = log2u(x);               // 2..14
+    return {2 * e + ((x >> (e - 1)) & 1), e - 1, x & ((1u << (e - 1)) - 1)};
 }
 
 // lane-private recency table (deterministic: one lane, positions in order)
@@ -282,11 +310,26 @@ DFL_HD inline void parse(Shared &s, uint32_t n, int lane, uint32_t lo, uint32_t 
     while (p < hi) {
         const uint32_t lim = (hi - p) < 258 ? (hi - p) : 258;
         const bool hashed = p + 4 <= n;
+#if DFL_DEVICE
+        // the dwords around p: the bytes at p (vp) and at p - 1 .. p - 4
+        // (the distance 1-4 candidates) without further loads
+        const uint32_t *wi = reinterpret_cast<const uint32_t *>(s.in);
+        const uint32_t pi = p >> 2, sh = p & 3;
+        const uint32_t W0 = pi ? wi[pi - 1] : 0u, W1 = wi[pi], W2 = wi[pi + 1];
+        const uint32_t vp = __builtin_amdgcn_alignbyte(W2, W1, sh);
+#else
         const uint32_t vp = ld32(s, p);
+#endif
         const uint32_t h = hashed ? hash4(vp) : 0;
         const uint32_t set = (h & (kLS - 1)) * 2;
         uint32_t best = 0, bd = 0;
-        const uint32_t t0 = t[set], t1 = t[set + 1];
+        // the set's two ways in one dword (t0 the latest)
+#if DFL_DEVICE
+        const uint32_t tw = *reinterpret_cast<const uint32_t *>(t + set);
+#else
+        const uint32_t tw = t[set] | (uint32_t)t[set + 1] << 16;
+#endif
+        const uint32_t t0 = tw & 0xffff, t1 = tw >> 16;
         if (lim >= 4) {
             uint32_t c[8];
             c[0] = t0 ? t0 - 1 : kNone;
@@ -303,8 +346,20 @@ DFL_UNROLL
             for (int k = 1; k <= 4; ++k) c[3 + k] = p >= (uint32_t)k ? p - (uint32_t)k : kNone;
             uint32_t ok = 0;
 DFL_UNROLL
-            for (int i = 0; i < 8; ++i)
+            for (int i = 0; i < 4; ++i)
                 if (c[i] != kNone && c[i] < p && p - c[i] <= 32768 && ld32(s, c[i]) == vp) ok |= 1u << i;
+DFL_UNROLL
+            for (int k = 1; k <= 4; ++k) {
+#if DFL_DEVICE
+                // bytes p - k .. p - k + 3 from W0 W1 W2 (offset 4 + sh - k in W0)
+                const uint32_t off = 4 + sh - (uint32_t)k;
+                const uint32_t vk = off < 4 ? __builtin_amdgcn_alignbyte(W1, W0, off)
+                                            : __builtin_amdgcn_alignbyte(W2, W1, off - 4);
+#else
+                const uint32_t vk = p >= (uint32_t)k ? ld32(s, p - (uint32_t)k) : 0u;
+#endif
+                if (p >= (uint32_t)k && vk == vp) ok |= 1u << (3 + k);
+            }
 DFL_UNROLL
             for (int i = 0; i < 8; ++i) {
                 if (!((ok >> i) & 1) || best >= lim) continue;
@@ -314,14 +369,18 @@ DFL_UNROLL
             }
         }
         if (hashed) {                                       // lt_insert(t, h, p)
+#if DFL_DEVICE
+            *reinterpret_cast<uint32_t *>(t + set) = (t0 << 16) | (p + 1);
+#else
             t[set + 1] = (uint16_t)t0;
             t[set] = (uint16_t)(p + 1);
+#endif
         }
         if (best >= 4) {
             v.match(best, bd);
             p += best;
         } else {
-            v.lit(s.in[p]);
+            v.lit((uint8_t)vp);   // the byte at p (vp's low byte, also past n: zero padding)
             ++p;
         }
     }
@@ -332,10 +391,10 @@ struct CountV {            // P2: symbol histogram, extra bits
     uint32_t extra = 0;
     DFL_HD void lit(uint8_t b) { aadd(&s.lit_freq[b], 1); }
     DFL_HD void match(uint32_t len, uint32_t d) {
-        const int ls = len_sym(len), ds = dist_sym(d);
-        aadd(&s.lit_freq[257 + ls], 1);
-        aadd(&s.dist_freq[ds], 1);
-        extra += kLenExtra[ls] + kDistExtra[ds];
+        const Sym L = len_code(len), D = dist_code(d);
+        aadd(&s.lit_freq[257 + L.sym], 1);
+        aadd(&s.dist_freq[D.sym], 1);
+        extra += L.nb + D.nb;
     }
 };
 
@@ -363,10 +422,14 @@ struct CountTokV {         // P2: both
 template <class V>
 DFL_HD inline void replay(const Shared &s, const uint32_t *t, int lane, uint32_t lo, V &v) {
     uint32_t p = lo;
+    uint32_t xn = t[lane];
     for (int e = 0; e < kTokE; ++e) {
-        const uint32_t x = t[e * kT + lane];
+        // the next entry's load is in flight while this one is replayed
+        // (entries past the tail hold stale words, never used)
+        const uint32_t x = xn;
+        if (e + 1 < kTokE) xn = t[(e + 1) * kT + lane];
         const uint32_t run = (x >> 23) & 255;
-        for (uint32_t q = 0; q < run; ++q) v.lit(s.in[p + q]);
+        v.lits(p, run);
         p += run;
         if (x >> 31) break;
         const uint32_t len = ((x >> 15) & 255) + 4;
@@ -375,13 +438,32 @@ DFL_HD inline void replay(const Shared &s, const uint32_t *t, int lane, uint32_t
     }
 }
 
+// A literal run of a replay, four bytes per step: one unaligned dword of
+// the block, then the four symbols' table entries loaded together.
+template <class F>
+DFL_HD inline void lit_run(const Shared &s, uint32_t p, uint32_t run, F &&f) {
+    uint32_t q = 0;
+    for (; q + 4 <= run; q += 4) {
+        const uint32_t w = ld32(s, p + q);
+        const uint32_t e0 = s.lit_cl[w & 255], e1 = s.lit_cl[(w >> 8) & 255], e2 = s.lit_cl[(w >> 16) & 255],
+                       e3 = s.lit_cl[w >> 24];
+        f(e0);
+        f(e1);
+        f(e2);
+        f(e3);
+    }
+    for (; q < run; ++q) f(s.lit_cl[s.in[p + q]]);
+}
+
 struct BitsV {             // P4: bits of a lane's tokens
     const Shared &s;
     uint32_t bits = 0;
-    DFL_HD void lit(uint8_t b) { bits += s.lit_len[b]; }
+    DFL_HD void lits(uint32_t p, uint32_t run) {
+        lit_run(s, p, run, [&](uint32_t e) { bits += e >> 16; });
+    }
     DFL_HD void match(uint32_t len, uint32_t d) {
-        const int ls = len_sym(len), ds = dist_sym(d);
-        bits += s.lit_len[257 + ls] + kLenExtra[ls] + s.dist_len[ds] + kDistExtra[ds];
+        const Sym L = len_code(len), D = dist_code(d);
+        bits += (s.lit_cl[257 + L.sym] >> 16) + L.nb + (s.dist_cl[D.sym] >> 16) + D.nb;
     }
 };
 
@@ -424,40 +506,69 @@ struct BitOut {
 struct EmitV {             // P5: write a lane's tokens
     const Shared &s;
     BitOut &o;
-    DFL_HD void lit(uint8_t b) { o.put(s.lit_code[b], s.lit_len[b]); }
+    DFL_HD void lits(uint32_t p, uint32_t run) {
+        lit_run(s, p, run, [&](uint32_t e) { o.put(e & 0xffff, e >> 16); });
+    }
     DFL_HD void match(uint32_t len, uint32_t d) {
-        const int ls = len_sym(len), ds = dist_sym(d);
-        o.put(s.lit_code[257 + ls], s.lit_len[257 + ls]);
-        o.put(len - kLenBase[ls], kLenExtra[ls]);
-        o.put(s.dist_code[ds], s.dist_len[ds]);
-        o.put(d - kDistBase[ds], kDistExtra[ds]);
+        const Sym L = len_code(len), D = dist_code(d);
+        const uint32_t le = s.lit_cl[257 + L.sym], de = s.dist_cl[D.sym];
+        o.put(le & 0xffff, le >> 16);
+        o.put(L.ev, L.nb);
+        o.put(de & 0xffff, de >> 16);
+        o.put(D.ev, D.nb);
     }
 };
 
-// ---- Huffman code lengths (thread 0) ----------------------------------------------
+// ---- Huffman code lengths (one wave) ----------------------------------------------
+// The serial code below runs on one lane.  DFL_SERIAL_WAVE=1 runs it on a
+// whole wave with the same data in every lane instead: each LDS read goes
+// through DFL_U() (readfirstlane), so indices and loop bounds live in scalar
+// registers and the branches are scalar; every lane stores the same value to
+// the same address.  That measured slower (readfirstlane after each LDS
+// load), so one lane it is.  The host emulation runs it once (lane 0).
+#ifndef DFL_SERIAL_WAVE
+#define DFL_SERIAL_WAVE 0      // 1: a whole wave with readfirstlane reads (measured slower: 6.95 vs 6.56 ms)
+#endif
+#if DFL_DEVICE && DFL_SERIAL_WAVE
+#define DFL_U(x) __builtin_amdgcn_readfirstlane((uint32_t)(x))
+#else
+#define DFL_U(x) ((uint32_t)(x))
+#endif
+// the wave that runs a serial step: the device's whole wave of `lane0`, the host's lane0 itself
+DFL_HD inline bool serial_lane(int lane, int lane0) {
+#if DFL_DEVICE && DFL_SERIAL_WAVE
+    return (lane >> 6) == (lane0 >> 6);
+#else
+    return lane == lane0;
+#endif
+}
 // In-place minimum-redundancy code lengths (Moffat & Katajainen 1995) over
 // a[0..m) = frequencies sorted ascending; on return a[i] is the code length
 // of the i-th symbol (non-increasing in i).
 DFL_HD inline void mr_lengths(uint32_t *a, int m) {
     if (m == 1) { a[0] = 1; return; }
     // phase 1: internal-node weights and parent pointers
-    a[0] += a[1];
+    a[0] = DFL_U(a[0]) + DFL_U(a[1]);
     int root = 0, leaf = 2;
     for (int next = 1; next < m - 1; ++next) {
-        if (leaf >= m || a[root] < a[leaf]) { a[next] = a[root]; a[root++] = (uint32_t)next; }
-        else a[next] = a[leaf++];
-        if (leaf >= m || (root < next && a[root] < a[leaf])) { a[next] += a[root]; a[root++] = (uint32_t)next; }
-        else a[next] += a[leaf++];
+        const uint32_t ar = DFL_U(a[root]), al = leaf < m ? DFL_U(a[leaf]) : 0u;
+        uint32_t w;
+        if (leaf >= m || ar < al) { w = ar; a[root++] = (uint32_t)next; }
+        else { w = al; ++leaf; }
+        const uint32_t ar2 = root < next ? DFL_U(a[root]) : 0u, al2 = leaf < m ? DFL_U(a[leaf]) : 0u;
+        if (leaf >= m || (root < next && ar2 < al2)) { w += ar2; a[root++] = (uint32_t)next; }
+        else { w += al2; ++leaf; }
+        a[next] = w;
     }
     // phase 2: internal-node depths
     a[m - 2] = 0;
-    for (int next = m - 3; next >= 0; --next) a[next] = a[a[next]] + 1;
+    for (int next = m - 3; next >= 0; --next) a[next] = DFL_U(a[DFL_U(a[next])]) + 1;
     // phase 3: leaf depths
     int avail = 1, used = 0, depth = 0;
     root = m - 2;
     int next = m - 1;
     while (avail > 0) {
-        while (root >= 0 && (int)a[root] == depth) { ++used; --root; }
+        while (root >= 0 && (int)DFL_U(a[root]) == depth) { ++used; --root; }
         while (avail > used) { a[next--] = (uint32_t)depth; --avail; }
         avail = 2 * used;
         ++depth;
@@ -470,33 +581,43 @@ DFL_HD inline void mr_lengths(uint32_t *a, int m) {
 // the rarest symbols take the longest codes.
 DFL_HD inline void limit_assign(uint32_t *a, const uint32_t *keys, int m, int max_len, uint8_t *len, uint32_t *num) {
     for (int i = 0; i <= 32; ++i) num[i] = 0;
-    for (int i = 0; i < m; ++i) num[a[i] > 32 ? 32 : a[i]]++;
-    for (int i = max_len + 1; i <= 32; ++i) { num[max_len] += num[i]; num[i] = 0; }
+    for (int i = 0; i < m; ++i) {
+        const uint32_t v = DFL_U(a[i]), k = v > 32 ? 32 : v;
+        num[k] = DFL_U(num[k]) + 1;
+    }
+    for (int i = max_len + 1; i <= 32; ++i) { num[max_len] = DFL_U(num[max_len]) + DFL_U(num[i]); num[i] = 0; }
     uint32_t total = 0;
-    for (int i = max_len; i > 0; --i) total += num[i] << (max_len - i);
+    for (int i = max_len; i > 0; --i) total += DFL_U(num[i]) << (max_len - i);
     while (total != (1u << max_len)) {
-        num[max_len]--;
-        for (int i = max_len - 1; i > 0; --i)
-            if (num[i]) { num[i]--; num[i + 1] += 2; break; }
+        num[max_len] = DFL_U(num[max_len]) - 1;
+        for (int i = max_len - 1; i > 0; --i) {
+            const uint32_t ni = DFL_U(num[i]);
+            if (ni) { num[i] = ni - 1; num[i + 1] = DFL_U(num[i + 1]) + 2; break; }
+        }
         total--;
     }
     int k = 0;
     for (int l = max_len; l >= 1; --l)
-        for (uint32_t c = 0; c < num[l]; ++c) len[keys[k++] & 511] = (uint8_t)l;
+        for (uint32_t c = 0, nl = DFL_U(num[l]); c < nl; ++c) len[DFL_U(keys[k++]) & 511] = (uint8_t)l;
 }
 
 // The counting half of limit_assign: codes per length, limited to max_len
 // with the Kraft sum restored (num[0..32]).
 DFL_HD inline void limit_counts(const uint32_t *a, int m, int max_len, uint32_t *num) {
     for (int i = 0; i <= 32; ++i) num[i] = 0;
-    for (int i = 0; i < m; ++i) num[a[i] > 32 ? 32 : a[i]]++;
-    for (int i = max_len + 1; i <= 32; ++i) { num[max_len] += num[i]; num[i] = 0; }
+    for (int i = 0; i < m; ++i) {
+        const uint32_t v = DFL_U(a[i]), k = v > 32 ? 32 : v;
+        num[k] = DFL_U(num[k]) + 1;
+    }
+    for (int i = max_len + 1; i <= 32; ++i) { num[max_len] = DFL_U(num[max_len]) + DFL_U(num[i]); num[i] = 0; }
     uint32_t total = 0;
-    for (int i = max_len; i > 0; --i) total += num[i] << (max_len - i);
+    for (int i = max_len; i > 0; --i) total += DFL_U(num[i]) << (max_len - i);
     while (total != (1u << max_len)) {
-        num[max_len]--;
-        for (int i = max_len - 1; i > 0; --i)
-            if (num[i]) { num[i]--; num[i + 1] += 2; break; }
+        num[max_len] = DFL_U(num[max_len]) - 1;
+        for (int i = max_len - 1; i > 0; --i) {
+            const uint32_t ni = DFL_U(num[i]);
+            if (ni) { num[i] = ni - 1; num[i + 1] = DFL_U(num[i + 1]) + 2; break; }
+        }
         total--;
     }
 }
@@ -518,19 +639,23 @@ DFL_HD inline void build_lengths_small(const uint32_t *freq, int n, int max_len,
     uint32_t *keys = scratch, *f = scratch + n;
     for (int i = 0; i < n; ++i) {
         len[i] = 0;
-        if (freq[i]) keys[m++] = (freq[i] << 9) | (uint32_t)i;
+        const uint32_t fi = DFL_U(freq[i]);
+        if (fi) keys[m++] = (fi << 9) | (uint32_t)i;
     }
     for (int i = 0; i < n && m < min_used; ++i)
-        if (!freq[i]) keys[m++] = (uint32_t)i;
+        if (!DFL_U(freq[i])) keys[m++] = (uint32_t)i;
     if (m == 0) return;
-    if (m == 1) { len[keys[0] & 511] = 1; return; }
+    if (m == 1) { len[DFL_U(keys[0]) & 511] = 1; return; }
     for (int i = 1; i < m; ++i) {
-        const uint32_t v = keys[i];
+        const uint32_t v = DFL_U(keys[i]);
         int j = i - 1;
-        while (j >= 0 && keys[j] > v) { keys[j + 1] = keys[j]; --j; }
+        for (uint32_t kj; j >= 0 && (kj = DFL_U(keys[j])) > v; --j) keys[j + 1] = kj;
         keys[j + 1] = v;
     }
-    for (int i = 0; i < m; ++i) f[i] = (keys[i] >> 9) ? (keys[i] >> 9) : 1;
+    for (int i = 0; i < m; ++i) {
+        const uint32_t fk = DFL_U(keys[i]) >> 9;
+        f[i] = fk ? fk : 1;
+    }
     mr_lengths(f, m);
     limit_assign(f, keys, m, max_len, len, num);
 }
@@ -547,11 +672,14 @@ DFL_HD inline uint32_t reverse_bits(uint32_t v, int nb) {
 
 DFL_HD inline void first_codes(const uint8_t *len, int n, uint32_t *next, uint32_t *cnt) {
     for (int l = 0; l < 16; ++l) cnt[l] = 0;
-    for (int i = 0; i < n; ++i) cnt[len[i]]++;
+    for (int i = 0; i < n; ++i) {
+        const uint32_t l = DFL_U(len[i]);
+        cnt[l] = DFL_U(cnt[l]) + 1;
+    }
     cnt[0] = 0;
     uint32_t c = 0;
     next[0] = 0;
-    for (int l = 1; l < 16; ++l) { c = (c + cnt[l - 1]) << 1; next[l] = c; }
+    for (int l = 1; l < 16; ++l) { c = (c + DFL_U(cnt[l - 1])) << 1; next[l] = c; }
 }
 
 // canonical code of symbol i: the first code of its length + the symbols of
@@ -604,13 +732,13 @@ DFL_HD inline void p3b_rank(Shared &s, int lane) {
 // first lane of the second wave: code lengths by rank, codes per length
 constexpr int kDistLane = kT > 64 ? 64 : 0;
 DFL_HD inline void p3c_trees(Shared &s, int lane) {
-    if (lane == 0) {
-        const int ml = (int)s.m_lit;                 // >= 2: a literal and end of block
+    if (serial_lane(lane, 0)) {
+        const int ml = (int)DFL_U(s.m_lit);              // >= 2: a literal and end of block
         mr_lengths(s.sort_a, ml);
         limit_counts(s.sort_a, ml, 15, s.num_lit);
     }
-    if (lane == kDistLane) {
-        const int md = (int)s.m_dist;
+    if (serial_lane(lane, kDistLane)) {
+        const int md = (int)DFL_U(s.m_dist);
         if (md <= 1) {                               // one code of length 1 (unused when md == 0)
             for (int i = 0; i <= 32; ++i) s.num_dist[i] = 0;
             s.num_dist[1] = 1;
@@ -640,56 +768,68 @@ DFL_HD inline void p3c_assign(Shared &s, int lane) {
 DFL_HD inline void first_codes_from_counts(const uint32_t *num, uint32_t *next) {
     uint32_t c = 0;
     next[0] = 0;
-    for (int l = 1; l < 16; ++l) { c = (c + (l > 1 ? num[l - 1] : 0)) << 1; next[l] = c; }
+    for (int l = 1; l < 16; ++l) { c = (c + (l > 1 ? DFL_U(num[l - 1]) : 0)) << 1; next[l] = c; }
 }
 
-// P3c3 (thread 0): first codes, the run-length-coded header and its code
+// P3c3 (one wave, serial): first codes, the run-length-coded header and its code
 DFL_HD inline void p3c_header(Shared &s) {
     first_codes_from_counts(s.num_lit, s.next_code[0]);
     first_codes_from_counts(s.num_dist, s.next_code[1]);
-    const int nlit = s.last_lit + 1 > 257 ? (int)s.last_lit + 1 : 257;
-    const int ndist = (int)s.last_dist + 1;
+    const uint32_t last_lit = DFL_U(s.last_lit);
+    const int nlit = last_lit + 1 > 257 ? (int)last_lit + 1 : 257;
+    const int ndist = (int)DFL_U(s.last_dist) + 1;
     s.hlit = (uint32_t)(nlit - 257);
     s.hdist = (uint32_t)(ndist - 1);
     // run-length code the lengths (symbols 16 / 17 / 18)
     const int N = nlit + ndist;
-    auto L = [&](int i) -> uint8_t { return i < nlit ? s.lit_len[i] : s.dist_len[i - nlit]; };
+    auto L = [&](int i) -> uint32_t { return i < nlit ? DFL_U(s.lit_len[i]) : DFL_U(s.dist_len[i - nlit]); };
     uint32_t *clf = s.t0_clf;
     for (int i = 0; i < 19; ++i) clf[i] = 0;
     uint32_t nr = 0;
+    uint32_t v_next = N > 0 ? L(0) : 0u;
     for (int i = 0; i < N;) {
-        const uint8_t v = L(i);
+        const uint32_t v = v_next;
         int run = 1;
-        while (i + run < N && L(i + run) == v) ++run;
+        while (i + run < N && (v_next = L(i + run)) == v) ++run;
         i += run;
         if (v == 0) {
-            while (run >= 11) { const int r = run < 138 ? run : 138; s.rle[nr++] = (uint16_t)(18 | ((r - 11) << 8)); clf[18]++; run -= r; }
-            if (run >= 3) { s.rle[nr++] = (uint16_t)(17 | ((run - 3) << 8)); clf[17]++; run = 0; }
-            while (run-- > 0) { s.rle[nr++] = 0; clf[0]++; }
+            while (run >= 11) { const int r = run < 138 ? run : 138; s.rle[nr++] = (uint16_t)(18 | ((r - 11) << 8)); clf[18] = DFL_U(clf[18]) + 1; run -= r; }
+            if (run >= 3) { s.rle[nr++] = (uint16_t)(17 | ((run - 3) << 8)); clf[17] = DFL_U(clf[17]) + 1; run = 0; }
+            if (run > 0) clf[0] = DFL_U(clf[0]) + (uint32_t)run;
+            while (run-- > 0) s.rle[nr++] = 0;
         } else {
-            s.rle[nr++] = v; clf[v]++; --run;
-            while (run >= 3) { const int r = run < 6 ? run : 6; s.rle[nr++] = (uint16_t)(16 | ((r - 3) << 8)); clf[16]++; run -= r; }
-            while (run-- > 0) { s.rle[nr++] = v; clf[v]++; }
+            s.rle[nr++] = (uint16_t)v; --run;
+            uint32_t nv = 1;
+            while (run >= 3) { const int r = run < 6 ? run : 6; s.rle[nr++] = (uint16_t)(16 | ((r - 3) << 8)); clf[16] = DFL_U(clf[16]) + 1; run -= r; }
+            nv += run > 0 ? (uint32_t)run : 0u;
+            while (run-- > 0) s.rle[nr++] = (uint16_t)v;
+            clf[v] = DFL_U(clf[v]) + nv;
         }
     }
     s.n_rle = nr;
     build_lengths_small(clf, 19, 7, s.cl_len, s.sort_a, 2, s.t0_num);
     first_codes(s.cl_len, 19, s.next_code[2], s.t0_cnt);
     int ncl = 19;
-    while (ncl > 4 && !s.cl_len[kClOrder[ncl - 1]]) --ncl;
+    while (ncl > 4 && !DFL_U(s.cl_len[kClOrder[ncl - 1]])) --ncl;
     s.hclen = (uint32_t)(ncl - 4);
     uint32_t bits = 3 + 5 + 5 + 4 + 3 * (uint32_t)ncl;
-    for (uint32_t i = 0; i < nr; ++i) {
-        const uint32_t sym = s.rle[i] & 31;
-        bits += s.cl_len[sym] + (sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0);
-    }
+    for (int k = 0; k < 19; ++k)
+        bits += DFL_U(clf[k]) * (DFL_U(s.cl_len[k]) + (k == 16 ? 2u : k == 17 ? 3u : k == 18 ? 7u : 0u));
     s.hdr_bits = bits;
 }
 
 // P3d (all lanes): canonical codes
 DFL_HD inline void p3d_codes(Shared &s, int lane) {
-    for (int i = lane; i < 288; i += kT) s.lit_code[i] = i < 286 ? code_of(s.lit_len, i, s.next_code[0]) : 0;
-    if (lane < 32) s.dist_code[lane] = lane < 30 ? code_of(s.dist_len, lane, s.next_code[1]) : 0;
+    for (int i = lane; i < 288; i += kT) {
+        const uint16_t c = i < 286 ? code_of(s.lit_len, i, s.next_code[0]) : 0;
+        s.lit_code[i] = c;
+        s.lit_cl[i] = c | (uint32_t)s.lit_len[i] << 16;
+    }
+    if (lane < 32) {
+        const uint16_t c = lane < 30 ? code_of(s.dist_len, lane, s.next_code[1]) : 0;
+        s.dist_code[lane] = c;
+        s.dist_cl[lane] = c | (uint32_t)s.dist_len[lane] << 16;
+    }
     if (lane < 19) s.cl_code[lane] = code_of(s.cl_len, lane, s.next_code[2]);
 }
 
@@ -788,11 +928,22 @@ DFL_HD inline void p4_scan(Shared &s, uint32_t n, uint32_t *out) {
     for (int l = 0; l < kT; ++l) c ^= s.lane_crc[l];
     s.crc = ~c;
 }
-// P5: into stage[] when use_stage (copied out by p6_copy), else into out
+// P5: into stage[] when use_stage (copied out by p6_copy), else into out.
+// Two inlined copies, so that the LDS one writes with LDS instructions (one
+// pointer that may be either is a flat pointer).
+#if DFL_DEVICE
+#define DFL_INLINE __attribute__((always_inline)) inline
+#else
+#define DFL_INLINE inline
+#endif
+DFL_HD DFL_INLINE void p5_emit_to(Shared &s, uint32_t n, int lane, const uint32_t *tok, uint32_t *out);
 DFL_HD inline void p5_emit(Shared &s, uint32_t n, int lane, const uint32_t *tok, uint32_t *out) {
+    if (s.use_stage) p5_emit_to(s, n, lane, tok, s.stage);
+    else p5_emit_to(s, n, lane, tok, out);
+}
+DFL_HD DFL_INLINE void p5_emit_to(Shared &s, uint32_t n, int lane, const uint32_t *tok, uint32_t *out) {
     uint32_t lo, hi;
     lane_range(n, lane, lo, hi);
-    if (s.use_stage) out = s.stage;
     if (s.stored) {
         // stored block: BFINAL=1 BTYPE=00, LEN, NLEN, raw bytes (byte-aligned after the 3 bits)
         uint8_t *o = reinterpret_cast<uint8_t *>(out) + 18 + 5;

@@ -364,7 +364,11 @@ __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
     const int64_t nb = (total + dfl::kMaxIn - 1) / dfl::kMaxIn;
     const bool st = D.stamps != nullptr;
     uint32_t *tok = D.tok + (size_t)blockIdx.x * dfl::kTokWords;
-    uint64_t t[12] = {0}, t0 = 0;
+    // phase stamps (dcr_deflate_probe): accumulated in LDS by lane 0, not
+    // in per-lane registers
+    __shared__ uint64_t t[12];
+    uint64_t t0 = 0;
+    if (st && lane < 12) t[lane] = 0;
     auto stamp = [&](int k) {
         if (st && lane == 0) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
@@ -409,11 +413,13 @@ __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
         stamp(3);
         dfl::p3c_trees(s, lane);
         __syncthreads();
+        stamp(4);
         dfl::p3c_assign(s, lane);
         __syncthreads();
-        if (lane == 0) dfl::p3c_header(s);
+        stamp(10);
+        if (dfl::serial_lane(lane, 0)) dfl::p3c_header(s);
         __syncthreads();
-        stamp(4);
+        stamp(11);
         dfl::p3d_codes(s, lane);
         __syncthreads();
         stamp(5);
@@ -432,7 +438,7 @@ __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
         stamp(9);
     }
     if (st && lane == 0)
-        for (int k = 0; k < 10; ++k) atomicAdd(&D.stamps[k], (unsigned long long)t[k]);
+        for (int k = 0; k < 12; ++k) atomicAdd(&D.stamps[k], (unsigned long long)t[k]);
 }
 
 // compressed blocks into one contiguous buffer (offsets from an exclusive scan)

@@ -3,6 +3,7 @@ s_memtime phase stamps (dcr_deflate_probe, diagnostic entry of libdcr.so)."""
 import ctypes
 import sys
 import time
+import zlib
 
 import numpy as np
 
@@ -11,8 +12,8 @@ from duplexumiconsensusreads_amd import _lib, native_io, synth  # noqa: E402
 from duplexumiconsensusreads_amd.params import ConsensusParams  # noqa: E402
 from duplexumiconsensusreads_amd.stream import DeviceStream  # noqa: E402
 
-PHASES = ["load+clear", "hash", "count+crc", "keys+rank", "lengths(t0)", "codes", "bits", "scan(t0)", "emit",
-          "frame(t0)"]
+PHASES = ["load+clear", "hash", "count+crc", "keys+rank", "trees(t0)", "codes", "bits", "scan(t0)", "emit",
+          "frame(t0)", "assign", "header(t0)"]
 
 
 def main():
@@ -29,15 +30,27 @@ def main():
     fn = lib.dcr_deflate_probe
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
-                   ctypes.c_void_p]
+                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    nb = (raw.nbytes + 0xff00 - 1) // 0xff00
+    slots = np.zeros(nb * 65536, np.uint8)
+    sizes = np.zeros(nb, np.int64)
     for dbg in [0]:
-        st = np.zeros(10, np.uint64)
+        st = np.zeros(12, np.uint64)
         ms = ctypes.c_float()
         cb = ctypes.c_int64()
         for rep in range(3):
             st[:] = 0
             _lib._check(fn(ctx._ctx, raw.ctypes.data, raw.nbytes, st.ctypes.data, ctypes.byref(ms),
-                           ctypes.byref(cb)))
+                           ctypes.byref(cb), slots.ctypes.data if rep == 0 else None,
+                           sizes.ctypes.data if rep == 0 else None))
+        # every member inflates (zlib, gzip framing) to its block of the input
+        rb = raw.tobytes()
+        for b in range(nb):
+            mem = slots[b * 65536:b * 65536 + int(sizes[b])].tobytes()
+            d = zlib.decompressobj(31)
+            got = d.decompress(mem)
+            assert d.eof and not d.unused_data and got == rb[b * 0xff00:(b + 1) * 0xff00], f"block {b} differs"
+        print(f"verified {nb} members with zlib")
         tot = st.sum()
         print(f"dbg={dbg}: {raw.nbytes / 1e6:.1f} MB -> {cb.value / 1e6:.1f} MB ({raw.nbytes / cb.value:.2f}x) in "
               f"{ms.value:.2f} ms = {raw.nbytes / ms.value / 1e6:.2f} GB/s")
