@@ -576,6 +576,77 @@ DFL_HD inline void mr_lengths(uint32_t *a, int m) {
     }
 }
 
+// The same code as mr_lengths, as counts of codes per length (num[0..32],
+// lengths above 32 counted at 32) and with the serial chains of LDS loads
+// batched: in phase 1 the leaves and the internal nodes are consumed in
+// order, so the next two of each are loaded together up front (an internal
+// node at root + 1 is only used once it exists, root + 1 < next); phase 2
+// takes the parent pointers of eight nodes in one go, then their parents'
+// depths (a parent inside the batch from the batch's own registers);
+// phase 3 counts equal depths eight at a time.  a[] is scratch afterwards.
+DFL_HD inline void mr_counts(uint32_t *a, int m, uint32_t *num) {
+    for (int i = 0; i <= 32; ++i) num[i] = 0;
+    if (m == 1) { num[1] = 1; return; }
+    // phase 1
+    a[0] = a[0] + a[1];
+    int root = 0, leaf = 2;
+    for (int next = 1; next < m - 1; ++next) {
+        const uint32_t r0 = a[root], r1 = a[root + 1];
+        const uint32_t l0 = leaf < m ? a[leaf] : 0u, l1 = leaf + 1 < m ? a[leaf + 1] : 0u;
+        uint32_t w;
+        bool took_root;
+        if (leaf >= m || r0 < l0) { w = r0; a[root] = (uint32_t)next; took_root = true; }
+        else { w = l0; took_root = false; }
+        const int root2 = took_root ? root + 1 : root, leaf2 = took_root ? leaf : leaf + 1;
+        const uint32_t rv = took_root ? r1 : r0, lv = took_root ? l0 : l1;
+        if (leaf2 >= m || (root2 < next && rv < lv)) { w += rv; a[root2] = (uint32_t)next; root = root2 + 1; leaf = leaf2; }
+        else { w += lv; root = root2; leaf = leaf2 + 1; }
+        a[next] = w;
+    }
+    // phase 2: internal-node depths (node m - 2 is the root)
+    a[m - 2] = 0;
+    constexpr int B = 8;
+    for (int next = m - 3; next >= 0; next -= B) {
+        uint32_t ptr[B], dep[B], got[B];
+DFL_UNROLL
+        for (int k = 0; k < B; ++k) ptr[k] = next - k >= 0 ? a[next - k] : (uint32_t)(m - 2);
+DFL_UNROLL
+        for (int k = 0; k < B; ++k) got[k] = a[ptr[k]];
+DFL_UNROLL
+        for (int k = 0; k < B; ++k) {
+            // parent inside this batch: node ptr[k] = next - j, j < k
+            uint32_t d = got[k];
+DFL_UNROLL
+            for (int j = 0; j < k; ++j)
+                if (ptr[k] == (uint32_t)(next - j)) d = dep[j];
+            dep[k] = d + 1;
+            if (next - k >= 0) a[next - k] = dep[k];
+        }
+    }
+    // phase 3: leaves per depth; internal depths are non-decreasing as the
+    // index falls
+    int avail = 1, depth = 0;
+    int r = m - 2;
+    while (avail > 0) {
+        int used = 0;
+        for (;;) {
+            uint32_t v[B];
+DFL_UNROLL
+            for (int k = 0; k < B; ++k) v[k] = r - k >= 0 ? a[r - k] : 0xffffffffu;
+            int eq = 0;
+DFL_UNROLL
+            for (int k = 0; k < B; ++k) eq += (v[k] == (uint32_t)depth) ? 1 : 0;
+            used += eq;
+            r -= eq;
+            if (eq < B) break;
+        }
+        const int leaves = avail - used;
+        num[depth > 32 ? 32 : depth] += (uint32_t)leaves;
+        avail = 2 * used;
+        ++depth;
+    }
+}
+
 // Length-limit code lengths a[0..m) (non-increasing, from mr_lengths) to
 // max_len and hand them to the symbols of keys[0..m) (ascending frequency):
 // the rarest symbols take the longest codes.
@@ -601,23 +672,16 @@ DFL_HD inline void limit_assign(uint32_t *a, const uint32_t *keys, int m, int ma
         for (uint32_t c = 0, nl = DFL_U(num[l]); c < nl; ++c) len[DFL_U(keys[k++]) & 511] = (uint8_t)l;
 }
 
-// The counting half of limit_assign: codes per length, limited to max_len
-// with the Kraft sum restored (num[0..32]).
-DFL_HD inline void limit_counts(const uint32_t *a, int m, int max_len, uint32_t *num) {
-    for (int i = 0; i <= 32; ++i) num[i] = 0;
-    for (int i = 0; i < m; ++i) {
-        const uint32_t v = DFL_U(a[i]), k = v > 32 ? 32 : v;
-        num[k] = DFL_U(num[k]) + 1;
-    }
-    for (int i = max_len + 1; i <= 32; ++i) { num[max_len] = DFL_U(num[max_len]) + DFL_U(num[i]); num[i] = 0; }
+// Codes per length limited to max_len with the Kraft sum restored (num[0..32]
+// from mr_counts)
+DFL_HD inline void limit_num(int max_len, uint32_t *num) {
+    for (int i = max_len + 1; i <= 32; ++i) { num[max_len] += num[i]; num[i] = 0; }
     uint32_t total = 0;
-    for (int i = max_len; i > 0; --i) total += DFL_U(num[i]) << (max_len - i);
+    for (int i = max_len; i > 0; --i) total += num[i] << (max_len - i);
     while (total != (1u << max_len)) {
-        num[max_len] = DFL_U(num[max_len]) - 1;
-        for (int i = max_len - 1; i > 0; --i) {
-            const uint32_t ni = DFL_U(num[i]);
-            if (ni) { num[i] = ni - 1; num[i + 1] = DFL_U(num[i + 1]) + 2; break; }
-        }
+        num[max_len]--;
+        for (int i = max_len - 1; i > 0; --i)
+            if (num[i]) { num[i]--; num[i + 1] += 2; break; }
         total--;
     }
 }
@@ -734,8 +798,8 @@ constexpr int kDistLane = kT > 64 ? 64 : 0;
 DFL_HD inline void p3c_trees(Shared &s, int lane) {
     if (serial_lane(lane, 0)) {
         const int ml = (int)DFL_U(s.m_lit);              // >= 2: a literal and end of block
-        mr_lengths(s.sort_a, ml);
-        limit_counts(s.sort_a, ml, 15, s.num_lit);
+        mr_counts(s.sort_a, ml, s.num_lit);
+        limit_num(15, s.num_lit);
     }
     if (serial_lane(lane, kDistLane)) {
         const int md = (int)DFL_U(s.m_dist);
@@ -743,8 +807,8 @@ DFL_HD inline void p3c_trees(Shared &s, int lane) {
             for (int i = 0; i <= 32; ++i) s.num_dist[i] = 0;
             s.num_dist[1] = 1;
         } else {
-            mr_lengths(s.sort_d, md);
-            limit_counts(s.sort_d, md, 15, s.num_dist);
+            mr_counts(s.sort_d, md, s.num_dist);
+            limit_num(15, s.num_dist);
         }
     }
 }
