@@ -836,6 +836,21 @@ DFL_HD inline void first_codes_from_counts(const uint32_t *num, uint32_t *next) 
 }
 
 // P3c3 (one wave, serial): first codes, the run-length-coded header and its code
+// the header's code-length code and its bit count, from the run-length
+// symbols' counts (t0_clf) (one lane)
+DFL_HD inline void p3c_header_post(Shared &s) {
+    uint32_t *clf = s.t0_clf;
+    build_lengths_small(clf, 19, 7, s.cl_len, s.sort_a, 2, s.t0_num);
+    first_codes(s.cl_len, 19, s.next_code[2], s.t0_cnt);
+    int ncl = 19;
+    while (ncl > 4 && !DFL_U(s.cl_len[kClOrder[ncl - 1]])) --ncl;
+    s.hclen = (uint32_t)(ncl - 4);
+    uint32_t bits = 3 + 5 + 5 + 4 + 3 * (uint32_t)ncl;
+    for (int k = 0; k < 19; ++k)
+        bits += DFL_U(clf[k]) * (DFL_U(s.cl_len[k]) + (k == 16 ? 2u : k == 17 ? 3u : k == 18 ? 7u : 0u));
+    s.hdr_bits = bits;
+}
+
 DFL_HD inline void p3c_header(Shared &s) {
     first_codes_from_counts(s.num_lit, s.next_code[0]);
     first_codes_from_counts(s.num_dist, s.next_code[1]);
@@ -871,15 +886,7 @@ DFL_HD inline void p3c_header(Shared &s) {
         }
     }
     s.n_rle = nr;
-    build_lengths_small(clf, 19, 7, s.cl_len, s.sort_a, 2, s.t0_num);
-    first_codes(s.cl_len, 19, s.next_code[2], s.t0_cnt);
-    int ncl = 19;
-    while (ncl > 4 && !DFL_U(s.cl_len[kClOrder[ncl - 1]])) --ncl;
-    s.hclen = (uint32_t)(ncl - 4);
-    uint32_t bits = 3 + 5 + 5 + 4 + 3 * (uint32_t)ncl;
-    for (int k = 0; k < 19; ++k)
-        bits += DFL_U(clf[k]) * (DFL_U(s.cl_len[k]) + (k == 16 ? 2u : k == 17 ? 3u : k == 18 ? 7u : 0u));
-    s.hdr_bits = bits;
+    p3c_header_post(s);
 }
 
 // P3d (all lanes): canonical codes

@@ -355,6 +355,102 @@ __device__ __forceinline__ void p4_scan_wg(dfl::Shared &s, uint32_t n, int lane,
     }
 }
 
+// dfl::p3c_header on wave 0 (lanes 0..63): the same greedy run-length
+// code of the code lengths, built in parallel.  Runs start where a length
+// differs from the one before it (ballots over five chunks of 64 positions);
+// each run's lane counts its symbols, an exclusive scan in run order gives
+// its offset in rle[], and it writes them; the symbol counts go in by LDS
+// atomics.  Lane 0 then finishes as the serial code does (p3c_header_post).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void p3c_header_wave(dfl::Shared &s, int lane) {
+    const uint32_t last_lit = s.last_lit, last_dist = s.last_dist;
+    const int nlit = last_lit + 1 > 257 ? (int)last_lit + 1 : 257;
+    const int ndist = (int)last_dist + 1;
+    const int N = nlit + ndist;                       // <= 316: five chunks
+    auto L = [&](int i) -> uint32_t { return i < nlit ? s.lit_len[i] : s.dist_len[i - nlit]; };
+    uint32_t *clf = s.t0_clf;
+    if (lane < 19) clf[lane] = 0;
+    if (lane == 0) {
+        dfl::first_codes_from_counts(s.num_lit, s.next_code[0]);
+        dfl::first_codes_from_counts(s.num_dist, s.next_code[1]);
+        s.hlit = (uint32_t)(nlit - 257);
+        s.hdist = (uint32_t)(ndist - 1);
+    }
+    constexpr int kC = 5;
+    uint32_t v[kC];
+    uint64_t st[kC];                                  // run starts per chunk (uniform)
+#pragma unroll
+    for (int c = 0; c < kC; ++c) {
+        const int i = 64 * c + lane;
+        v[c] = i < N ? L(i) : 0xffu;
+        const uint32_t pv = (i > 0 && i <= N) ? L(i - 1) : 0xfeu;
+        st[c] = __ballot(i < N && v[c] != pv);
+    }
+    wave_lds_sync();                                  // clf zeroed before the atomics
+    uint32_t base = 0;
+#pragma unroll
+    for (int c = 0; c < kC; ++c) {
+        const int i = 64 * c + lane;
+        const bool start = (st[c] >> lane) & 1u;
+        // the next run start after i: in this chunk above the lane, else in a later chunk, else N
+        int nxt = N;
+        const uint64_t above = lane == 63 ? 0ull : st[c] & (~0ull << (lane + 1));
+        if (above) nxt = 64 * c + (int)__builtin_ctzll(above);
+        else {
+#pragma unroll
+            for (int d = kC - 1; d > c; --d)
+                if (st[d]) nxt = 64 * d + (int)__builtin_ctzll(st[d]);
+        }
+        int run = nxt - i;
+        uint32_t ns = 0, n18 = 0, n17 = 0, n16 = 0, nv = 0;
+        const uint32_t val = v[c];
+        if (start) {
+            int r = run;
+            if (val == 0) {
+                while (r >= 11) { r -= r < 138 ? r : 138; ++n18; }
+                if (r >= 3) { ++n17; r = 0; }
+                nv = (uint32_t)r;
+                ns = n18 + n17 + nv;
+            } else {
+                --r;
+                nv = 1;
+                while (r >= 3) { r -= r < 6 ? r : 6; ++n16; }
+                nv += (uint32_t)r;
+                ns = 1 + n16 + (uint32_t)r;
+            }
+        }
+        const uint32_t inc = wave_incl_scan(ns);
+        uint32_t off = base + inc - ns;
+        base += __shfl(inc, 63, kW);
+        if (start) {
+            int r = run;
+            if (val == 0) {
+                while (r >= 11) { const int t = r < 138 ? r : 138; s.rle[off++] = (uint16_t)(18 | ((t - 11) << 8)); r -= t; }
+                if (r >= 3) { s.rle[off++] = (uint16_t)(17 | ((r - 3) << 8)); r = 0; }
+                while (r-- > 0) s.rle[off++] = 0;
+            } else {
+                s.rle[off++] = (uint16_t)val;
+                --r;
+                while (r >= 3) { const int t = r < 6 ? r : 6; s.rle[off++] = (uint16_t)(16 | ((t - 3) << 8)); r -= t; }
+                while (r-- > 0) s.rle[off++] = (uint16_t)val;
+            }
+            if (n18) atomicAdd(&clf[18], n18);
+            if (n17) atomicAdd(&clf[17], n17);
+            if (n16) atomicAdd(&clf[16], n16);
+            if (nv) atomicAdd(&clf[val], nv);
+        }
+    }
+    wave_lds_sync();
+    if (lane == 0) {
+        s.n_rle = base;
+        dfl::p3c_header_post(s);
+    }
+}
+
 // one workgroup (256 lanes) per BGZF block of the record stream
 __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
     extern __shared__ __align__(16) uint8_t smem[];
@@ -417,7 +513,7 @@ __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
         dfl::p3c_assign(s, lane);
         __syncthreads();
         stamp(10);
-        if (dfl::serial_lane(lane, 0)) dfl::p3c_header(s);
+        if (lane < kW) p3c_header_wave(s, lane);
         __syncthreads();
         stamp(11);
         dfl::p3d_codes(s, lane);

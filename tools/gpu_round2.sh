@@ -17,7 +17,7 @@ timeout -k 10 500 python3 -u bench.py > "$O/bench.json" 2> "$O/bench.log" || { e
 cat "$O/bench.json"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/kt" -o kt --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu > "$O/bench_prof.json" 2> "$O/bench_prof.log" || { echo "prof failed"; tail -30 "$O/bench_prof.log"; exit 1; }
 find "$O/kt" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats.csv" \;
-find "$O/kt" -name "*kernel_trace.csv" -exec python3 tools/kt_grid.py {} k_consensus_fast k_recmeta k_scatter k_deflate \; > "$O/kernel_grid.csv"
+find "$O/kt" -name "*kernel_trace.csv" -exec python3 tools/kt_grid.py {} k_consensus_fast k_recmeta k_deflate k_inflate \; > "$O/kernel_grid.csv"
 rm -rf "$O/kt"
 head -12 "$O/kernel_grid.csv"
 bash tools/gpu_traffic.sh "$TAG" || exit 1
