@@ -50,7 +50,7 @@ def main():
             d = zlib.decompressobj(31)
             got = d.decompress(mem)
             assert d.eof and not d.unused_data and got == rb[b * 0xff00:(b + 1) * 0xff00], f"block {b} differs"
-        print(f"verified {nb} members with zlib")
+        print(f"verified {nb} members with zlib, {int(sizes.sum())} compressed bytes")
         tot = st.sum()
         print(f"dbg={dbg}: {raw.nbytes / 1e6:.1f} MB -> {cb.value / 1e6:.1f} MB ({raw.nbytes / cb.value:.2f}x) in "
               f"{ms.value:.2f} ms = {raw.nbytes / ms.value / 1e6:.2f} GB/s")
