@@ -34,3 +34,21 @@ extern "C" int64_t dcr_deflate_emulate(const uint8_t *in, int64_t n, uint8_t *ou
     std::memcpy(out, w.data(), total);
     return total;
 }
+
+// (test) the device's batched Huffman code-length counts (mr_counts) against
+// the plain in-place algorithm (mr_lengths) on one alphabet: freq[0..m)
+// ascending, m in 2..288; num_a / num_b (33 each) get the codes per length
+// (limited to 15 bits) of the two
+extern "C" int dcr_deflate_lengths_ab(const uint32_t *freq, int m, uint32_t *num_a, uint32_t *num_b) {
+    if (!freq || !num_a || !num_b || m < 2 || m > 288) return -1;
+    for (int i = 1; i < m; ++i)
+        if (freq[i] < freq[i - 1] || !freq[i - 1]) return -1;
+    std::vector<uint32_t> a(freq, freq + m), b(freq, freq + m);
+    dfl::mr_lengths(a.data(), m);
+    for (int i = 0; i <= 32; ++i) num_a[i] = 0;
+    for (int i = 0; i < m; ++i) num_a[a[i] > 32 ? 32 : a[i]]++;
+    dfl::limit_num(15, num_a);
+    dfl::mr_counts(b.data(), m, num_b);
+    dfl::limit_num(15, num_b);
+    return 0;
+}

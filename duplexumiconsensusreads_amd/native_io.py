@@ -100,6 +100,7 @@ def load():
             "dcr_fmt_write": (_i32, [_vp, _vp, _vp, _vp, _i32]),
             "dcr_synth_write": (_i32, [_vp, _vp, _i32]),
             "dcr_deflate_emulate": (_i64, [_vp, _i64, _vp]),
+            "dcr_deflate_lengths_ab": (_i32, [_vp, _i32, _vp, _vp]),
             "dcr_split_points": (_i32, [ctypes.c_char_p, _i32, _vp, _vp]),
             "dcr_ingest_open_range": (_vp, [ctypes.c_char_p, _vp, _i64, _i64]),
             "dcr_ingest_sample_calls": (_i64, [_vp, _vp, _i64]),

@@ -236,6 +236,10 @@ int dcr_fmt_write(dcr_bgzw *w, const dcr_host_batch *hb, const dcr_fmt_out *ss, 
  * lane on the host, for tests: one BGZF block of in[0, n) (n <= 0xff00) into
  * out (>= 64 KiB); returns its size or -1 */
 int64_t dcr_deflate_emulate(const uint8_t *in, int64_t n, uint8_t *out);
+/* (test) codes per length of the device's batched Huffman code-length count
+ * (dcr_deflate.h mr_counts) and of the plain in-place algorithm, for freq[0..m)
+ * ascending and nonzero, m in 2..288; 0, or -1 on bad arguments */
+int dcr_deflate_lengths_ab(const uint32_t *freq, int m, uint32_t *num_a, uint32_t *num_b);
 
 /* ---- synthetic inputs (bench / tests) ----
  * Records of n_fam duplex families from dcr_batch-layout arrays (reads of

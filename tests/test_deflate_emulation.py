@@ -77,3 +77,26 @@ def test_bad_sizes_rejected():
         native_io.deflate_emulate(b"")
     with pytest.raises(Exception):
         native_io.deflate_emulate(b"x" * (0xff00 + 1))
+
+
+@pytest.mark.parametrize("mode", ["flat", "wide", "skewed"])
+def test_batched_code_lengths_equal_plain(mode):
+    """The kernel's Huffman code lengths (mr_counts: LDS loads batched, counts
+    per depth) equal the plain in-place minimum-redundancy algorithm's, codes
+    per length after the 15-bit limit, on random alphabets of 2..288 symbols."""
+    lib = native_io.load()
+    rng = np.random.default_rng({"flat": 1, "wide": 2, "skewed": 3}[mode])
+    a = np.zeros(33, np.uint32)
+    b = np.zeros(33, np.uint32)
+    for _ in range(400):
+        m = int(rng.integers(2, 289))
+        if mode == "flat":
+            f = rng.integers(1, 6, m)
+        elif mode == "wide":
+            f = rng.integers(1, 100000, m)
+        else:
+            f = np.where(rng.random(m) < 0.9, rng.integers(1, 4, m), rng.integers(1, 60000, m))
+        f = np.sort(f).astype(np.uint32)
+        assert lib.dcr_deflate_lengths_ab(f.ctypes.data, m, a.ctypes.data, b.ctypes.data) == 0
+        assert (a == b).all(), (m, a, b)
+        assert sum(int(a[k]) << (15 - k) for k in range(1, 16)) == 1 << 15   # complete code
