@@ -36,6 +36,7 @@ barriers on all ranks.  --in-level sets the input's BGZF level (default 1;
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import json
 import os
 import shutil
@@ -44,6 +45,8 @@ import tempfile
 import time
 
 import numpy as np
+
+faulthandler.enable()     # a native crash prints the Python stacks to stderr
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

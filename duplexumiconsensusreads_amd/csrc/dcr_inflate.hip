@@ -529,8 +529,12 @@ __global__ __launch_bounds__(64) void k_inflate(Args a) {
                 }
             } else if (dist < kW) {
                 // a period below the wave: byte i repeats byte i mod dist
-                const uint32_t rep = (uint32_t)lane % dist;      // then + dist steps of the period
-                const uint32_t step = kW - kW % dist;            // a multiple of dist
+                // lane mod dist and the largest multiple of dist <= 64 by a
+                // float reciprocal (exact here: (x + 0.5) / dist is >= 0.5 / 63
+                // away from an integer), not an integer division sequence
+                const float rd = __builtin_amdgcn_rcpf((float)dist);
+                const uint32_t rep = (uint32_t)lane - dist * (uint32_t)(((float)lane + 0.5f) * rd);
+                const uint32_t step = dist * uni((uint32_t)(((float)kW + 0.5f) * rd));   // a multiple of dist
                 const uint8_t v = s.ring[(o.opos - dist + rep) & kRM];
                 for (uint32_t c0 = 0; c0 < len; c0 += step) s.ring[(o.opos + c0 + lane) & kRM] = v;
             } else {
