@@ -38,6 +38,7 @@
 #include "../../include/dcr_inflate.h"
 #include "dcr_deflate.h"
 #include "dcr_internal.h"
+#include "dcr_span_stream.h"
 
 #ifndef DINF_STAMP
 #define DINF_STAMP 0      // diagnostic builds: per-phase s_memtime cycles and token counts in Args::dbg
@@ -795,41 +796,11 @@ extern "C" int dcr_inflater_stamps(dcr_inflater *h, double *out16, int reset) {
 }
 
 // ---- streaming: spans of members launched ahead of the reader ---------------
-// The reader's helper thread appends the input's members as it walks the
-// BGZF headers (stream_add).  The producer thread forms spans of them, copies
-// a span's compressed bytes out of the caller's mapping into page-locked
-// staging, uploads them and launches k_inflate into one of kSlots device
-// output slots; fetch waits for the spans that cover a range, checks their
-// members' statuses and copies the range out (DMA into the caller's
-// page-locked chunk buffer).  A slot is reused once every byte of its span
-// has been fetched.  The first spans are small (the reader starts early:
-// a member takes ~4 ms of serial decode whatever the launch size), the
-// others hold 4,096 members, enough to fill the device.  The slots' device
-// and page-locked buffers belong to the inflater and outlive the stream.
-struct dcr_inflate_stream {
-    static constexpr int kSlots = InflSlots::kSlots;
-    dcr_inflater *h = nullptr;
-    InflSlots *sl = nullptr;
-    const uint8_t *file = nullptr;
-    std::vector<dcr_bgzf_member> m;      // appended by stream_add
-    bool m_done = false;
-    struct Span {
-        int32_t m0 = 0, m1 = 0;
-        int64_t out0 = 0, out1 = 0, in0 = 0, in1 = 0;
-        bool launched = false, checked = false;
-        int rc = 0;
-        hipEvent_t start = nullptr, done = nullptr;
-    };
-    std::deque<Span> spans;             // formed by the producer (stable references)
-    std::vector<dcr_bgzf_member> mrel[kSlots];
-    std::thread producer;
-    std::mutex mu;
-    std::condition_variable cv;
-    int64_t fetched = 0;                // output bytes handed to the reader (monotonic)
-    bool stop = false, produced = false;
-    int err = 0;                        // producer-side runtime error
-};
-
+// The protocol (spans, slots, when a slot is reused) is csrc/dcr_span_stream.h;
+// this backend copies a span's compressed bytes from page-locked staging to
+// the device, launches k_inflate into the slot's device output and DMAs
+// fetched ranges into the caller's page-locked chunk buffer.  The slots'
+// device and page-locked buffers belong to the inflater and outlive a stream.
 namespace {
 hipError_t pinned_grow(uint8_t *&p, size_t &cap, size_t n) {
     if (n <= cap) return hipSuccess;
@@ -841,68 +812,30 @@ hipError_t pinned_grow(uint8_t *&p, size_t &cap, size_t n) {
     return e;
 }
 
-void stream_produce(dcr_inflate_stream *st) {
-    dcr_inflater *h = st->h;
-    InflSlots &S = *st->sl;
-    (void)hipSetDevice(h->device);
-    int32_t mnext = 0;
-    for (size_t k = 0;; ++k) {
-        const int32_t want = k == 0 ? 128 : k == 1 ? 1024 : 4096;
-        dcr_inflate_stream::Span *spp;
-        {
-            std::unique_lock<std::mutex> lk(st->mu);
-            st->cv.wait(lk, [&] { return st->stop || st->m_done || (int32_t)st->m.size() - mnext >= want; });
-            if (st->stop || (st->m_done && mnext == (int32_t)st->m.size())) break;
-            dcr_inflate_stream::Span sp;
-            sp.m0 = mnext;
-            sp.m1 = std::min((int32_t)st->m.size(), mnext + want);
-            sp.out0 = st->m[sp.m0].out_off;
-            sp.out1 = st->m[sp.m1 - 1].out_off + st->m[sp.m1 - 1].isize;
-            sp.in0 = st->m[sp.m0].in_off;
-            sp.in1 = sp.in0;
-            for (int32_t i = sp.m0; i < sp.m1; ++i)
-                sp.in1 = std::max<int64_t>(sp.in1, st->m[i].in_off + st->m[i].in_len);
-            if (hipEventCreateWithFlags(&sp.done, hipEventBlockingSync) != hipSuccess ||
-                hipEventCreate(&sp.start) != hipSuccess) {
-                st->err = -1;
-                st->cv.notify_all();
-                return;
-            }
-            st->spans.push_back(sp);
-            spp = &st->spans.back();
-            // the slot's previous span must be fully read
-            st->cv.wait(lk, [&] {
-                return st->stop || k < (size_t)dcr_inflate_stream::kSlots ||
-                       st->fetched >= st->spans[k - dcr_inflate_stream::kSlots].out1;
-            });
-            if (st->stop) break;
-        }
-        auto &sp = *spp;
-        mnext = sp.m1;
-        const int slot = (int)(k % dcr_inflate_stream::kSlots);
-        const int32_t n = sp.m1 - sp.m0;
-        const size_t nin = (size_t)(sp.in1 - sp.in0), nout = (size_t)(sp.out1 - sp.out0);
-        if (pinned_grow(S.h_stage[slot], S.cap_stage[slot], nin + 16) != hipSuccess ||
-            pinned_grow(S.h_st[slot], S.cap_hst[slot], (size_t)n) != hipSuccess ||
-            grow(S.d_in[slot], S.cap_in[slot], nin + dinf::kPad) != hipSuccess ||
-            grow(S.d_out[slot], S.cap_out[slot], nout + 16) != hipSuccess ||
-            grow(S.d_m[slot], S.cap_m[slot], (size_t)n) != hipSuccess ||
-            grow(S.d_st[slot], S.cap_dst[slot], (size_t)n) != hipSuccess) {
-            std::lock_guard<std::mutex> g(st->mu);
-            st->err = -1;
-            st->cv.notify_all();
-            return;
-        }
-        std::memcpy(S.h_stage[slot], st->file + sp.in0, nin);
-        auto &mr = st->mrel[slot];
-        {
-            std::lock_guard<std::mutex> g(st->mu);
-            mr.assign(st->m.begin() + sp.m0, st->m.begin() + sp.m1);
-        }
-        for (auto &x : mr) {
-            x.in_off -= sp.in0;
-            x.out_off -= sp.out0;
-        }
+struct HipSpanBackend {
+    using Event = hipEvent_t;
+    dcr_inflater *h;
+    InflSlots &S;
+    bool new_events(Event &start, Event &done) {
+        return hipEventCreateWithFlags(&done, hipEventBlockingSync) == hipSuccess &&
+               hipEventCreate(&start) == hipSuccess;
+    }
+    void free_events(Event &start, Event &done) {
+        if (start) (void)hipEventDestroy(start);
+        if (done) (void)hipEventDestroy(done);
+        start = done = nullptr;
+    }
+    bool ensure(int slot, size_t nin, size_t nout, int32_t n) {
+        (void)hipSetDevice(h->device);
+        return pinned_grow(S.h_stage[slot], S.cap_stage[slot], nin + 16) == hipSuccess &&
+               pinned_grow(S.h_st[slot], S.cap_hst[slot], (size_t)n) == hipSuccess &&
+               grow(S.d_in[slot], S.cap_in[slot], nin + dinf::kPad) == hipSuccess &&
+               grow(S.d_out[slot], S.cap_out[slot], nout + 16) == hipSuccess &&
+               grow(S.d_m[slot], S.cap_m[slot], (size_t)n) == hipSuccess &&
+               grow(S.d_st[slot], S.cap_dst[slot], (size_t)n) == hipSuccess;
+    }
+    uint8_t *stage(int slot) { return S.h_stage[slot]; }
+    bool launch(int slot, const dcr_bgzf_member *rel, int32_t n, size_t nin, Event start, Event done) {
         dinf::Args a = h->base;
         a.in = S.d_in[slot];
         a.out = S.d_out[slot];
@@ -910,25 +843,56 @@ void stream_produce(dcr_inflate_stream *st) {
         a.status = S.d_st[slot];
         a.dbg = nullptr;
         a.n = n;
-        (void)hipMemcpyAsync(S.d_in[slot], S.h_stage[slot], nin, hipMemcpyHostToDevice, S.s_k);
-        (void)hipMemcpyAsync(S.d_m[slot], mr.data(), (size_t)n * sizeof(dcr_bgzf_member), hipMemcpyHostToDevice, S.s_k);
-        (void)hipEventRecord(sp.start, S.s_k);
+        // rel is the producer's per-slot copy: it is rewritten only after
+        // this span is done (the protocol waits for `done` before reusing)
+        if (hipMemcpyAsync(S.d_in[slot], S.h_stage[slot], nin, hipMemcpyHostToDevice, S.s_k) != hipSuccess ||
+            hipMemcpyAsync(S.d_m[slot], rel, (size_t)n * sizeof(dcr_bgzf_member), hipMemcpyHostToDevice, S.s_k) !=
+                hipSuccess ||
+            hipEventRecord(start, S.s_k) != hipSuccess)
+            return false;
         hipLaunchKernelGGL(dinf::k_inflate, dim3((unsigned)n), dim3(64), sizeof(dinf::WaveLds), S.s_k, a);
-        (void)hipMemcpyAsync(S.h_st[slot], S.d_st[slot], (size_t)n, hipMemcpyDeviceToHost, S.s_k);
-        (void)hipEventRecord(sp.done, S.s_k);
-        {
-            // the slot's staging and mrel are reused kSlots spans later,
-            // after the reader has fetched this span (its event done)
-            std::lock_guard<std::mutex> g(st->mu);
-            sp.launched = true;
-        }
-        st->cv.notify_all();
+        return hipGetLastError() == hipSuccess &&
+               hipMemcpyAsync(S.h_st[slot], S.d_st[slot], (size_t)n, hipMemcpyDeviceToHost, S.s_k) == hipSuccess &&
+               hipEventRecord(done, S.s_k) == hipSuccess;
     }
-    std::lock_guard<std::mutex> g(st->mu);
-    st->produced = true;
-    st->cv.notify_all();
-}
+    bool wait(Event start, Event done, float *ms) {
+        if (hipEventSynchronize(done) != hipSuccess) return false;
+        if (ms) {
+            *ms = 0;
+            (void)hipEventElapsedTime(ms, start, done);
+        }
+        return true;
+    }
+    const uint8_t *status(int slot) { return S.h_st[slot]; }
+    bool copy_out(uint8_t *dst, int slot, int64_t off, int64_t n) {
+        return hipMemcpyAsync(dst, S.d_out[slot] + off, (size_t)n, hipMemcpyDeviceToHost, S.s_out) == hipSuccess;
+    }
+    bool sync_out() { return hipStreamSynchronize(S.s_out) == hipSuccess; }
+    void drain() {
+        (void)hipSetDevice(h->device);
+        if (S.s_k) (void)hipStreamSynchronize(S.s_k);
+        if (S.s_out) (void)hipStreamSynchronize(S.s_out);
+    }
+    void account(float ms, int32_t members, int64_t bytes) {
+        std::lock_guard<std::mutex> g(h->mu);
+        if (members) {
+            h->tot[0] += ms;
+            h->tot[1] += 1;
+            h->tot[2] += members;
+        }
+        h->tot[3] += (double)bytes;
+    }
+    void error(const std::string &msg) { dcr::set_error(DCR_EARG, msg); }
+};
 }  // namespace
+
+static_assert(InflSlots::kSlots == dcr_span::kSlots, "one device slot per protocol slot");
+
+struct dcr_inflate_stream {
+    HipSpanBackend be;
+    dcr_span::Stream<HipSpanBackend> s;
+    dcr_inflate_stream(dcr_inflater *h, const uint8_t *file) : be{h, *h->slots}, s(be, file) {}
+};
 
 extern "C" dcr_inflate_stream *dcr_inflate_stream_open(dcr_inflater *h, const uint8_t *file) {
     if (!h || !file) {
@@ -944,18 +908,17 @@ extern "C" dcr_inflate_stream *dcr_inflate_stream_open(dcr_inflater *h, const ui
         }
         h->slots->busy = true;
     }
-    auto *st = new dcr_inflate_stream;
-    st->h = h;
-    st->sl = h->slots;
-    st->file = file;
+    InflSlots &S = *h->slots;
     (void)hipSetDevice(h->device);
-    if ((!st->sl->s_k && hipStreamCreateWithFlags(&st->sl->s_k, hipStreamNonBlocking) != hipSuccess) ||
-        (!st->sl->s_out && hipStreamCreateWithFlags(&st->sl->s_out, hipStreamNonBlocking) != hipSuccess)) {
-        dcr_inflate_stream_close(st);
+    if ((!S.s_k && hipStreamCreateWithFlags(&S.s_k, hipStreamNonBlocking) != hipSuccess) ||
+        (!S.s_out && hipStreamCreateWithFlags(&S.s_out, hipStreamNonBlocking) != hipSuccess)) {
+        std::lock_guard<std::mutex> g(h->mu);
+        S.busy = false;
         dcr::set_error(DCR_EHIP, "dcr_inflate_stream_open: HIP setup failed");
         return nullptr;
     }
-    st->producer = std::thread(stream_produce, st);
+    auto *st = new dcr_inflate_stream(h, file);
+    st->s.start();
     return st;
 }
 
@@ -964,96 +927,22 @@ extern "C" int dcr_inflate_stream_add(dcr_inflate_stream *st, const dcr_bgzf_mem
     for (int32_t i = 0; i < n; ++i)
         if (m[i].isize > 65536 || m[i].in_off < 0 || m[i].out_off < 0)
             return dcr::set_error(DCR_EARG, "dcr_inflate_stream_add: member out of range");
-    {
-        std::lock_guard<std::mutex> g(st->mu);
-        st->m.insert(st->m.end(), m, m + n);
-        if (last) st->m_done = true;
-    }
-    st->cv.notify_all();
-    return 0;
+    return st->s.add(m, n, last);
 }
 
 extern "C" int dcr_inflate_stream_fetch(dcr_inflate_stream *st, int64_t out_off, int64_t n, uint8_t *dst) {
     if (!st || n < 0 || (n && !dst)) return -1;
-    if (n == 0) return 0;
-    (void)hipSetDevice(st->h->device);
-    InflSlots &S = *st->sl;
-    const int64_t end = out_off + n;
-    for (size_t k = 0;; ++k) {
-        dcr_inflate_stream::Span *spp;
-        {
-            std::unique_lock<std::mutex> lk(st->mu);
-            st->cv.wait(lk, [&] { return st->spans.size() > k || st->produced || st->err; });
-            if (st->spans.size() <= k) {
-                if (st->err) return -1;
-                dcr::set_error(DCR_EARG, "dcr_inflate_stream_fetch: range past the stream's members");
-                return -1;
-            }
-            spp = &st->spans[k];
-            if (spp->out0 >= end) break;
-            if (spp->out1 <= out_off) continue;
-            st->cv.wait(lk, [&] { return spp->launched || st->err; });
-            if (!spp->launched) return -1;
-        }
-        auto &sp = *spp;
-        const int slot = (int)(k % dcr_inflate_stream::kSlots);
-        if (!sp.checked) {
-            if (hipEventSynchronize(sp.done) != hipSuccess) return -1;
-            for (int32_t i = 0; i < sp.m1 - sp.m0; ++i)
-                if (S.h_st[slot][i] != dinf::ST_OK) {
-                    sp.rc = sp.m0 + i + 1;
-                    break;
-                }
-            sp.checked = true;
-            float ms = 0;
-            (void)hipEventElapsedTime(&ms, sp.start, sp.done);
-            std::lock_guard<std::mutex> g(st->h->mu);
-            st->h->tot[0] += ms;
-            st->h->tot[1] += 1;
-            st->h->tot[2] += sp.m1 - sp.m0;
-        }
-        if (sp.rc) {
-            dcr::set_error(DCR_EARG, "BGZF member " + std::to_string(sp.rc - 1) + " failed to inflate or CRC mismatch");
-            return sp.rc;
-        }
-        const int64_t a = std::max(out_off, sp.out0), b = std::min(end, sp.out1);
-        if (hipMemcpyAsync(dst + (a - out_off), S.d_out[slot] + (a - sp.out0), (size_t)(b - a), hipMemcpyDeviceToHost,
-                           S.s_out) != hipSuccess)
-            return -1;
-        if (sp.out1 >= end) break;
-    }
-    if (hipStreamSynchronize(S.s_out) != hipSuccess) return -1;
-    {
-        std::lock_guard<std::mutex> g(st->mu);
-        st->fetched = std::max(st->fetched, end);
-    }
-    st->cv.notify_all();
-    std::lock_guard<std::mutex> g(st->h->mu);
-    st->h->tot[3] += (double)n;
-    return 0;
+    (void)hipSetDevice(st->be.h->device);
+    return st->s.fetch(out_off, n, dst);
 }
 
 extern "C" void dcr_inflate_stream_close(dcr_inflate_stream *st) {
     if (!st) return;
-    {
-        std::lock_guard<std::mutex> g(st->mu);
-        st->stop = true;
-    }
-    st->cv.notify_all();
-    if (st->producer.joinable()) st->producer.join();
-    (void)hipSetDevice(st->h->device);
-    if (st->sl->s_k) (void)hipStreamSynchronize(st->sl->s_k);
-    if (st->sl->s_out) (void)hipStreamSynchronize(st->sl->s_out);
-    for (auto &sp : st->spans)
-    {
-        if (sp.start) (void)hipEventDestroy(sp.start);
-        if (sp.done) (void)hipEventDestroy(sp.done);
-    }
-    {
-        std::lock_guard<std::mutex> g(st->h->mu);
-        st->sl->busy = false;
-    }
+    st->s.close();
+    dcr_inflater *h = st->be.h;
     delete st;
+    std::lock_guard<std::mutex> g(h->mu);
+    h->slots->busy = false;
 }
 
 static void *hook_stream_open(void *u, const uint8_t *file) {

@@ -512,29 +512,33 @@ class Inflater {
     // (the walk fill() makes chunk by chunk) and appends them in batches, the
     // first small so the first launch starts at once.  On anything
     // unexpected it stops appending; fill()'s own walk then reports it.
+    // Called before th_ starts: the walk's start offset is read here, on the
+    // constructing thread, never by mth_ (fill() on th_ advances cbeg_; a
+    // late-scheduled mth_ would start the stream at a later member, shifting
+    // every fetch while each member's CRC still passed).
     void open_stream() {
         stream_ = hook_.stream_open(hook_.user, map_);
         if (!stream_) return;
         stream_out_ = 0;
-        mth_ = std::thread([this] { scan_members(); });
+        const size_t p0 = cbeg_, p_end = cend_;
+        mth_ = std::thread([this, p0, p_end] { scan_members(p0, p_end); });
     }
-    void scan_members() {
+    void scan_members(size_t p, const size_t cend) {
         std::vector<dcr_bgzf_member> ms;
-        size_t p = cbeg_;
         int64_t out = 0;
         size_t batch = 128;
         auto flush = [&](bool last) {
             hook_.stream_add(stream_, ms.data(), (int32_t)ms.size(), last ? 1 : 0);
             ms.clear();
         };
-        while (p + 18 <= cend_ && !stop_members_.load(std::memory_order_relaxed)) {
+        while (p + 18 <= cend && !stop_members_.load(std::memory_order_relaxed)) {
             if (end_coff_ >= 0 && p >= (uint64_t)end_coff_) {
                 if (p != (uint64_t)end_coff_ || end_uoff_ == 0) break;
             }
             const uint8_t *h = map_ + p;
             if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) break;
             const size_t xlen = rd16(h + 10);
-            if (cend_ - p < 12 + xlen) break;
+            if (cend - p < 12 + xlen) break;
             long bsize = -1;
             for (size_t i = 0; i + 4 <= xlen;) {
                 const uint8_t *sf = h + 12 + i;
@@ -544,7 +548,7 @@ class Inflater {
             }
             if (bsize < 0) break;
             const size_t blen = (size_t)bsize + 1;
-            if (blen < 12 + xlen + 8 || cend_ - p < blen) break;
+            if (blen < 12 + xlen + 8 || cend - p < blen) break;
             const uint32_t isize = rd32(h + blen - 4);
             if (isize > 0x10000) break;
             ms.push_back(dcr_bgzf_member{(int64_t)(p + 12 + xlen), out, (uint32_t)(blen - 12 - xlen - 8), isize,

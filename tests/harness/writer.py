@@ -15,7 +15,7 @@ numpy 1.x printed it (``"[1, 2, 3]"``): the reference needs numpy < 1.24
 """
 from __future__ import annotations
 
-from .records import AlignedSegment
+from duplexumiconsensusreads_amd.records import AlignedSegment
 
 _PHRED33 = bytes((i + 33) & 0xff for i in range(256))
 

@@ -1,0 +1,216 @@
+// stream_host.cpp — TEST INFRASTRUCTURE: a host emulation of the device
+// inflater's hook (include/dcr_inflate.h) that runs the same span protocol
+// (csrc/dcr_span_stream.h) as libdcr.so's stream, with a worker thread in the
+// role of the GPU (zlib raw inflate per member, CRC32 and ISIZE checked) and
+// plain heap slot buffers that are freed and re-allocated when they grow, as
+// the device slots are.  Built with -fsanitize=thread / address by
+// tests/native/Makefile, it lets the CPU suite drive the real ingest
+// (libdcr_io) through the stream path on inputs of any BGZF block size.
+#include <zlib.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <memory>
+
+#include "../../duplexumiconsensusreads_amd/csrc/dcr_span_stream.h"
+
+namespace {
+
+struct Done {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+};
+
+struct Job {
+    int slot;
+    const dcr_bgzf_member *rel;
+    int32_t n;
+    std::shared_ptr<Done> done;
+};
+
+int inflate_member(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t isize, uint32_t crc) {
+    z_stream z{};
+    if (inflateInit2(&z, -15) != Z_OK) return 1;
+    z.next_in = const_cast<uint8_t *>(in);
+    z.avail_in = in_len;
+    uint8_t dummy;
+    z.next_out = isize ? out : &dummy;
+    z.avail_out = isize;
+    const int r = inflate(&z, Z_FINISH);
+    const uLong got = z.total_out;
+    inflateEnd(&z);
+    if (r != Z_STREAM_END || got != isize) return 1;
+    return (uint32_t)crc32(0L, out, isize) == crc ? 0 : 2;
+}
+
+// slot buffers that move when they grow (like hipFree + hipMalloc)
+struct Buf {
+    uint8_t *p = nullptr;
+    size_t cap = 0;
+    bool grow(size_t n) {
+        if (n <= cap) return true;
+        std::free(p);
+        p = (uint8_t *)std::malloc(n);
+        cap = p ? n : 0;
+        return p != nullptr;
+    }
+    ~Buf() { std::free(p); }
+};
+
+struct HostBackend {
+    using Event = std::shared_ptr<Done>;
+    Buf stage_[dcr_span::kSlots], out_[dcr_span::kSlots], st_[dcr_span::kSlots];
+    std::thread worker;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Job> q;
+    bool quit = false;
+    int64_t launches = 0, members = 0, bytes = 0;
+
+    HostBackend() { worker = std::thread([this] { run(); }); }
+    ~HostBackend() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            quit = true;
+        }
+        cv.notify_all();
+        worker.join();
+    }
+    void run() {
+        for (;;) {
+            Job j;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return quit || !q.empty(); });
+                if (q.empty()) return;
+                j = q.front();
+                q.pop_front();
+            }
+            for (int32_t i = 0; i < j.n; ++i) {
+                const dcr_bgzf_member &m = j.rel[i];
+                st_[j.slot].p[i] =
+                    (uint8_t)inflate_member(stage_[j.slot].p + m.in_off, m.in_len, out_[j.slot].p + m.out_off, m.isize,
+                                            m.crc);
+            }
+            {
+                std::lock_guard<std::mutex> g(j.done->mu);
+                j.done->done = true;
+            }
+            j.done->cv.notify_all();
+        }
+    }
+    bool new_events(Event &start, Event &done) {
+        start = std::make_shared<Done>();
+        done = std::make_shared<Done>();
+        return true;
+    }
+    void free_events(Event &start, Event &done) {
+        start.reset();
+        done.reset();
+    }
+    bool ensure(int slot, size_t nin, size_t nout, int32_t n) {
+        return stage_[slot].grow(nin + 16) && out_[slot].grow(nout + 16) && st_[slot].grow((size_t)n);
+    }
+    uint8_t *stage(int slot) { return stage_[slot].p; }
+    bool launch(int slot, const dcr_bgzf_member *rel, int32_t n, size_t, Event, Event done) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            q.push_back(Job{slot, rel, n, done});
+            ++launches;
+        }
+        cv.notify_all();
+        return true;
+    }
+    bool wait(Event, Event done, float *ms) {
+        std::unique_lock<std::mutex> lk(done->mu);
+        done->cv.wait(lk, [&] { return done->done; });
+        if (ms) *ms = 0;
+        return true;
+    }
+    const uint8_t *status(int slot) { return st_[slot].p; }
+    bool copy_out(uint8_t *dst, int slot, int64_t off, int64_t n) {
+        std::memcpy(dst, out_[slot].p + off, (size_t)n);
+        return true;
+    }
+    bool sync_out() { return true; }
+    void drain() {
+        std::unique_lock<std::mutex> lk(mu);
+        // the worker empties the queue; a job in flight signals its event
+        while (!q.empty()) {
+            lk.unlock();
+            std::this_thread::yield();
+            lk.lock();
+        }
+    }
+    void account(float, int32_t m, int64_t b) {
+        std::lock_guard<std::mutex> g(mu);
+        members += m;
+        bytes += b;
+    }
+    void error(const std::string &msg) { std::fprintf(stderr, "stream_host: %s\n", msg.c_str()); }
+};
+
+struct HostStream {
+    HostBackend be;
+    dcr_span::Stream<HostBackend> s;
+    explicit HostStream(const uint8_t *file) : s(be, file) {}
+    ~HostStream() { s.close(); }   // the protocol stops before the backend's worker
+};
+
+std::mutex g_mu;
+int64_t g_streams = 0, g_spans = 0, g_members = 0, g_bytes = 0;
+
+void *h_open(void *, const uint8_t *file) {
+    auto *hs = new HostStream(file);
+    hs->s.start();
+    std::lock_guard<std::mutex> g(g_mu);
+    ++g_streams;
+    return hs;
+}
+int h_add(void *s, const dcr_bgzf_member *m, int32_t n, int32_t last) {
+    return ((HostStream *)s)->s.add(m, n, last);
+}
+int h_fetch(void *s, int64_t off, int64_t n, uint8_t *dst) { return ((HostStream *)s)->s.fetch(off, n, dst); }
+void h_close(void *s) {
+    auto *hs = (HostStream *)s;
+    hs->s.close();
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        g_spans += hs->be.launches;
+        g_members += hs->be.members;
+        g_bytes += hs->be.bytes;
+    }
+    delete hs;
+}
+int h_run(void *, const uint8_t *in, int64_t, const dcr_bgzf_member *m, int32_t n, uint8_t *out, int64_t) {
+    for (int32_t i = 0; i < n; ++i)
+        if (inflate_member(in + m[i].in_off, m[i].in_len, out + m[i].out_off, m[i].isize, m[i].crc)) return i + 1;
+    return 0;
+}
+void *h_alloc(void *, size_t bytes) { return std::malloc(bytes); }
+void h_free(void *, void *p) { std::free(p); }
+
+}  // namespace
+
+extern "C" {
+// the hook (streaming when the ingest maps its input)
+void dcr_test_stream_hook(dcr_inflate_hook *hook) {
+    hook->user = nullptr;
+    hook->run = h_run;
+    hook->host_alloc = h_alloc;
+    hook->host_free = h_free;
+    hook->stream_open = h_open;
+    hook->stream_add = h_add;
+    hook->stream_fetch = h_fetch;
+    hook->stream_close = h_close;
+}
+// streams opened, spans launched, members checked, bytes fetched (totals)
+void dcr_test_stream_stats(int64_t *out4) {
+    std::lock_guard<std::mutex> g(g_mu);
+    out4[0] = g_streams;
+    out4[1] = g_spans;
+    out4[2] = g_members;
+    out4[3] = g_bytes;
+}
+}

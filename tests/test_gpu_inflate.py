@@ -214,3 +214,55 @@ def test_ingest_gpu_inflate_corrupt_block(tmp_path):
                     raise RuntimeError(hb.error()[1])
                 break
     ing.close()
+
+
+def _with_gpu_inflate(flag, fn):
+    from duplexumiconsensusreads_amd import cli
+    old = os.environ.get("DCR_GPU_INFLATE")
+    os.environ["DCR_GPU_INFLATE"] = flag
+    try:
+        cli.gpu_inflate(0)
+        return fn()
+    finally:
+        if old is None:
+            os.environ.pop("DCR_GPU_INFLATE", None)
+        else:
+            os.environ["DCR_GPU_INFLATE"] = old
+        cli.gpu_inflate(0)
+
+
+def test_stream_small_bgzf_blocks_same_outputs_as_host_inflate(tmp_path):
+    """Blocks of 0.5-4 KiB of data (any size is valid BGZF): one 64 MiB ingest
+    chunk then covers more than the stream's four slots of spans, the case the
+    per-span `fetched` mark fixes (csrc/dcr_span_stream.h).  CLI outputs and
+    stdout equal the host pool's."""
+    from duplexumiconsensusreads_amd import bam
+    from .bgzf_util import reblock
+    big = str(tmp_path / "big.bam")
+    synth.write_packed_bam(big, synth.packed_fixed_size(8000, seed=13), seed=13, level=1)
+    inp = str(tmp_path / "small.bam")
+    assert reblock(big, inp, 512, 4096, seed=2) > 25_000
+    so_gpu = _cli(inp, str(tmp_path / "g.bam"), "1")
+    so_host = _cli(inp, str(tmp_path / "h.bam"), "0")
+    assert so_gpu == so_host
+    for suf in (".bam", "_filteredreads.bam", "_filteredfamilies.bam"):
+        assert bam.bgzf_stream(str(tmp_path / ("g" + suf))) == bam.bgzf_stream(str(tmp_path / ("h" + suf)))
+
+
+def test_stream_ranged_ingest_same_batches_as_host_inflate(tmp_path):
+    """The sharded CLI's ranged ingests (dcr_split_points, start/end virtual
+    offsets) through the device stream pack the same batches, family table and
+    side records as through the host pool, part by part."""
+    from duplexumiconsensusreads_amd import native_io
+    from duplexumiconsensusreads_amd.params import ConsensusParams
+    from .bgzf_util import ingest_digest
+    inp = str(tmp_path / "in.bam")
+    synth.write_packed_bam(inp, synth.packed_config(synth.CONFIGS["C5"], 40_000, seed=6), seed=6, level=6)
+    pts = native_io.split_points(inp, 3, ConsensusParams())
+    assert all(p > 0 for p in pts)
+    bounds = list(zip([0] + pts, pts + [-1]))
+    for lo, hi in bounds:
+        g = _with_gpu_inflate("1", lambda: ingest_digest(inp, lo, hi))
+        h = _with_gpu_inflate("0", lambda: ingest_digest(inp, lo, hi))
+        assert g[3] and not h[3]
+        assert g[:3] == h[:3], (lo, hi)

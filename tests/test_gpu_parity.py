@@ -256,42 +256,3 @@ def test_gpu_deep_records_edge_bytes(ctx, seed, minbq, rate):
     finally:
         ctx.set_params(ConsensusParams())
 
-
-# k_consensus_pair (two single-strand records per wave; off by default, on
-# with DCR_PAIR=1 read at context creation): the same bits as the fast kernel
-# on the C2 shape, mixed shapes and the decision borderline.
-@pytest.fixture(scope="module")
-def ctx_pair():
-    import os
-    old = os.environ.get("DCR_PAIR")
-    os.environ["DCR_PAIR"] = "1"
-    try:
-        c = _lib.Context(ConsensusParams(), device=0, want_info=True)
-    finally:
-        if old is None:
-            del os.environ["DCR_PAIR"]
-        else:
-            os.environ["DCR_PAIR"] = old
-    yield c
-    c.close()
-
-
-@pytest.mark.parametrize("seed,kind", [(1, "C1"), (2, "indel"), (3, "clip"), (5, "wild"), (8, "len90")])
-def test_gpu_pair_kernel_matches_oracle(ctx_pair, seed, kind):
-    packed = synth.packed_from_records(random_cfg(kind, seed))
-    params = ConsensusParams(max_reads=10_000)
-    ctx_pair.set_params(params)
-    got = ctx_pair.run_host(packed)
-    want = dcr_oracle_c.run(packed, params)
-    assert_same(packed, got, want)
-    for k in ("seq_start", "len", "status", "has_ins"):
-        assert np.array_equal(got[2][k], want[2][k]), k
-
-
-def test_gpu_pair_kernel_c2_shape(ctx_pair):
-    packed = synth.packed_fixed_size(20_000, seed=11)
-    params = ConsensusParams()
-    ctx_pair.set_params(params)
-    got = ctx_pair.run_host(packed)
-    want = dcr_oracle_c.run(packed, params, n_threads=8)
-    assert_same(packed, got, want)

@@ -19,7 +19,9 @@ import subprocess
 import numpy as np
 import pytest
 
-from duplexumiconsensusreads_amd import bam, native_io, pipeline, synth
+from duplexumiconsensusreads_amd import bam, native_io, synth
+
+from .harness import pipeline
 from duplexumiconsensusreads_amd.batch import BATCH_FIELDS, pack_families
 from duplexumiconsensusreads_amd.params import ConsensusParams
 

@@ -4,7 +4,7 @@ import random
 
 import pytest
 
-from duplexumiconsensusreads_amd import pipeline
+from .harness import pipeline
 from duplexumiconsensusreads_amd.params import ConsensusParams
 from oracle import dcr_oracle_c
 from tests.golden_io import input_record, load_families

@@ -5,7 +5,7 @@ import random
 import numpy as np
 import pytest
 
-from duplexumiconsensusreads_amd import writer
+from .harness import writer
 from oracle import dcr_oracle as O
 from tests.golden_io import input_record, load_families, load_kats
 

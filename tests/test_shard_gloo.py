@@ -10,7 +10,9 @@ import socket
 import pytest
 import torch.multiprocessing as mp
 
-from duplexumiconsensusreads_amd import bam, pipeline, shard
+from duplexumiconsensusreads_amd import bam
+
+from .harness import pipeline, shard
 from duplexumiconsensusreads_amd.params import ConsensusParams
 from tests.golden_io import GOLDEN
 

@@ -4,7 +4,9 @@ each rank generating only its own families (synth.packed_config keep=)."""
 import numpy as np
 import pytest
 
-from duplexumiconsensusreads_amd import batch, shard, synth
+from duplexumiconsensusreads_amd import batch, synth
+
+from .harness import shard
 from duplexumiconsensusreads_amd.params import ConsensusParams
 from oracle import dcr_oracle_c
 
