@@ -27,11 +27,15 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
 owns its own shard of families: weak scaling, no data-path collective.  C4
 at N > 1 deals one shared stream of N x 1,000 families to the ranks by LPT.)
 
---sharded: strong scaling of the drop-in itself: ONE input BAM (rank 0's
-batch) through the sharded CLI (cli --gpus: split points at family starts,
-one process per GPU over its range, parallel part merge), every pass between
-barriers on all ranks.  --in-level sets the input's BGZF level (default 1;
-6 is samtools' default).
+N > 1 (the driver's scaling runs) times the drop-in's own multi-GPU mode by
+default: ONE input BAM holding every rank's families (N x 312,500 on C2,
+assembled from the ranks' BGZF pieces) through the sharded CLI (cli --gpus:
+split points at family starts, one process per GPU over its range, parallel
+part merge), every pass between barriers on all ranks; per-GPU work is fixed
+("weak").  --independent times one private BAM per rank instead.
+--sharded-input-of-rank0 splits rank 0's batch alone over the N ranks
+(strong scaling of one 10 M-read input).  --in-level sets the input's BGZF
+level (default 1; 6 is samtools' default).
 """
 from __future__ import annotations
 
@@ -181,6 +185,38 @@ def device_resident(packed, params, local, steps, warmup):
     return {k: v / steps for k, v in kms.items()}, bases, n_bad, dt / steps
 
 
+def one_input_bam(path, packed, seed, level, rank, world, tdist):
+    """ONE BAM of every rank's families (the sharded CLI's input at N > 1):
+    each rank writes its records as BGZF blocks, rank 0 the header, and every
+    rank copies its piece (EOF block dropped) to its offset in ``path`` (an
+    exclusive scan of the piece sizes), as the CLI's parallel merge does."""
+    from duplexumiconsensusreads_amd import cli, native_io, synth
+    eof = len(cli._BGZF_EOF)
+    piece = f"{path}.piece{rank}"
+    synth.write_packed_bam(piece, packed, seed=seed, level=level, header=False)
+    head = f"{path}.head"
+    if rank == 0:
+        w = native_io.BgzfWriter(head, synth.BamHeader_bytes(), level=level)
+        w.close()
+    sizes = [None] * world
+    tdist.all_gather_object(sizes, os.path.getsize(piece) - eof)
+    tdist.barrier()
+    hl = os.path.getsize(head) - eof
+    if rank == 0:
+        with open(path, "wb") as f:
+            f.truncate(hl + sum(sizes) + eof)
+        fd = os.open(path, os.O_WRONLY)
+        cli._copy_range(head, fd, hl, 0)
+        os.pwrite(fd, cli._BGZF_EOF, hl + sum(sizes))
+        os.close(fd)
+    tdist.barrier()
+    fd = os.open(path, os.O_WRONLY)
+    cli._copy_range(piece, fd, sizes[rank], hl + sum(sizes[:rank]))
+    os.close(fd)
+    os.remove(piece)
+    tdist.barrier()
+
+
 def e2e_passes(path, params_args, device, steps, warmup, workdir):
     """W untimed + K timed CLI runs over the BAM at ``path``; returns
     (seconds of the K runs, stats of the last run)."""
@@ -295,8 +331,11 @@ def main():
     ap.add_argument("--kernel-only", action="store_true", help="skip the whole-node CLI runs")
     ap.add_argument("--kernel-steps", type=int, default=10, help="device-resident passes for the roofline")
     ap.add_argument("--sharded", action="store_true",
-                    help="strong scaling: ONE input BAM (rank 0's batch) through the sharded CLI, one process "
-                         "per GPU over ranges of whole families (cli._main_sharded), instead of one BAM per rank")
+                    help="the sharded CLI over ONE input (the default at N > 1; at N = 1 the plain CLI)")
+    ap.add_argument("--independent", action="store_true",
+                    help="N > 1: one private BAM per rank through the plain CLI (no sharding)")
+    ap.add_argument("--sharded-input-of-rank0", action="store_true",
+                    help="strong scaling: ONE input of rank 0's batch only, split over the N ranks")
     ap.add_argument("--in-level", type=int, default=1, help="BGZF compression level of the synthetic input BAM")
     ap.add_argument("--max-reads", type=int, default=None,
                     help="--max_reads of the CLI runs (default: the reference's 100; C4: 1000, the whole deep "
@@ -311,6 +350,9 @@ def main():
     # on a one-GPU box); counting devices does not initialise the GPU
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     dist = world > 1
+    # N > 1: the drop-in's own multi-GPU mode (one input, cli --gpus) unless --independent
+    args.sharded = (args.sharded or args.sharded_input_of_rank0 or dist) and not args.independent
+    one_input_of_all = args.sharded and not args.sharded_input_of_rank0
     dev = f"cuda:{local}"
     tdist = None
     if dist:
@@ -359,9 +401,13 @@ def main():
         if not args.kernel_only:
             bam_path = os.path.join(workdir, "in.bam")
             t0 = time.perf_counter()
-            if rank == 0 or not args.sharded:
-                synth.write_packed_bam(bam_path, bam_packed if bam_packed is not None else packed,
-                                       seed=args.seed + 1000 * rank, level=args.in_level)
+            src = bam_packed if bam_packed is not None else packed
+            if one_input_of_all and dist:
+                one_input_bam(bam_path, src, args.seed + 1000 * rank, args.in_level, rank, world, tdist)
+                log(f"[rank {rank}] one input of {world} ranks' families: {os.path.getsize(bam_path) / 1e6:.0f} MB "
+                    f"BAM (level {args.in_level}) in {time.perf_counter() - t0:.1f} s")
+            elif rank == 0 or not args.sharded:
+                synth.write_packed_bam(bam_path, src, seed=args.seed + 1000 * rank, level=args.in_level)
                 log(f"[rank {rank}] wrote {os.path.getsize(bam_path) / 1e6:.0f} MB BAM (level {args.in_level}) "
                     f"in {time.perf_counter() - t0:.1f} s")
             if dist:
@@ -383,7 +429,7 @@ def main():
 
     e2e_bases = stats.get("consensus_bases", 0) * args.steps
     in_bases = int((bam_packed if bam_packed is not None else packed).seq_len.astype(np.int64).sum()) * args.steps
-    if args.sharded and rank != 0:
+    if args.sharded and not one_input_of_all and rank != 0:
         in_bases = 0            # one input: rank 0's batch
     # per-rank busy time of the last CLI pass (whole pass, ingest thread, waits on the device)
     mine = {"rank": rank, "e2e_s_per_pass": (e2e_s or 0.0) / max(args.steps, 1),
@@ -425,12 +471,15 @@ def main():
         res = {
             "metric": METRIC, "value": value, "unit": "consensus bases/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
-            "higher_is_better": True, "scaling": "strong" if args.sharded else "weak", "vs_baseline": None,
+            "higher_is_better": True,
+            "scaling": "strong" if (args.sharded and not one_input_of_all) else "weak", "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": WORKLOAD[args.config] + (
-                           f"; --sharded: ONE input of {packed.n_reads} reads split over the {world} GPU(s) by "
-                           "the sharded CLI" if args.sharded else ""),
+                           (f"; ONE input of {world} x {packed.n_reads} reads (every rank's families) split over the "
+                            f"{world} GPUs by the sharded CLI (cli --gpus {world})" if one_input_of_all else
+                            f"; ONE input of {packed.n_reads} reads split over the {world} GPU(s) by the sharded CLI")
+                           if args.sharded and dist else ""),
                        "value_is": value_kind, "input_bgzf_level": args.in_level, "max_reads": max_reads,
                        "input_reads_per_gpu": (bam_packed if bam_packed is not None else packed).n_reads,
                        "families_per_gpu": packed.n_fam, "reads_per_gpu": packed.n_reads,
@@ -441,7 +490,7 @@ def main():
                                            "ms_per_step": dev_slowest * 1e3, "kernel_ms": kavg,
                                            "records_not_ok": n_bad},
                        "single_strand_stage_GBps": alg / (sum(kavg[k] for k in _lib.KERNELS[0:4]) / 1e3) / 1e9,
-                       "parallelism": (f"one input sharded x{world} by ranges of whole families (cli --gpus), "
+                       "parallelism": (f"one input sharded x{world} by ranges of whole families (cli --gpus {world}), "
                                        "one process per GPU, parallel part merge, no data-path collective"
                                        if args.sharded else
                                        f"family-sharded x{world}, one process per GPU, no data-path collective"),

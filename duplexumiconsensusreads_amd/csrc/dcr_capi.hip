@@ -18,7 +18,6 @@
 #include "dcr_internal.h"
 #include "dcr_deflate.h"
 #include "dcr_writer.h"
-#include <hipcub/hipcub.hpp>
 
 namespace {
 thread_local std::string g_err;
@@ -793,11 +792,7 @@ int dcr_submit_write(dcr_ctx *c, int slot, const dcr_batch *h, const dcr_wmeta *
     // writer buffers
     const int64_t B = stream_bound(h, m);
     const int64_t nbm = B / (int64_t)dfl::kMaxIn + 2;
-    size_t scan1 = 0, scan2 = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan1, (const int64_t *)nullptr, (int64_t *)nullptr,
-                                             (int)(2 * F + 1)));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan2, (const int64_t *)nullptr, (int64_t *)nullptr,
-                                             (int)(nbm + 1)));
+    const size_t scan1 = dcrw::scan_tmp_bytes((int)(2 * F + 1)), scan2 = dcrw::scan_tmp_bytes((int)(nbm + 1));
     size_t wo = 0;
     auto take = [&](size_t bytes) { size_t o = wo; wo = align_up(wo + std::max<size_t>(bytes, 1)); return o; };
     const size_t o_names = take((size_t)m->n_names + 1);
@@ -855,8 +850,7 @@ int dcr_submit_write(dcr_ctx *c, int slot, const dcr_batch *h, const dcr_wmeta *
         const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((2 * F + 3) / 4, (int64_t)c->n_cu * 8));
         hipLaunchKernelGGL(dcrw::k_fmt_size, dim3(g), dim3(256), 0, c->stream, A);
         HIP_TRY(hipGetLastError());
-        size_t tb = std::max(scan1, scan2);
-        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(wb + o_scan, tb, rsz, A.rec_off, (int)(2 * F + 1), c->stream));
+        HIP_TRY(dcrw::scan_excl_i64(rsz, A.rec_off, (int)(2 * F + 1), (int64_t *)(wb + o_scan), c->stream));
         hipLaunchKernelGGL(dcrw::k_fmt_write, dim3(g), dim3(256), 0, c->stream, A);
         HIP_TRY(hipGetLastError());
     } else {
@@ -866,9 +860,8 @@ int dcr_submit_write(dcr_ctx *c, int slot, const dcr_batch *h, const dcr_wmeta *
     dcrw::DflArgs D{A.stream, A.rec_off + 2 * F, (uint8_t *)(wb + o_slots), bsz, (uint32_t *)(wb + o_tok), nullptr};
     hipLaunchKernelGGL(dcrw::k_deflate, dim3(gd), dim3(dfl::kT), sizeof(dfl::Shared), c->stream, D);
     HIP_TRY(hipGetLastError());
-    size_t tb = std::max(scan1, scan2);
     int64_t *boff = (int64_t *)(wb + o_boff);
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(wb + o_scan, tb, bsz, boff, (int)(nbm + 1), c->stream));
+    HIP_TRY(dcrw::scan_excl_i64(bsz, boff, (int)(nbm + 1), (int64_t *)(wb + o_scan), c->stream));
     dcrw::CompactArgs C{(const uint8_t *)(wb + o_slots), bsz, boff, A.rec_off + 2 * F,
                         (uint8_t *)(wb + o_comp), (int64_t *)(wb + o_tot)};
     hipLaunchKernelGGL(dcrw::k_compact, dim3(gd), dim3(256), 0, c->stream, C);

@@ -49,4 +49,9 @@ __global__ void k_fmt_write(FmtArgs A);
 __global__ void k_deflate(DflArgs D);
 __global__ void k_compact(CompactArgs C);
 
+// exclusive prefix sum out[i] = in[0] + .. + in[i-1] (in != out), tmp of
+// scan_tmp_bytes(n) bytes; launches on s
+size_t scan_tmp_bytes(int n);
+hipError_t scan_excl_i64(const int64_t *in, int64_t *out, int n, int64_t *tmp, hipStream_t s);
+
 }  // namespace dcrw

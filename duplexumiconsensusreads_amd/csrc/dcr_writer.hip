@@ -9,7 +9,6 @@
 // byte layout is exactly the host formatter's (csrc/dcr_format.cpp), which
 // tests/test_cli_e2e.py pins to the Python record codec.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include "dcr_deflate.h"
 #include "dcr_internal.h"
@@ -557,6 +556,86 @@ __global__ __launch_bounds__(256) void k_compact(CompactArgs C) {
         C.totals[1] = 0;
         C.totals[2] = 0;
     }
+}
+
+
+// ---- exclusive prefix sums of int64 (record sizes -> record offsets, block
+// sizes -> block offsets).  Tiles of 2,048 values per 256-lane workgroup: each
+// lane sums its 8 consecutive values, the workgroup scans the lane sums (wave
+// shuffles, then the four wave totals through LDS) and writes the tile's
+// exclusive prefixes; tile totals go to `part`.  More than one tile: one
+// workgroup scans the tile totals, and every tile after the first adds its
+// prefix.  Plain launches, no inter-workgroup waiting.
+constexpr int kScanT = 256, kScanPer = 8, kScanTile = kScanT * kScanPer;
+
+__device__ __forceinline__ int64_t wg_excl_scan(int64_t v, int64_t &total, int64_t *wsum) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int64_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int64_t before = 0;
+    for (int k = 0; k < w; ++k) before += wsum[k];
+    total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+    return before + x - v;
+}
+
+__global__ __launch_bounds__(kScanT) void k_scan_tiles(const int64_t *in, int64_t *out, int64_t *part, int n) {
+    __shared__ int64_t wsum[4];
+    const int64_t t0 = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanPer;
+    int64_t v[kScanPer], s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        v[k] = t0 + k < n ? in[t0 + k] : 0;
+        s += v[k];
+    }
+    int64_t total;
+    int64_t run = wg_excl_scan(s, total, wsum);
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        if (t0 + k < n) out[t0 + k] = run;
+        run += v[k];
+    }
+    if (part && threadIdx.x == 0) part[blockIdx.x] = total;
+}
+
+// one workgroup: exclusive scan of the tile totals in place
+__global__ __launch_bounds__(kScanT) void k_scan_part(int64_t *part, int nt) {
+    __shared__ int64_t wsum[4];
+    int64_t carry = 0;
+    for (int base = 0; base < nt; base += kScanT) {
+        const int i = base + (int)threadIdx.x;
+        const int64_t v = i < nt ? part[i] : 0;
+        int64_t total;
+        const int64_t e = wg_excl_scan(v, total, wsum);
+        if (i < nt) part[i] = carry + e;
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(kScanT) void k_scan_add(int64_t *out, const int64_t *part, int n) {
+    const int64_t add = part[blockIdx.x + 1];
+    const int64_t t0 = (int64_t)(blockIdx.x + 1) * kScanTile;
+    for (int k = (int)threadIdx.x; k < kScanTile; k += kScanT)
+        if (t0 + k < n) out[t0 + k] += add;
+}
+
+size_t scan_tmp_bytes(int n) { return 8 * (size_t)((n + kScanTile - 1) / kScanTile + 1); }
+
+hipError_t scan_excl_i64(const int64_t *in, int64_t *out, int n, int64_t *tmp, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int nt = (n + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)nt), dim3(kScanT), 0, s, in, out, nt > 1 ? tmp : nullptr, n);
+    if (nt > 1) {
+        hipLaunchKernelGGL(k_scan_part, dim3(1), dim3(kScanT), 0, s, tmp, nt);
+        hipLaunchKernelGGL(k_scan_add, dim3((unsigned)(nt - 1)), dim3(kScanT), 0, s, out, (const int64_t *)tmp, n);
+    }
+    return hipGetLastError();
 }
 
 }  // namespace dcrw

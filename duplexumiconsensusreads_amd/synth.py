@@ -171,15 +171,16 @@ def write_config_bam(path, cfg: SynthConfig, n_families=None, seed=None):
     return path
 
 
-def write_packed_bam(path, packed, seed=0, level=1, n_threads=0, chunk_families=1 << 16):
+def write_packed_bam(path, packed, seed=0, level=1, n_threads=0, chunk_families=1 << 16, header=True):
     """Write the families of a packed batch (``packed_fixed_size`` /
     ``packed_config``) as a duplex BAM through the native record writer
     (include/dcr_io.h dcr_synth_write): the bench's 10 M+-read inputs.  UMIs
     are random per family (seeded); every read passes the reference's filters
-    (paired, proper, MAPQ >= 20 as generated)."""
+    (paired, proper, MAPQ >= 20 as generated).  header=False: the records'
+    BGZF blocks only (plus the EOF block), a piece of a larger BAM."""
     from . import native_io
     from .batch import PackedBatch
-    hdr = BamHeader_bytes()
+    hdr = BamHeader_bytes() if header else b""
     w = native_io.BgzfWriter(path, hdr, level=level, n_threads=n_threads)
     rng = np.random.default_rng(seed)
     F = packed.n_fam
