@@ -85,3 +85,30 @@ def test_cli_c4_default_max_reads_downsampled(tmp_path):
     assert so_gpu == so_cpu
     assert rng_gpu.getstate() == rng_cpu.getstate()
     _compare(str(tmp_path / "gpu.bam"), str(tmp_path / "cpu.bam"))
+
+
+def test_cli_device_writer_c3_shard(tmp_path):
+    """One GPU's share of C3 (100 M reads over 8 GPUs: 400 k families, ~12.3 M
+    reads) with its insertion layouts, deletions, soft clips and Zipf(1.5)
+    subfamily sizes 1..100, at BGZF level 6 and the CLI's default batch: the
+    general and exact kernels, the device writer and the device inflate all
+    on the product path, byte-compared with the oracle-backend CLI
+    (reference :473-545 insertion columns, :191-265 clips, :1519-1631)."""
+    inp = str(tmp_path / "c3.bam")
+    packed = synth.packed_config(synth.CONFIGS["C3"], 400_000, seed=3)
+    synth.write_packed_bam(inp, packed, seed=3, level=6)
+    n_fam = packed.n_fam
+    del packed
+    from duplexumiconsensusreads_amd.params import ConsensusParams
+    be = cli.default_backend(ConsensusParams())
+    assert be.device_writer
+    out_gpu = str(tmp_path / "gpu.bam")
+    out_cpu = str(tmp_path / "cpu.bam")
+    so_gpu, st_gpu = _run(inp, out_gpu, be, random.Random(4))
+    assert st_gpu["batches"] >= 20
+    assert st_gpu["consensus_records"] == 2 * n_fam
+    oracle = functools.partial(dcr_oracle_c.run, n_threads=min(16, os.cpu_count() or 1))
+    so_cpu, st_cpu = _run(inp, out_cpu, oracle, random.Random(4))
+    assert so_gpu == so_cpu
+    assert st_gpu["consensus_bases"] == st_cpu["consensus_bases"]
+    _compare(out_gpu, out_cpu)
