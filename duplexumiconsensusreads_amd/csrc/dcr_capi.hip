@@ -108,6 +108,7 @@ struct dcr_ctx {
     // pass (the exact pass takes them whole); DCR_EXACT_DIRECT_R overrides
     int direct_r = 3;
     uint16_t *d_llr16 = nullptr;   // device [128]
+    double *d_e1000 = nullptr;     // device [1001]: k / 1000 (the fast kernel's E)
     uint32_t *d_wtab = nullptr;    // device [DCR_LUT_N] (general kernel's decision pass)
     int n_cu = 256;     // compute units (persistent grid size)
     int dfl_blocks = 1; // resident k_deflate workgroups per CU (dynamic LDS = sizeof(dfl::Shared))
@@ -244,6 +245,7 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
         hi_prio_stream(&c->stream) != hipSuccess ||
         hipMalloc(&c->d_params, sizeof(dcr_params)) != hipSuccess ||
         hipMalloc(&c->d_llr16, 128 * sizeof(uint16_t)) != hipSuccess ||
+        hipMalloc(&c->d_e1000, 1001 * sizeof(double)) != hipSuccess ||
         hipMalloc(&c->d_wtab, DCR_LUT_N * sizeof(uint32_t)) != hipSuccess) {
         fail(DCR_EHIP, "context allocation failed");
         delete c;
@@ -266,7 +268,10 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
         c->dfl_blocks < 1)
         c->dfl_blocks = 1;
     c->host_params = *params;
+    double e1000[1001];
+    for (int k = 0; k <= 1000; ++k) e1000[k] = (double)k / 1000.0;   // IEEE division: numpy's rint(x)/1000
     if (hipMemcpy(c->d_params, params, sizeof(dcr_params), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_e1000, e1000, sizeof(e1000), hipMemcpyHostToDevice) != hipSuccess ||
         upload_fast(c, params) != DCR_OK) {
         fail(DCR_EHIP, "params upload failed");
         dcr_destroy(c);
@@ -296,6 +301,7 @@ void dcr_destroy(dcr_ctx *c) {
     if (c->ev_fetch) (void)hipEventDestroy(c->ev_fetch);
     if (c->d_params) (void)hipFree(c->d_params);
     if (c->d_llr16) (void)hipFree(c->d_llr16);
+    if (c->d_e1000) (void)hipFree(c->d_e1000);
     if (c->d_wtab) (void)hipFree(c->d_wtab);
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -426,6 +432,26 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         f.minbq = duplex ? -1 : c->host_params.min_base_quality;
         f.lo_check = duplex || c->host_params.min_base_quality < c->fast_qlo;
         f.llr16 = c->d_llr16;
+        f.e1000 = c->d_e1000;
+        {
+            // record-scalar stores at 32-bit offsets from the lowest array
+            // (k_consensus_fast): every array + its largest index within 4 GiB
+            const dcr_out &O = f.O;
+            const int64_t nrec = (duplex ? 2 : 4) * in->n_fam, ncol = duplex ? in->ds_cols : in->ss_cols;
+            const uint8_t *p[10] = {(const uint8_t *)O.pos, (const uint8_t *)O.mapq, (const uint8_t *)O.len,
+                                    (const uint8_t *)O.n_cig, (const uint8_t *)O.n_de, (const uint8_t *)O.D,
+                                    (const uint8_t *)O.M, (const uint8_t *)O.E, (const uint8_t *)O.E + 4,
+                                    (const uint8_t *)O.cigar};
+            const uint8_t *lo = p[0];
+            for (int k = 1; k < 10; ++k) lo = std::min(lo, p[k]);
+            bool ok = lo != nullptr;
+            for (int k = 0; k < 10 && ok; ++k) {
+                const uint64_t reach = (uint64_t)(p[k] - lo) + (k == 9 ? 4 * (uint64_t)ncol : (k == 7 || k == 8 ? 8 : 4) * (uint64_t)nrec);
+                ok = p[k] != nullptr && reach < 0xFFFFFFF0ull;
+                f.sofs[k] = (uint32_t)(p[k] - lo);
+            }
+            f.sbase = ok ? (uint8_t *)lo : nullptr;
+        }
         f.want_info = (c->options & DCR_OPT_READ_INFO) ? 1 : 0;
         f.direct_r = duplex ? 0 : c->direct_r;
         return f;

@@ -922,7 +922,8 @@ struct dcr_ingest {
     FILE *f = nullptr;
     IngestProf prof;
     dcr_ingest_cfg cfg{};
-    std::unique_ptr<Pool> pool;          // pack jobs
+    std::unique_ptr<Pool> pool;          // pack jobs (on the packer thread, below)
+    std::unique_ptr<Pool> ppool;         // record parse of serially scanned records (walk thread)
     std::unique_ptr<Inflater> infl;
     RecParser rp;
     // decompressed window: wb[wpos, wend) (a chunk's buffer, or big[] for huge leftovers)
@@ -952,6 +953,7 @@ struct dcr_ingest {
     std::vector<int> idx_tmp;
 
     ~dcr_ingest() {
+        pk_stop_thread();
         if (prof.on)
             std::fprintf(stderr,
                          "[ingest] walk %.3f s: chunk wait %.3f, serial scan %.3f, parse %.3f, pack copy %.3f; "
@@ -1007,7 +1009,67 @@ struct dcr_ingest {
     }
 
     // -- pack jobs -------------------------------------------------------------
+    // The walk appends a job per read it packs; every kPkStep jobs it hands
+    // the new ones to the packer thread, which copies them on the pool while
+    // the walk goes on (the copy had run between walk steps, the walk waiting
+    // for it: ~40 % of an ingest).  Jobs point into the current window and
+    // the batch, so the walk waits for the packer before the window moves
+    // (need()) and before the batch is handed out (next()).  `jobs` is
+    // reserved for the batch's reads, so it never reallocates under the packer.
     dcr_host_batch *hb = nullptr;
+    static constexpr size_t kPkStep = 4096;
+    std::thread pk_th;
+    std::mutex pk_mu;
+    std::condition_variable pk_cv;
+    size_t pk_sub = 0, pk_done = 0;      // jobs [0, pk_sub) handed over, [0, pk_done) copied
+    bool pk_quit = false;
+    const uint8_t *pk_w = nullptr;       // the window and batch of the handed-over jobs
+    dcr_host_batch *pk_b = nullptr;
+
+    void pk_start_thread() {
+        pk_th = std::thread([this] {
+            for (;;) {
+                size_t j0, j1;
+                const uint8_t *w;
+                dcr_host_batch *b;
+                {
+                    std::unique_lock<std::mutex> lk(pk_mu);
+                    pk_cv.wait(lk, [&] { return pk_quit || pk_sub > pk_done; });
+                    if (pk_quit) return;
+                    j0 = pk_done;
+                    j1 = pk_sub;
+                    w = pk_w;
+                    b = pk_b;
+                }
+                pack_range(w, b, jobs.data(), j0, j1);
+                {
+                    std::lock_guard<std::mutex> g(pk_mu);
+                    pk_done = j1;
+                }
+                pk_cv.notify_all();
+            }
+        });
+    }
+    void pk_stop_thread() {
+        if (!pk_th.joinable()) return;
+        {
+            std::lock_guard<std::mutex> g(pk_mu);
+            pk_quit = true;
+        }
+        pk_cv.notify_all();
+        pk_th.join();
+    }
+    // hand the jobs appended since the last hand-over to the packer
+    void kick_jobs(bool force) {
+        if (jobs.size() == pk_sub || (!force && jobs.size() - pk_sub < kPkStep)) return;
+        {
+            std::lock_guard<std::mutex> g(pk_mu);
+            pk_sub = jobs.size();
+            pk_w = wb;
+            pk_b = hb;
+        }
+        pk_cv.notify_all();
+    }
     void flush_jobs() {
         if (jobs.empty()) return;
         const double tf = prof.on ? IngestProf::now() : 0;
@@ -1016,14 +1078,21 @@ struct dcr_ingest {
             bool on;
             ~Acc() { if (on) d += IngestProf::now() - t; }
         } acc{prof.flush, tf, prof.on};
+        kick_jobs(true);
+        {
+            std::unique_lock<std::mutex> lk(pk_mu);
+            pk_cv.wait(lk, [&] { return pk_done == pk_sub; });
+            pk_sub = pk_done = 0;
+        }
+        jobs.clear();
+    }
+    void pack_range(const uint8_t *w, dcr_host_batch *b, const Job *jobv, size_t j0, size_t j1) {
         const size_t chunk = 2048;
-        const size_t nchunks = (jobs.size() + chunk - 1) / chunk;
-        const uint8_t *w = wb;
-        dcr_host_batch *b = hb;
+        const size_t nchunks = (j1 - j0 + chunk - 1) / chunk;
         pool->run(nchunks, [&](size_t c) {
-            const size_t j1 = std::min(jobs.size(), (c + 1) * chunk);
-            for (size_t j = c * chunk; j < j1; ++j) {
-                const Job &jb = jobs[j];
+            const size_t je = std::min(j1, j0 + (c + 1) * chunk);
+            for (size_t j = j0 + c * chunk; j < je; ++j) {
+                const Job &jb = jobv[j];
                 const uint8_t *r = w + jb.rec + 4;
                 const uint32_t l_rn = r[8];
                 const uint32_t n_cig = rd16(r + 12);
@@ -1043,7 +1112,6 @@ struct dcr_ingest {
             }
             return true;
         });
-        jobs.clear();
     }
 
     // parsed records ahead of the walk: rqp[rq_pos, rq_n) (the scanner's
@@ -1123,7 +1191,7 @@ struct dcr_ingest {
         const size_t chunk = 512;
         const double tp = prof.on ? IngestProf::now() : 0;
         if (prof.on) prof.scan += tp - ts;
-        pool->run((n + chunk - 1) / chunk, [&](size_t c) {
+        ppool->run((n + chunk - 1) / chunk, [&](size_t c) {
             const size_t e = std::min(n, (c + 1) * chunk);
             for (size_t i = c * chunk; i < e; ++i) rq[i].perr = (uint8_t)rp.parse_at(wb, rq_off[i], rq[i]);
             return true;
@@ -1344,6 +1412,7 @@ struct dcr_ingest {
         b->ss_col_off[0] = 0;
         b->ds_col_off[0] = 0;
         cap_err = 0;
+        if (jobs.capacity() < (size_t)b->cap_reads) jobs.reserve((size_t)b->cap_reads);
         if (errored || finished) {
             b->end_kind = errored ? DCR_END_ERROR : DCR_END_EOF;
             return fail(DCR_IO_EARG, "the input has already ended");
@@ -1401,6 +1470,7 @@ struct dcr_ingest {
                 const int c = complete_family();
                 if (c <= 0) return c;      // 0: batch full, the read stays unconsumed
                 fam.clear();
+                kick_jobs(false);
             }
             ++passed;
             ++records;
@@ -1574,6 +1644,8 @@ static dcr_ingest *open_impl(const char *path, const dcr_ingest_cfg *cfg, bool r
     // walk) and draw quota throttling (profiles/r02pool: 192-194 -> 217-224 M
     // consensus bases/s with 8 + 8 instead of 16 + 16)
     ing->pool.reset(new Pool(env_threads("DCR_PACK_THREADS", std::max(1, pick_threads(cfg->n_threads) / 2))));
+    ing->ppool.reset(new Pool(std::max(1, std::min(4, pick_threads(cfg->n_threads) / 4))));
+    ing->pk_start_thread();
     ing->rp.min_map_quality = cfg->min_map_quality;
     ing->rp.min_base_quality = cfg->min_base_quality;
     const int64_t end_coff = end_voff >= 0 ? (end_voff >> 16) : -1;

@@ -97,6 +97,12 @@ struct FastArgs {
     int minbq;                      // single-strand: min_base_quality (masked rows in the table); duplex: -1
     int lo_check;                   // some unmasked quality may lie below fast_qlo: check the bytes
     const uint16_t *llr16;          // [123] per-quality LLR term, 1/16 nat, rounded down
+    const double *e1000;            // [1001] k / 1000 correctly rounded (numpy round(x, 3) = rint(1000 x) / 1000)
+    // record scalars (pos, mapq, len, n_cig, n_de, D, M, E lo, E hi, cigar):
+    // the lowest of the ten arrays and each one's byte offset from it, when
+    // every store lies within 4 GiB above it (else sbase = null: 64-bit addresses)
+    uint8_t *sbase;
+    uint32_t sofs[10];
     int want_info;                  // single-strand: write every read's dcr_read_info (DCR_OPT_READ_INFO)
     int direct_r;                   // single-strand records of at most this many reads go to the exact queue unstaged
 };

@@ -38,6 +38,15 @@
 #ifndef DCR_PIPE2
 #define DCR_PIPE2 2   // tiles up to which the products keep two reads in flight
 #endif
+#ifndef DCR_STORE_MODE
+#define DCR_STORE_MODE 1  // fast kernel's column stores: 1 32-bit offsets from scalar bases, 0 64-bit lane addresses
+#endif
+#ifndef DCR_SCAL_MODE
+#define DCR_SCAL_MODE 1   // fast kernel's record scalars: 1 32-bit offsets from one base, 0 64-bit lane addresses
+#endif
+#ifndef DCR_MEAN_MODE
+#define DCR_MEAN_MODE 0   // fast kernel's E: 0 double estimate of the rational, 1 scalar division, 2 + table load
+#endif
 #ifndef DCR_ABL
 #define DCR_ABL 0   // diagnostic builds only (tools/ablate.py); fast kernel: 1 staging only, 2 +products,
                     // 4 always the exact pairwise mean, 5 no per-column stores
@@ -67,6 +76,99 @@ struct WaveLds {
     int stk_off[24], stk_n[24], stk_stage[24];
     double stk_left[24];
 };
+
+// ---- the insertion layout by events (general kernel, records of <= 128 reads
+// with insertion columns).  reconstruct_alignment (:430-547) run as a scan
+// over its events instead of column by column: a column is an insertion column
+// exactly while some read sits at an I op (:476-478).  A read advances one op
+// per normal column once pos >= its start (M/D; only while its sequence lasts,
+// :514), and through its own I runs only at insertion columns; so the I runs
+// of all reads happen in "blocks" of consecutive insertion columns, and the
+// next block starts at the earliest column where some read reaches its next I
+// run.  The wave finds the blocks one event at a time (lane = read), then
+// every column tile is laid out in parallel (lane = column): a normal column
+// t is read r's normal advance a = N(t) - N(s_r) (N: normal columns before),
+// an insertion column of block b at offset o is read r's I run element o when
+// r takes part in b, else '+'.  The overlay lives in the wave's tile scratch.
+constexpr int kEvBlk = 32;               // insertion blocks per record
+constexpr int kEvEnt = 96;               // (read, block) participations per record
+constexpr int kEvReads = 128;            // reads per record (two 64-lane chunks)
+struct EvLds {
+    uint64_t bmask[kEvBlk][2];           // reads taking part in block b
+    // per read: first kept base - the record's staging base; offset of its
+    // runs from the record's run base; kept length | N(s_r) << 16 (the normal
+    // columns before its start column); number of runs
+    uint4 ri[kEvReads];
+    uint16_t bstart[kEvBlk], blen[kEvBlk], beoff[kEvBlk + 1];
+    uint16_t es0[kEvEnt], eL[kEvEnt];    // participation: sequence index of the I run's first base, run length
+};
+
+// The element of read ri in this lane's column of the event layout: -1 and
+// the code in c (pad, '+', '-'), or the sequence index whose base it takes.
+// A normal column is the read's normal advance av = N(t) - N(s_r): its av-th
+// M / D op, after the I runs before it (consumed in their blocks).
+__device__ __forceinline__ int ev_pos(const EvLds &EV, const uint4 ri, const uint32_t *cig0, int r, bool ins_col,
+                                      int bo, int nt, uint64_t mk0, uint64_t mk1, int eo, uint32_t &c, bool &idx_err) {
+    const int len = (int)(ri.z & 0xFFFFu);
+    if (ins_col) {                                       // :478-499
+        const uint64_t mk = r < kWave ? mk0 : mk1;
+        const int rb = r & (kWave - 1);
+        c = kPlus;
+        if (!((mk >> rb) & 1ull)) return -1;
+        const int idx = eo + (r < kWave ? 0 : __popcll(mk0)) + __popcll(mk & ((1ull << rb) - 1ull));
+        if (bo >= (int)EV.eL[idx]) return -1;            // its I run ended inside the block
+        const int is = (int)EV.es0[idx] + bo;
+        if (is >= len) { idx_err = true; c = kPad; return -1; }
+        return is;
+    }
+    c = kPad;
+    const int av = nt - (int)(ri.z >> 16);
+    if (av < 0) return -1;                               // :506-510
+    const int nc = (int)ri.w;
+    const uint32_t *cig = cig0 + ri.y;
+    if (nc == 1 && (cig[0] & 15u) == 0u) return av < len ? av : -1;   // one M run (the usual read)
+    int acc = 0, sq = 0;
+    for (int k = 0; k < nc; ++k) {
+        const uint32_t v = cig[k];
+        const int op = (int)(v & 15u), ln = (int)(v >> 4);
+        if (op == 1) { sq += ln; continue; }             // consumed in its block
+        if (av < acc + ln) {
+            const int is = sq + (op != 2 ? av - acc : 0);
+            if (is >= len) return -1;                    // :540-544
+            if (op == 2) { c = kDel; return -1; }        // :517-524
+            return is;                                   // :528-535
+        }
+        acc += ln;
+        if (op != 2) sq += ln;
+    }
+    if (sq < len) idx_err = true;                        // ops exhausted with bases left (:517)
+    return -1;
+}
+
+// a read's next I run from run index k with md M/D ops and sq bases consumed
+// before it: run index (-1: none reachable), M/D ops before it, length, first
+// base.  A read whose sequence has run out stops at its next M or D op for
+// good (:514, :540); an I run met right at the end of the sequence is reached
+// (its first element raises IndexError, :483).
+struct EvRead { int s, A, k, m, L, s0; };
+__device__ __forceinline__ void ev_next(EvRead &e, const uint32_t *cig, int ncig, int len, int k, int md, int sq) {
+    e.k = -1;
+    for (; k < ncig; ++k) {
+        const uint32_t v = cig[k];
+        const int op = (int)(v & 15u), ln = (int)(v >> 4);
+        if (op == 1) {
+            e.k = k;
+            e.m = md;
+            e.L = ln;
+            e.s0 = sq;
+            return;
+        }
+        if (sq >= len) return;           // stuck at an M / D op
+        if (op != 2 && sq + ln > len) return;   // the sequence runs out inside this M run
+        md += ln;
+        if (op != 2) sq += ln;           // M (and any other op kept as M, :528-535)
+    }
+}
 
 // class of an input base (A/T/C/G/N; anything else is invalid, :580-585)
 __device__ __forceinline__ uint32_t base_class(uint32_t b) {
@@ -1092,15 +1194,11 @@ __device__ bool decide_accumulate_tab(const Args &a, const int64_t rec, const in
 // decided (call b, quality maxQ, unmasked) and fills `co` with the reference's
 // finalize outputs for it (:603-621, :1001-1012); false leaves the tile to the
 // double products.
-template <class Src>
-__device__ __forceinline__ bool decide_tile(const Args &a, int R, bool live, bool ins_col, const Src &src,
-                                            const uint32_t *s_wtab, ColOut &co) {
-    if (a.t16 < 0 || R > 4095) return false;
+struct DecideSums {
     uint32_t S[6] = {0, 0, 0, 0, 0, 0}, N[6] = {0, 0, 0, 0, 0, 0};
     uint32_t nN = 0, Z = 0;
     bool bad = false;
-    for (int r = 0; r < R; ++r) {
-        const uint32_t e = src(r);
+    __device__ __forceinline__ void add(uint32_t e, const uint32_t *s_wtab) {
         const uint32_t cls = e >> 9;
         const uint32_t w = s_wtab[e & 511u];
         bad |= cls == 7 || (cls != 6 && (w >> 31) != 0);
@@ -1113,29 +1211,34 @@ __device__ __forceinline__ bool decide_tile(const Args &a, int R, bool live, boo
         nN += cls == 6;
         Z += (w >> 16) & 0x7FFFu;
     }
+};
+__device__ __forceinline__ bool decide_usable(const Args &a, int R) { return a.t16 >= 0 && R <= 4095; }
+// the decision from the summed rows (see decide_tile)
+__device__ __forceinline__ bool decide_end(const Args &a, int R, bool live, bool ins_col, const DecideSums &D,
+                                           ColOut &co) {
     // the first largest in the reference's order A T C G + -
-    uint32_t Lb = S[0], kb = 0;
+    uint32_t Lb = D.S[0], kb = 0;
 #pragma unroll
     for (int k = 1; k < 6; ++k) {
-        const bool g = S[k] > Lb;
-        Lb = g ? S[k] : Lb;
+        const bool g = D.S[k] > Lb;
+        Lb = g ? D.S[k] : Lb;
         kb = g ? (uint32_t)k : kb;
     }
     uint32_t L2 = 0, nb = 0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-        L2 = max(L2, kb != (uint32_t)k ? S[k] : 0u);
-        nb = kb == (uint32_t)k ? N[k] : nb;
+        L2 = max(L2, kb != (uint32_t)k ? D.S[k] : 0u);
+        nb = kb == (uint32_t)k ? D.N[k] : nb;
     }
-    const int nother = R - (int)nN - (int)nb;           // rows of the other classes (each adds <= 1/16 nat)
-    const bool ok = !bad && (int)(Lb - L2) - nother >= a.t16 && (int)Z - (int)Lb <= 16 * 700;
+    const int nother = R - (int)D.nN - (int)nb;         // rows of the other classes (each adds <= 1/16 nat)
+    const bool ok = !D.bad && (int)(Lb - L2) - nother >= a.t16 && (int)D.Z - (int)Lb <= 16 * 700;
     if (__ballot(live && !ok)) return false;
     // finalize (:613-618, :1001-1012) for an unmasked call kb
-    const bool has_plus = N[4] > 0;
+    const bool has_plus = D.N[4] > 0;
     const bool lower = has_plus && kb < 4;
     co.ch = (int)((0x2D2B47435441ull >> (8 * kb)) & 0xffu) + (lower ? 32 : 0);   // "ATCG+-"
     co.q = a.P->max_base_quality;
-    co.d = R - (int)nN - (int)N[4];
+    co.d = R - (int)D.nN - (int)D.N[4];
     int match;
     if (kb == 4) match = (int)nb;
     else if (kb == 5) match = ins_col ? 0 : (int)nb;
@@ -1143,6 +1246,14 @@ __device__ __forceinline__ bool decide_tile(const Args &a, int R, bool live, boo
     co.e = R - match;
     co.overflow = false;
     return true;
+}
+template <class Src>
+__device__ __forceinline__ bool decide_tile(const Args &a, int R, bool live, bool ins_col, const Src &src,
+                                            const uint32_t *s_wtab, ColOut &co) {
+    if (!decide_usable(a, R)) return false;
+    DecideSums D;
+    for (int r = 0; r < R; ++r) D.add(src(r), s_wtab);
+    return decide_end(a, R, live, ins_col, D, co);
 }
 
 // --------------------------------------------------- per-read register view
@@ -1324,6 +1435,95 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
     lr.cl = (myrd.pos - minpos) | (myrd.len << 16);
     lr.sn = (int)(myrd.seq_start - base_al) | (myrd.ncig << 16);
 
+    // ---- insertion layout by events (EvLds, see there): the blocks of
+    // insertion columns, one event per step (lane = read, two 64-read chunks)
+    static_assert(sizeof(EvLds) <= sizeof(W.tile), "the event layout lives in the tile scratch");
+    EvLds &EV = *reinterpret_cast<EvLds *>(&W.tile[0][0]);
+    int ev_nb = 0;
+    bool ev_ok = !FAST && ins && R <= kEvReads && T < 0xFFFF && DCR_ABL < 9;
+    const uint32_t *ev_cig0 = DUPLEX ? a.ss.cigar + a.in.ss_col_off[2 * rec] : a.ws.norm_cig;
+    if (ev_ok) {
+        EvRead ev[2];
+        bool valid[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int r = c * kWave + lane;
+            valid[c] = r < R;
+            ev[c] = EvRead{0x7fffffff, 0, -1, 0, 0, 0};
+            if (valid[c]) {
+                const ReadRef rd = get_read<DUPLEX>(a, rec, r);
+                ev[c].s = rd.pos - minpos;
+                EV.ri[r] = make_uint4((uint32_t)(rd.seq_start - base_al), (uint32_t)(rd.cig - ev_cig0),
+                                      (uint32_t)rd.len & 0xFFFFu, (uint32_t)rd.ncig);
+                ev_next(ev[c], rd.cig, rd.ncig, rd.len, 0, 0, 0);
+            }
+        }
+        // the next block starts where some read reaches its next I run: at
+        // once when it needs no further normal advance (an I op is current
+        // whatever pos is, :416-427), else after the missing advances, which
+        // only count from its start column on
+        int t = 0, ne = 0;
+        for (;;) {
+            int tr[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+                tr[c] = valid[c] && ev[c].k >= 0
+                            ? (ev[c].m == ev[c].A ? t : max(t, ev[c].s) + (ev[c].m - ev[c].A))
+                            : 0x7fffffff;
+            const int te = wave_min(min(tr[0], tr[1]));
+            if (te >= T) break;
+            if (ev_nb == kEvBlk) { ev_ok = false; break; }
+            bool part[2];
+            int lmax = 0;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                part[c] = tr[c] == te;
+                // normal columns [t, te) advance the reads that have started
+                ev[c].A += max(0, te - max(t, ev[c].s));
+                lmax = max(lmax, part[c] ? ev[c].L : 0);
+            }
+            const int lb = wave_max(lmax);
+            const uint64_t pm0 = __ballot(part[0]), pm1 = __ballot(part[1]);
+            const int np = __popcll(pm0) + __popcll(pm1);
+            if (ne + np > kEvEnt) { ev_ok = false; break; }
+            if (lane == 0) {
+                EV.bstart[ev_nb] = (uint16_t)te;
+                EV.blen[ev_nb] = (uint16_t)min(lb, T - te);
+                EV.beoff[ev_nb] = (uint16_t)ne;
+                EV.bmask[ev_nb][0] = pm0;
+                EV.bmask[ev_nb][1] = pm1;
+            }
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (part[c]) {
+                    const int idx = ne + (c ? __popcll(pm0) : 0) + __popcll((c ? pm1 : pm0) & lanemask_lt(lane));
+                    EV.es0[idx] = (uint16_t)ev[c].s0;
+                    EV.eL[idx] = (uint16_t)ev[c].L;
+                    const ReadRef rd = get_read<DUPLEX>(a, rec, c * kWave + lane);
+                    ev_next(ev[c], rd.cig, rd.ncig, rd.len, ev[c].k + 1, ev[c].m, ev[c].s0 + ev[c].L);
+                }
+            }
+            ne += np;
+            ++ev_nb;
+            t = te + lb;
+        }
+        if (ev_ok) {
+            if (lane == 0) EV.beoff[ev_nb] = (uint16_t)ne;
+            lds_fence();
+            // N(s_r): the normal columns before each read's start column
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (valid[c]) {
+                    int ib = 0;
+                    for (int b = 0; b < ev_nb; ++b)
+                        ib += min(max(ev[c].s - (int)EV.bstart[b], 0), (int)EV.blen[b]);
+                    EV.ri[c * kWave + lane].z |= (uint32_t)(ev[c].s - ib) << 16;
+                }
+            }
+        }
+        lds_fence();
+    }
+
     // R > 64 with insertion columns: precompute the insertion-column flags
     // (all reads must be consulted per column, :476-478) and keep per-read
     // layout state in global scratch between column tiles.
@@ -1333,7 +1533,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
     // within 64-read chunk c): the flags pass walks the runs without touching
     // HBM, and the tiles stage each chunk's next 32 bytes per read
     constexpr int kBigCh = 4;
-    const bool regbig = !FAST && ins && big && !DUPLEX && R <= kBigCh * kWave;
+    const bool regbig = !FAST && ins && big && !DUPLEX && R <= kBigCh * kWave && !ev_ok;
     struct SlimRead {
         int pos, len, ncig;
         const uint32_t *cig;
@@ -1381,7 +1581,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
         }
         wave_fence();
     }
-    if (!FAST && ins && big && !DUPLEX && !regbig) {
+    if (!FAST && ins && big && !DUPLEX && !regbig && !ev_ok) {
         for (int c = 0; c < R; c += kWave) {
             const int r = c + lane;
             if (r < R) {
@@ -1466,7 +1666,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
     };
 
     // ---- phases 1+2: column tiles (lane = column)
-    const int tw = ins ? kTileIns : kWave;       // insertion layout: 32-column tiles
+    const int tw = ins && !ev_ok ? kTileIns : kWave;       // stepped insertion layout: 32-column tiles
     for (int c0 = 0; c0 < T; c0 += tw) {
         const int t = c0 + lane;
         const bool live = lane < tw && t < T;
@@ -1512,6 +1712,87 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
                 return e;
             };
             accumulate(A, R, src, s_lut);
+        } else if (ev_ok) {
+            // the event layout: this lane's column is in insertion block bi at
+            // offset bo, or normal with N(t) normal columns before it
+            int insb = 0, bi = -1, bo = 0;
+            for (int b = 0; b < ev_nb; ++b) {
+                const int bs = EV.bstart[b], bl = EV.blen[b];
+                if (t >= bs + bl) insb += bl;
+                else if (t >= bs) { bi = b; bo = t - bs; }
+            }
+            ins_col = live && bi >= 0;
+            const int nt = t - insb;
+            uint64_t mk0 = 0, mk1 = 0;
+            int eo = 0;
+            if (bi >= 0) {
+                mk0 = EV.bmask[bi][0];
+                mk1 = EV.bmask[bi][1];
+                eo = EV.beoff[bi];
+            }
+            if (fits) {
+                // the bases are staged: a read's element is one more LDS read
+                auto src = [&](int r) -> uint32_t {
+                    uint32_t c;
+                    const uint4 ri = EV.ri[r];
+                    const int is = live ? ev_pos(EV, ri, ev_cig0, r, ins_col, bo, nt, mk0, mk1, eo, c, idx_err) : -1;
+                    return is >= 0 ? (uint32_t)W.stage[ri.x + is] : (live ? c : kPad);
+                };
+                tdec = decide_tile(a, R, live, ins_col, src, s_wtab, tco);
+                if (!tdec) accumulate(A, R, src, s_lut);
+            } else {
+                // 32 reads at a time: their codes in this tile's columns into
+                // the (unused) stage, [read][column], four reads' base and
+                // quality loads in flight together; the decision sums first,
+                // the products only when some column stays undecided
+                const uint8_t *gbb = gb + base_al, *gqb = gq + base_al;
+                uint16_t *cb = W.stage;
+                auto stage_group = [&](int g0, int ng) {
+                    lds_fence();
+                    for (int r0 = 0; r0 < ng; r0 += 4) {
+                        int is[4];
+                        uint32_t c[4], so[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int r = g0 + min(r0 + j, ng - 1);
+                            const uint4 ri = EV.ri[r];
+                            so[j] = ri.x;
+                            is[j] = live ? ev_pos(EV, ri, ev_cig0, r, ins_col, bo, nt, mk0, mk1, eo, c[j], idx_err) : -1;
+                            if (!live) c[j] = kPad;
+                        }
+                        uint32_t bq[4][2];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int o = (int)so[j] + max(is[j], 0);
+                            bq[j][0] = is[j] >= 0 ? gbb[o] : 0u;
+                            bq[j][1] = is[j] >= 0 ? gqb[o] : 0u;
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (r0 + j < ng)
+                                cb[((r0 + j) << 6) + lane] =
+                                    (uint16_t)(is[j] >= 0 ? make_code<DUPLEX>(bq[j][0], bq[j][1], minbq) : c[j]);
+                    }
+                    lds_fence();
+                };
+                auto src_cb = [&](int rr) -> uint32_t { return (uint32_t)cb[(rr << 6) + lane]; };
+                if (decide_usable(a, R)) {
+                    DecideSums D;
+                    for (int g0 = 0; g0 < R; g0 += 32) {
+                        const int ng = min(32, R - g0);
+                        stage_group(g0, ng);
+                        for (int rr = 0; rr < ng; ++rr) D.add(src_cb(rr), s_wtab);
+                    }
+                    tdec = decide_end(a, R, live, ins_col, D, tco);
+                }
+                if (!tdec) {
+                    for (int g0 = 0; g0 < R; g0 += 32) {
+                        const int ng = min(32, R - g0);
+                        stage_group(g0, ng);
+                        accumulate(A, ng, src_cb, s_lut);
+                    }
+                }
+            }
         } else if (!big) {
             uint64_t insmask = 0;
             // bytes that do not fit the stage: each read's next 32 bytes (the
@@ -2365,15 +2646,16 @@ constexpr int kTable = 5 * 0x800;                          // 5 class banks of 2
 constexpr int kStage0 = kTable;                            // 4 KiB per wave
 constexpr int kInvD = kStage0 + kWaves * 0x1000;           // f64 [64] 1 / d
 constexpr int kSent = kInvD + 64 * 8;                      // u16 pad code (out-of-read sentinel)
-constexpr int kPtrs = kSent + 16;                          // u64 [24] pointers (kP* below)
-constexpr int kRm = kPtrs + 24 * 8;                        // per wave: u64 [64] the current record's read words
+constexpr int kPtrs = kSent + 16;                          // u64 [32] pointers (kP* below)
+constexpr int kRm = kPtrs + 32 * 8;                        // per wave: u64 [64] the current record's read words
 constexpr int kMv = kRm + kWaves * kWave * 8;              // per wave: u32 [8] a later record's descriptor
 constexpr int kOv = kMv + kWaves * 32;                     // per wave: u16 [256] column words d | e << 6 | call << 12
 constexpr int kM720 = kOv + kWaves * 512;                  // u32 [64] 720720 / d for depths d <= 16, else 0
 #ifndef DCR_LDS_PAD
 #define DCR_LDS_PAD 0
 #endif
-constexpr int kLdsBytes = kM720 + 64 * 4 + DCR_LDS_PAD;       // PAD: diagnostic builds only
+constexpr int kSofs = kM720 + 64 * 4;                      // u32 [10][2]: record-scalar array offsets from sbase, shifts
+constexpr int kLdsBytes = kSofs + 16 * 8 + DCR_LDS_PAD;       // PAD: diagnostic builds only
 static_assert(kStageElems * 2 == 0x1000, "one 4 KiB stage per wave");
 static_assert(16 * (kRowMax + 5) <= 0x800, "a class bank fits 2 KiB");
 static_assert(5 * kLdsBytes <= 160 * 1024, "five blocks (20 waves) per CU");
@@ -2384,7 +2666,8 @@ __device__ __forceinline__ int stage_base(int wave) { return kStage0 + (wave << 
 // loop (the kernel's arguments no longer spill into VGPR lanes, whose
 // restores are VALU instructions)
 constexpr int kPNormCig = 10, kPCigOff = 11, kPOvf = 12, kPOvfCount = 13, kPXlist = 14, kPXcount = 15;
-constexpr int kPD = 16, kPE = 17, kPSeq = 18, kPQual = 19, kPStatus = 20, kPInfo = 21, kPParams = 22;
+constexpr int kPD = 16, kPE = 17, kPSeq = 18, kPQual = 19, kPStatus = 20, kPInfo = 21, kPParams = 22, kPSbase = 23;
+constexpr int kPE1000 = 24, kNPtrs = 25;
 }  // namespace fk
 
 constexpr int kStageDw = kStageElems / 4 / kWave;   // staged dwords per lane
@@ -2578,8 +2861,10 @@ __device__ __forceinline__ uint64_t scalar_dest(const dcr_out &O, int k) {
 // wait of the record loop also waited for them)
 #if defined(__HIP_DEVICE_COMPILE__)
 #define DCR_G __attribute__((address_space(1)))
+#define DCR_C __attribute__((address_space(4)))   // constant: uniform loads become scalar loads
 #else
 #define DCR_G                  // the host pass only parses device functions
+#define DCR_C
 #endif
 template <class Tp>
 __device__ __forceinline__ DCR_G Tp *lds_vptr(const uint8_t *lds, int slot) {
@@ -2830,6 +3115,9 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     DCR_G uint16_t *pd = nullptr, *pe = nullptr;
     DCR_G uint8_t *ps = nullptr, *pq = nullptr;
     if (!EXACT) {
+        // per-record bases in scalar registers (from the LDS pointer cache +
+        // the record's column offset); lanes store at 32-bit byte offsets
+        // from them (global_store ... v_off, s_base): no per-lane 64-bit address
         pd = lds_sgptr<uint16_t>(lds, fk::kPD) + off;
         pe = lds_sgptr<uint16_t>(lds, fk::kPE) + off;
         ps = lds_sgptr<uint8_t>(lds, fk::kPSeq) + off;
@@ -2866,10 +3154,18 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         und |= (uint32_t)(live && undecided) << tt;
         if (EXACT || R > 16) *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (kb << 12));
         if (!EXACT && DCR_ABL != 5 && t < T16) {
-            pd[t] = (uint16_t)d;
-            pe[t] = (uint16_t)e;
-            ps[t] = (uint8_t)(t < T ? __builtin_amdgcn_perm(0u, 0x47435441u, kb) : 0x4Eu);   // "ATCG"[call]
-            pq[t] = (uint8_t)(t < T ? (uint32_t)a.maxq : 0u);
+            if (DCR_STORE_MODE) {
+                const uint32_t ut = (uint32_t)t, ut2 = 2u * ut;
+                *(DCR_G uint16_t *)((DCR_G uint8_t *)pd + ut2) = (uint16_t)d;
+                *(DCR_G uint16_t *)((DCR_G uint8_t *)pe + ut2) = (uint16_t)e;
+                ps[ut] = (uint8_t)(t < T ? __builtin_amdgcn_perm(0u, 0x47435441u, kb) : 0x4Eu);   // "ATCG"[call]
+                pq[ut] = (uint8_t)(t < T ? (uint32_t)a.maxq : 0u);
+            } else {
+                pd[t] = (uint16_t)d;
+                pe[t] = (uint16_t)e;
+                ps[t] = (uint8_t)(t < T ? __builtin_amdgcn_perm(0u, 0x47435441u, kb) : 0x4Eu);
+                pq[t] = (uint8_t)(t < T ? (uint32_t)a.maxq : 0u);
+            }
         }
         fx += live ? __umul24((uint32_t)e, m720[d]) : 0u;
         dmax = max(dmax, live ? d : -1);
@@ -3029,18 +3325,52 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     // reference's own double rounding (< 1e-9 here), so rint agrees with
     // numpy's; a tie, or any other record, takes the double sum below.
     double E = 0.0;
+    uint32_t E_lo = 0, E_hi = 0;         // E's words, scalar registers
     bool slow = exact || R > 16 || DCR_ABL == 4;
     if (!slow) {
         const uint32_t S = (uint32_t)wave_sum((int)fx);
-        const int64_t num = 25 * (int64_t)S;
-        const int den = 18018 * T;
-        const double dn = (double)den;
-        double rc = __builtin_amdgcn_rcp(dn);
-        rc = __builtin_fma(__builtin_fma(-dn, rc, 1.0), rc, rc);
-        const int k = __builtin_amdgcn_readfirstlane((int)__builtin_rint((double)num * rc));
-        const int64_t r = num - (int64_t)k * den;
-        slow = 2 * (r < 0 ? -r : r) >= den || k > 1000;                   // a tie (or a bad estimate)
-        E = div1000(k);
+        if (DCR_MEAN_MODE == 0) {
+            // the rational 25 S / (18018 T) in doubles: k = rint, remainder exact
+            const int64_t num = 25 * (int64_t)S;
+            const int den = 18018 * T;
+            const double dn = (double)den;
+            double rc = __builtin_amdgcn_rcp(dn);
+            rc = __builtin_fma(__builtin_fma(-dn, rc, 1.0), rc, rc);
+            const int k = __builtin_amdgcn_readfirstlane((int)__builtin_rint((double)num * rc));
+            const int64_t r = num - (int64_t)k * den;
+            slow = 2 * (r < 0 ? -r : r) >= den || k > 1000;                   // a tie (or a bad estimate)
+            const double Ed = div1000(k);
+            E_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)__double_as_longlong(Ed));
+            E_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)__double_as_longlong(Ed) >> 32));
+        } else {
+            // k = round(25 S / (18018 T)) by restoring division in scalar
+            // registers (S and T are wave-uniform; 25 S < 2^32 for T <= 238,
+            // and the quotient is at most 1000 < 2^10); a tie (2 r = den) or
+            // T > 238 takes the double path
+            const uint32_t num = 25u * S, den = 18018u * (uint32_t)T;
+            uint32_t q = 0, r = num;
+#pragma unroll
+            for (int b = 9; b >= 0; --b) {
+                const uint32_t dv = den << b;
+                if (r >= dv) {
+                    r -= dv;
+                    q |= 1u << b;
+                }
+            }
+            const uint32_t k = q + (2u * r > den ? 1u : 0u);
+            slow = 2u * r == den || k > 1000u || T > 238;
+            if (DCR_MEAN_MODE == 2) {
+                // E = k / 1000 correctly rounded from the host's table (a scalar load)
+                const DCR_C uint2 *tab = (const DCR_C uint2 *)lds_ptr<const uint2>(lds, fk::kPE1000);
+                const uint2 Ew = tab[min(k, 1000u)];
+                E_lo = Ew.x;
+                E_hi = Ew.y;
+            } else {
+                const double Ed = div1000((int)min(k, 1000u));
+                E_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)__double_as_longlong(Ed));
+                E_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)__double_as_longlong(Ed) >> 32));
+            }
+        }
         // the common kernel kept no column words for the double walk: the
         // EXACT kernel takes the record (a tie is rare)
         if (!EXACT && slow) return false;
@@ -3086,6 +3416,8 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         const double total = 0.0 + pairwise_et(et, T, ln);
         E = __builtin_rint((total / (double)T) * 1000.0) / 1000.0;
     }
+    E_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)__double_as_longlong(E));
+    E_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)__double_as_longlong(E) >> 32));
     }
     sp.mark(9);                          // [8] mean
     // the record's scalar fields straight into the dcr_out arrays: lane k
@@ -3094,8 +3426,6 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     // waves of one XCD take consecutive records (k_consensus_fast), so the
     // lines these 4-byte stores share fill up in one L2
     {
-        const uint32_t E_lo = (uint32_t)__double_as_longlong(E);
-        const uint32_t E_hi = (uint32_t)((uint64_t)__double_as_longlong(E) >> 32);
         const int mapq = (int)((uint32_t)m.d0 >> 16);                        // k_recmeta
         uint32_t v = 0;
         v = write_lane<0>(v, __builtin_amdgcn_readfirstlane((uint32_t)(minpos + first)));
@@ -3105,10 +3435,17 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         v = write_lane<4>(v, __builtin_amdgcn_readfirstlane((uint32_t)T));
         v = write_lane<5>(v, __builtin_amdgcn_readfirstlane((uint32_t)Dmax));
         v = write_lane<6>(v, __builtin_amdgcn_readfirstlane((uint32_t)Dmin));
-        v = write_lane<7>(v, __builtin_amdgcn_readfirstlane(E_lo));
-        v = write_lane<8>(v, __builtin_amdgcn_readfirstlane(E_hi));
+        v = write_lane<7>(v, E_lo);
+        v = write_lane<8>(v, E_hi);
         v = write_lane<9>(v, __builtin_amdgcn_readfirstlane((uint32_t)klen << 4));
-        if (lane < 10) {
+        DCR_G uint8_t *sb = DCR_SCAL_MODE ? lds_sgptr<uint8_t>(lds, fk::kPSbase) : nullptr;
+        if (sb && lane < 10) {
+            // the ten arrays lie within 4 GiB above sbase (checked by the
+            // host): lane k stores at a 32-bit offset from that one base
+            const uint2 w = *(const uint2 *)(lds + fk::kSofs + 8 * lane);   // offset of array k, its shift
+            const uint32_t idx = lane == 9 ? (uint32_t)off : (uint32_t)rec;
+            *(DCR_G uint32_t *)(sb + (w.x + (idx << w.y))) = v;
+        } else if (lane < 10) {
             // destination word of field k (scalar_dest), from the LDS cache
             const uint64_t pw = *(const uint64_t *)(lds + fk::kPtrs + 8 * lane);
             const uint64_t idx = lane == 9 ? (uint64_t)off : (uint64_t)rec;
@@ -3204,7 +3541,11 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
         const int t = threadIdx.x;
         ((uint32_t *)(lds + fk::kM720))[t] = t == 0 || t > 16 ? 0u : 720720u / (uint32_t)t;
     }
-    if (threadIdx.x < 24) {
+    if (threadIdx.x < 10) {
+        const int k = threadIdx.x;
+        *(uint2 *)(lds + fk::kSofs + 8 * k) = make_uint2(a.sofs[k], (k == 7 || k == 8) ? 3u : 2u);
+    }
+    if (threadIdx.x < fk::kNPtrs) {
         const int k = threadIdx.x;
         uint64_t v;
         switch (k) {
@@ -3221,7 +3562,8 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
         case fk::kPStatus: v = (uint64_t)(uintptr_t)a.O.status; break;
         case fk::kPInfo: v = (uint64_t)(uintptr_t)a.info; break;
         case fk::kPParams: v = (uint64_t)(uintptr_t)a.P; break;
-        case 23: v = 0; break;
+        case fk::kPSbase: v = (uint64_t)(uintptr_t)a.sbase; break;
+        case fk::kPE1000: v = (uint64_t)(uintptr_t)a.e1000; break;
         default: v = scalar_dest(a.O, k); break;
         }
         *(uint64_t *)(lds + fk::kPtrs + 8 * k) = v;
