@@ -602,8 +602,11 @@ def _print_summary(c):
 #     family's first read arrives;
 #   * random.sample draws: the (population, size) of every call depends only
 #     on the data, so each rank's exact starting state is the state after
-#     the calls of the ranks before it; ranks that ran from another state run
-#     again (none when nothing is downsampled);
+#     the calls of the ranks before it.  A rank's ingest asks for that state
+#     at its first random.sample call and waits for the earlier ranks' calls
+#     (their own passes, or host-only count passes started on demand:
+#     _StateExchange); no rank runs twice, and an input that is never
+#     downsampled neither counts nor waits;
 #   * the first failing rank ends the output exactly as the reference stops:
 #     its parts are already cut where the reference stops writing, later
 #     ranks are dropped and its exception is raised.
@@ -674,9 +677,10 @@ def _launch_ranks(argv, n):
     return subprocess.call(cmd, env=env)
 
 
-def _run_range(args, params, backend, path, rng, rng_state, rng_range, parts, device):
+def _run_range(args, params, backend, path, rng, rng_state, rng_range, parts, device, gate=None):
     """The ordinary pipeline over one range of families into part files;
-    stdout, outcome, counters and random.sample calls in a dict."""
+    stdout, outcome, counters and random.sample calls in a dict.  ``gate``
+    (optional): the ingest's state gate (native_io.Ingest.set_state_gate)."""
     res = {"status": "ok", "exc_args": (), "calls": [], "counters": None, "stdout": "", "stats": {},
            "sizes": [0, 0, 0]}
     out = io.StringIO()
@@ -687,6 +691,8 @@ def _run_range(args, params, backend, path, rng, rng_state, rng_range, parts, de
     be = _as_backend(backend, params, device)
     cons, excl, unproc = _open_writers(parts, b"", args, ing)
     ing.set_rng_state(rng_state)
+    if gate is not None:
+        ing.set_state_gate(gate)
     drv = _Driver(args, params, be, ing, cons, excl, unproc)
     drv.ends_at_eof = rng_range[1] == -1
     try:
@@ -709,6 +715,108 @@ def _run_range(args, params, backend, path, rng, rng_state, rng_range, parts, de
             ing.close()
         res["sizes"] = [os.path.getsize(p) for p in parts]
     return res
+
+
+def _count_calls(path, params, rng_range, threads, stop):
+    """The (population, size) of every random.sample call of one range, by a
+    host-only ingest (host inflate, no device work, batches discarded): the
+    calls depend only on the data (family and subfamily sizes), not on the
+    generator's state.  Stops early (partial list, unused) when ``stop`` is
+    set; an input error ends the list where the ingest stops."""
+    ing = native_io.Ingest(path, params.min_map_quality, params.min_reads, params.max_reads,
+                           params.min_base_quality, threads, rng_range[0], rng_range[1], host_inflate=True)
+    try:
+        hb = native_io.HostBatch(reads=1 << 18)
+        while not stop.is_set():
+            ing.next(hb)
+            if hb.end_kind != native_io.END_FULL:
+                break
+    except Exception:  # noqa: BLE001 - the calls up to the stop are the range's calls
+        pass
+    finally:
+        calls = ing.sample_calls()
+        ing.close()
+    return calls
+
+
+class _StateExchange:
+    """Rerun-free random.sample states for the sharded CLI.
+
+    Rank r's exact starting state is the state after every call of the ranks
+    before it.  Each rank's ingest is gated (``gate``): a rank that reaches
+    its first random.sample call asks for that state, and waits only then; a
+    rank that never samples never waits (its output does not depend on the
+    state).  The calls of rank q are published in the process group's store
+    by whichever finishes first: rank q's own pass, or a host-only count
+    pass over rank q's range (``_count_calls``) that rank q starts in a
+    thread once any rank has asked.  Nothing is counted, and nothing waits,
+    for an input that is never downsampled."""
+
+    _seq = 0
+
+    def __init__(self, dist, rank, world, s0, path, params, rng_range, threads):
+        from datetime import timedelta
+        _StateExchange._seq += 1       # every rank opens its exchanges in the same order
+        self.store = dist.distributed_c10d._get_default_store()
+        self.pre = "dcr_shard/%d/" % _StateExchange._seq
+        self.rank, self.world, self.s0 = rank, world, s0
+        self.wait_timeout = timedelta(hours=6)
+        self.lock = threading.Lock()
+        self.published = False
+        self.gated_state = None
+        self.wait_s = 0.0
+        self.counted = False
+        self.stop = threading.Event()
+        self.th = None
+        if rng_range is not None and rank < world - 1:
+            # only later ranks read this rank's calls
+            self.th = threading.Thread(target=self._counter, args=(path, params, rng_range, threads),
+                                       name="dcr-count", daemon=True)
+            self.th.start()
+
+    def publish(self, calls):
+        with self.lock:
+            if self.published:
+                return
+            self.published = True
+        flat = np.asarray(calls, np.int32).reshape(-1)
+        self.store.set(self.pre + "calls%d" % self.rank, flat.tobytes())
+
+    def _counter(self, path, params, rng_range, threads):
+        from datetime import timedelta
+        while not self.stop.is_set():
+            try:
+                self.store.wait([self.pre + "need"], timedelta(milliseconds=200))
+                break
+            except Exception:  # noqa: BLE001 - the store's timeout
+                continue
+        if self.stop.is_set() or self.published:
+            return
+        self.counted = True
+        calls = _count_calls(path, params, rng_range, threads, self.stop)
+        if not self.stop.is_set():
+            self.publish(calls)
+
+    def gate(self):
+        """The ingest's state gate: the state after ranks 0..rank-1's calls."""
+        t0 = time.perf_counter()
+        self.store.set(self.pre + "need", b"1")
+        keys = [self.pre + "calls%d" % q for q in range(self.rank)]
+        if keys:
+            self.store.wait(keys, self.wait_timeout)
+        state = self.s0
+        for k in keys:
+            flat = np.frombuffer(self.store.get(k), np.int32)
+            state = native_io.py_replay(state, [(int(flat[2 * i]), int(flat[2 * i + 1]))
+                                                for i in range(len(flat) // 2)])
+        self.gated_state = state
+        self.wait_s += time.perf_counter() - t0
+        return state
+
+    def close(self):
+        self.stop.set()
+        if self.th is not None:
+            self.th.join()
 
 
 def _copy_range(src, dst_fd, n, dst_off):
@@ -809,9 +917,17 @@ def _main_sharded(args, params, backend, rng, stats, group):
     empty = {"status": "ok", "exc_args": (), "calls": [], "counters": None, "stdout": "", "stats": {},
              "sizes": [0, 0, 0]}
     result, used, rounds = empty, None, 0
-    if mine is not None:
-        result = _run_range(args, params, backend, path, rng, s0, mine, parts, device)
-        used, rounds = s0, 1
+    xch = _StateExchange(dist, rank, world, s0, path, params, mine, args.threads)
+    try:
+        if mine is not None:
+            result = _run_range(args, params, backend, path, rng, s0, mine, parts, device,
+                                gate=xch.gate if rank > 0 else None)
+            used, rounds = (xch.gated_state or s0), 1
+        # this rank's calls for the later ranks (if no count pass published them first)
+        xch.publish(result["calls"])
+    finally:
+        xch.close()
+    # a safety net only: with the gate, a rank sampled from its exact state
     while True:
         results = [None] * world
         dist.all_gather_object(results, result)
@@ -823,7 +939,8 @@ def _main_sharded(args, params, backend, rng, stats, group):
             state = native_io.py_replay(state, results[r]["calls"])
         else:
             target = state
-        again = bool(mine is not None and target is not None and target != used)
+        # a rank that never sampled does not depend on the state
+        again = bool(mine is not None and target is not None and result["calls"] and target != used)
         flags = [None] * world
         dist.all_gather_object(flags, again)
         if not any(flags):
@@ -835,6 +952,8 @@ def _main_sharded(args, params, backend, rng, stats, group):
     if stats is not None:
         stats.update(result["stats"])
         stats["shard_rounds"] = rounds
+        stats["state_wait_s"] = xch.wait_s
+        stats["count_pass"] = xch.counted
     # the first failing rank ends the output as the reference stops; later
     # ranks are dropped (every rank derives the same cut from the results)
     fail = next((r for r in range(world) if results[r]["status"] != "ok"), None)

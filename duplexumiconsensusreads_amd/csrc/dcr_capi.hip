@@ -548,6 +548,16 @@ int dcr_debug_stamps(dcr_ctx *c, unsigned long long *out, int n, int reset) {
     return DCR_OK;
 }
 
+// diagnostic (not in include/dcr.h): the last batch's queue counters -- err,
+// ovf_count[2], fast_count[2], xcount[2] (exact queue), gen_next[2], deep_count
+int dcr_debug_counts(dcr_ctx *c, int *out10) {
+    if (!c || !out10) return fail(DCR_EARG, "NULL argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(out10, c->w.err, sizeof(int) * 10, hipMemcpyDeviceToHost));
+    return DCR_OK;
+}
+
 int dcr_last_kernel_timing(dcr_ctx *c, float *ms) {
     if (!c || !ms) return fail(DCR_EARG, "NULL argument");
     if (!c->timed) return fail(DCR_EARG, "no batch has run");

@@ -427,7 +427,7 @@ class Inflater {
     // bytes into its data, on a record boundary (no header); end_coff >= 0:
     // stop end_uoff bytes into the data of the block at end_coff
     Inflater(FILE *f, int n_threads, const RecParser &rp, bool ranged = false, uint64_t start_coff = 0,
-             uint32_t start_uoff = 0, int64_t end_coff = -1, uint32_t end_uoff = 0)
+             uint32_t start_uoff = 0, int64_t end_coff = -1, uint32_t end_uoff = 0, bool host_only = false)
         : f_(f), pool_(env_threads("DCR_INFLATE_THREADS", n_threads)),
           spool_(env_threads("DCR_SCAN_THREADS", std::max(1, n_threads / 2))), rp_(rp), end_coff_(end_coff),
           end_uoff_(end_uoff) {
@@ -462,7 +462,7 @@ class Inflater {
         {
             std::lock_guard<std::mutex> g(g_hook_mu);
             const char *e = std::getenv("DCR_GPU_INFLATE");
-            if (g_hook_set && !(e && std::strcmp(e, "0") == 0)) {
+            if (g_hook_set && !host_only && !(e && std::strcmp(e, "0") == 0)) {
                 hook_ = g_hook;
                 gpu_ = true;
             }
@@ -942,6 +942,11 @@ struct dcr_ingest {
     std::string umi2_;                   // check_family_UMIs scratch
     bool mid_end = false;     // the range stops before the end of the file
     std::vector<int32_t> sample_calls;   // (n, k) of every random.sample call
+    // state gate (dcr_ingest_set_state_gate): called once, before the first
+    // random.sample call, for the exact generator state to sample from
+    dcr_state_gate_fn gate_fn = nullptr;
+    void *gate_user = nullptr;
+    bool gate_open = false;
     bool started = false;     // any passing read seen
     bool finished = false;    // EOF processed
     bool errored = false;
@@ -1303,6 +1308,14 @@ struct dcr_ingest {
             if (n < cfg.min_reads) { enough = false; break; }
             if (n > cfg.max_reads) {
                 if (cfg.max_reads < 0) return stop(DCR_ERR_VALUE, "Sample larger than population or is negative");
+                if (gate_fn && !gate_open) {
+                    gate_open = true;
+                    if (gate_fn(gate_user, rng.mt, &rng.index) != 0 || rng.index < 0 || rng.index > 624)
+                    {
+                        g_err = "the state gate gave no generator state";
+                        return -1;
+                    }
+                }
                 rng.sample(n, cfg.max_reads, idx_tmp);
                 sample_calls.push_back(n);
                 sample_calls.push_back(cfg.max_reads);
@@ -1652,7 +1665,8 @@ static dcr_ingest *open_impl(const char *path, const dcr_ingest_cfg *cfg, bool r
     const uint32_t end_uoff = end_voff >= 0 ? (uint32_t)(end_voff & 0xffff) : 0;
     ing->mid_end = end_voff >= 0;
     ing->infl.reset(new Inflater(f, pick_threads(cfg->n_threads), ing->rp, ranged, (uint64_t)start_voff >> 16,
-                                 (uint32_t)(start_voff & 0xffff), end_coff, end_uoff));
+                                 (uint32_t)(start_voff & 0xffff), end_coff, end_uoff,
+                                 (cfg->flags & DCR_INGEST_HOST_INFLATE) != 0));
     // seed like an unseeded random.Random is not reproducible; callers pass
     // their state with dcr_ingest_set_rng.  Default: random.seed(0).
     for (int i = 0; i < 624; ++i) ing->rng.mt[i] = 0;
@@ -1830,6 +1844,14 @@ int dcr_ingest_get_rng(dcr_ingest *ing, uint32_t *mt, int32_t *index) {
     if (!ing || !mt || !index) return fail(DCR_IO_EARG, "NULL argument");
     std::memcpy(mt, ing->rng.mt, sizeof ing->rng.mt);
     *index = ing->rng.index;
+    return DCR_IO_OK;
+}
+
+int dcr_ingest_set_state_gate(dcr_ingest *ing, dcr_state_gate_fn fn, void *user) {
+    if (!ing) return fail(DCR_IO_EARG, "NULL argument");
+    ing->gate_fn = fn;
+    ing->gate_user = user;
+    ing->gate_open = false;
     return DCR_IO_OK;
 }
 

@@ -21,6 +21,7 @@ LIB_PATH = os.path.join(HERE, "libdcr_io.so")
 _i32, _i64, _vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p
 
 END_FULL, END_EOF, END_ERROR = 0, 1, 2
+INGEST_HOST_INFLATE = 1                  # dcr_ingest_cfg.flags
 ERR_NAMES = {1: "exit", 2: "TypeError", 3: "IndexError", 4: "ValueError", 5: "AttributeError"}
 FAM_PROCESSED, FAM_FILTERED = 0, 1
 FAIL_NAMES = {1: "IndexError", 2: "TypeError", 3: "ValueError", 4: "OverflowError", 5: "exit",
@@ -29,7 +30,7 @@ FAIL_NAMES = {1: "IndexError", 2: "TypeError", 3: "ValueError", 4: "OverflowErro
 
 class IngestCfg(ctypes.Structure):
     _fields_ = [("min_map_quality", _i32), ("min_reads", _i32), ("max_reads", _i32),
-                ("min_base_quality", _i32), ("n_threads", _i32), ("reserved", _i32)]
+                ("min_base_quality", _i32), ("n_threads", _i32), ("flags", _i32)]
 
 
 # (name, dtype, length expression) of the caller-owned arrays, in struct order
@@ -108,6 +109,7 @@ def load():
             "dcr_bam_header": (_i64, [ctypes.c_char_p, _vp, _i64]),
             "dcr_io_set_inflate_hook": (_i32, [_vp]),
             "dcr_ingest_gpu_inflate": (_i32, [_vp]),
+            "dcr_ingest_set_state_gate": (_i32, [_vp, _vp, _vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -232,15 +234,21 @@ def set_inflate_hook(hook):
     _HOOK = hook
 
 
+_GATE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
+                            ctypes.POINTER(ctypes.c_int32))
+
+
 class Ingest:
     """dcr_ingest: a BAM opened for batched reading."""
 
     def __init__(self, path, min_map_quality=20, min_reads=1, max_reads=100, min_base_quality=20, n_threads=0,
-                 start_voff=0, end_voff=-1):
+                 start_voff=0, end_voff=-1, host_inflate=False):
         """``start_voff`` / ``end_voff``: a range of whole families
-        (split_points); the header is then empty."""
+        (split_points); the header is then empty.  ``host_inflate``: the host
+        inflate pool even when a GPU inflate hook is set."""
         lib = load()
-        cfg = IngestCfg(min_map_quality, min_reads, max_reads, min_base_quality, n_threads, 0)
+        cfg = IngestCfg(min_map_quality, min_reads, max_reads, min_base_quality, n_threads,
+                        INGEST_HOST_INFLATE if host_inflate else 0)
         if start_voff == 0 and end_voff == -1:
             self._h = lib.dcr_ingest_open(os.fsencode(path), ctypes.byref(cfg))
         else:
@@ -269,6 +277,32 @@ class Ingest:
         words = np.asarray(state[1][:624], np.uint32)
         if load().dcr_ingest_set_rng(self._h, words.ctypes.data, int(state[1][624])) != 0:
             raise _err("set_rng")
+
+    def set_state_gate(self, fn):
+        """``fn()`` -> a ``random.getstate()`` tuple, called once on the thread
+        running next(), right before this ingest's first random.sample call
+        (never when it does not sample); None removes the gate.  An exception
+        in ``fn`` ends the ingest with an error."""
+        lib = load()
+        if fn is None:
+            self._gate = None
+            lib.dcr_ingest_set_state_gate(self._h, None, None)
+            return
+
+        def gate(_user, mt, index):
+            try:
+                st = fn()
+                words = np.asarray(st[1][:624], np.uint32)
+                ctypes.memmove(mt, words.ctypes.data, 624 * 4)
+                index[0] = int(st[1][624])
+                return 0
+            except BaseException as e:   # noqa: BLE001 - reported through the ingest's error
+                self.gate_error = e
+                return 1
+        self.gate_error = None
+        self._gate = _GATE_FN(gate)      # kept alive with the ingest
+        if lib.dcr_ingest_set_state_gate(self._h, ctypes.cast(self._gate, _vp), None) != 0:
+            raise _err("set_state_gate")
 
     def rng_state(self, template):
         words = np.zeros(624, np.uint32)

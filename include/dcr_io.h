@@ -71,8 +71,13 @@ typedef struct dcr_ingest_cfg {
     int32_t max_reads;         /* --max_reads                                    */
     int32_t min_base_quality;  /* --min_base_quality (=/X count after the trim)  */
     int32_t n_threads;         /* inflate / pack threads (0: up to 16)           */
-    int32_t reserved;
+    int32_t flags;             /* DCR_INGEST_* below (0: defaults)               */
 } dcr_ingest_cfg;
+
+/* dcr_ingest_cfg.flags: inflate on the host pool even when a GPU inflate
+ * hook is set (dcr_io_set_inflate_hook), e.g. a count-only pass running
+ * beside a GPU pass */
+#define DCR_INGEST_HOST_INFLATE 1
 
 /* One host batch.  The caller allocates every array (pinned memory for the
  * GPU path) and sets the capacities; dcr_ingest_next fills it.  The first
@@ -177,6 +182,14 @@ dcr_ingest *dcr_ingest_open_range(const char *path, const dcr_ingest_cfg *cfg, i
  * order (check_number_reads :157-188): returns the count, copies up to cap
  * pairs into out */
 int64_t dcr_ingest_sample_calls(dcr_ingest *ing, int32_t *out, int64_t cap);
+/* State gate of a range that starts after other ranges (the sharded CLI):
+ * called once, on the thread running dcr_ingest_next, right before the
+ * range's first random.sample call, it writes the exact generator state to
+ * sample from (the state after every earlier range's calls) and returns 0;
+ * a range that never samples never calls it.  Nonzero ends the ingest with
+ * an error.  NULL removes the gate. */
+typedef int (*dcr_state_gate_fn)(void *user, uint32_t *mt624, int32_t *index);
+int dcr_ingest_set_state_gate(dcr_ingest *ing, dcr_state_gate_fn fn, void *user);
 /* random.sample(range(n_i), k_i) for each pair: the state after those calls */
 int dcr_py_replay(uint32_t *mt624, int32_t *index, const int32_t *calls, int64_t n_calls);
 /* the BAM header as stored (magic .. references) without opening an ingest:

@@ -6,9 +6,11 @@ infrastructure; the ranks' GPU path is the same code with the HIP backend).
 Identical means: the three output BAMs record for record, stdout, the
 exception, and the caller's random state afterwards.  Cases: excluded reads
 and filtered families; downsampling in every range (the ranks' random
-states come from the calls of the ranks before them, so later ranks run a
-second time); the reference stopping at a read inside the first or the
-second range."""
+states come from the calls of the ranks before them: each later
+rank's ingest waits at its first random.sample call for the state after the
+earlier ranks' calls, which those ranks publish from their own pass or from a
+host-only count pass; no rank runs twice); the reference stopping at a read
+inside the first or the second range, with and without downsampling."""
 import contextlib
 import io
 import multiprocessing as mp
@@ -50,7 +52,7 @@ def _rank_main(rank, world, port, argv, seed, q):
     try:
         stats = {}
         out, exc, state = _outcome(argv, seed, stats)
-        q.put((rank, out, exc, state, stats.get("shard_rounds")))
+        q.put((rank, out, exc, state, (stats.get("shard_rounds"), stats.get("count_pass"))))
     finally:
         dist.destroy_process_group()
 
@@ -98,7 +100,8 @@ def compare(tmp_path, in_bam, extra, seed, world, expect_exc=None, expect_rounds
     for r in range(1, world):
         assert got[r][0] == "" and got[r][1] is None        # ranks > 0 print nothing
     if expect_rounds is not None:
-        assert max(g[3] or 0 for g in got.values()) == expect_rounds
+        assert max(g[3][0] or 0 for g in got.values()) == expect_rounds
+    return got
     # nothing left behind but the three outputs
     left = sorted(p.name for p in tmp_path.iterdir() if ".part" in p.name)
     assert left == []
@@ -156,14 +159,23 @@ def test_sharded_filters_and_summary(tmp_path, filters_bam, world):
     compare(tmp_path, filters_bam, ["--min_reads", "3", "-v"], 5, world, expect_rounds=1)
 
 
-def test_sharded_downsampling_random_states(tmp_path, filters_bam):
-    # subfamilies above --max_reads 3 are sampled in every range: rank 1 runs
-    # again from the state after rank 0's calls
-    compare(tmp_path, filters_bam, ["--max_reads", "3"], 7, 2, expect_rounds=2)
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_downsampling_random_states(tmp_path, filters_bam, world):
+    # subfamilies above --max_reads 3 are sampled in every range: ranks > 0
+    # wait at their first sample call for the exact state, and none runs twice
+    got = compare(tmp_path, filters_bam, ["--max_reads", "3"], 7, world, expect_rounds=1)
+    # the last rank's calls are read by nobody: it never counts
+    assert got[world - 1][3][1] is False
 
 
-@pytest.mark.parametrize("where", [0.2, 0.8])
-def test_sharded_reference_stop(tmp_path, filters_bam, where):
+def test_sharded_no_downsampling_counts_nothing(tmp_path, filters_bam):
+    # nothing above --max_reads: no rank asks for a state, no count pass runs
+    got = compare(tmp_path, filters_bam, ["--max_reads", "1000"], 7, 3, expect_rounds=1)
+    assert all(g[3][1] is False for g in got.values())
+
+
+@pytest.mark.parametrize("where,extra", [(0.2, []), (0.8, []), (0.2, ["--max_reads", "3"]), (0.8, ["--max_reads", "3"])])
+def test_sharded_reference_stop(tmp_path, filters_bam, where, extra):
     # a read without RX: pass_filters prints and exits (:1135-1181) there
     recs = list(bam.AlignmentFile(filters_bam, "rb"))
     k = int(len(recs) * where)
@@ -176,4 +188,4 @@ def test_sharded_reference_stop(tmp_path, filters_bam, where):
     with bam.AlignmentFile(path, "wb", header=hdr) as out:
         for r in recs:
             out.write(r)
-    compare(tmp_path, path, ["--min_reads", "3"], 3, 2, expect_exc="SystemExit(1)")
+    compare(tmp_path, path, ["--min_reads", "3", *extra], 3, 2, expect_exc="SystemExit(1)")

@@ -42,6 +42,13 @@ for rnd in range(6):
         lib.dcr_last_kernel_timing(ctx, ms)
         if rnd:
             res[path].append(list(ms))
+for path, lib, ctx in handles:
+    if hasattr(lib, "dcr_debug_counts"):
+        c = (ctypes.c_int * 10)()
+        lib.dcr_debug_counts(ctypes.c_void_p(ctx), c)
+        print(f"{os.path.basename(path):24s} counts: fast ss/ds {c[3]}/{c[4]} exact ss/ds {c[5]}/{c[6]} "
+              f"ovf {c[1]}/{c[2]} deep {c[9]}")
+        break
 for path in libs:
     v = res[path]
     med = [sorted(x[k] for x in v)[len(v) // 2] for k in range(9)]
