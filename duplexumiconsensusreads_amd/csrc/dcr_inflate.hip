@@ -66,13 +66,25 @@ struct IStamp {
     }
 };
 
+#ifndef DINF_RING
+#define DINF_RING 8192    // LDS output history per member (bytes; its size sets the waves per CU)
+#endif
+#ifndef DINF_LB
+#define DINF_LB 10        // literal/length root table bits
+#endif
 constexpr int kW = 64;
-constexpr int kLB = 10;                    // literal/length root table bits
+constexpr int kLB = DINF_LB;               // literal/length root table bits
 constexpr int kDB = 8;                     // distance root table bits
 constexpr int kCB = 7;                     // code-length code (all codes <= 7 bits)
-constexpr uint32_t kRing = 8192;           // output history in LDS
+constexpr uint32_t kRing = DINF_RING;      // output history in LDS
 constexpr uint32_t kRM = kRing - 1;
-constexpr uint32_t kPiece = 4096;          // ring -> HBM write unit
+constexpr uint32_t kPiece = kRing / 2;     // ring -> HBM write unit
+constexpr uint32_t kStripe = kPiece / kW;  // CRC stripe per lane in a piece
+static_assert((kRing & (kRing - 1)) == 0 && kRing >= 2048, "ring: a power of two");
+// bytes not yet in HBM stay in the ring: [gpos, opos) spans < kPiece + 322
+// (a match of <= 258 and <= 63 literals between keep_room calls) and a step
+// writes <= 320 bytes past opos
+static_assert(kPiece + 322 + 320 <= kRing, "the ring holds the unwritten bytes");
 constexpr int kPad = 1024;                 // readable bytes past the last member (window prefetch)
 
 // root entry: bits 0-4 bits to consume (0: a longer code, canonical slow path),
@@ -102,7 +114,7 @@ struct Args {
     uint8_t *status;
     uint32_t *dbg;                        // [4 n]: failing loop, bits used, output bytes, iterations (may be null)
     int32_t n;
-    uint32_t x8n_piece;                   // x^(8*4096) mod P
+    uint32_t x8n_piece;                   // x^(8 kPiece) mod P
 };
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -334,7 +346,7 @@ __device__ __noinline__ uint32_t write_piece(uint8_t *g, uint32_t g0, uint32_t m
     } else {
         for (uint32_t k = lane; k < m; k += kW) dst[k] = s.ring[(g0 + k) & kRM];
     }
-    const uint32_t lo = min(m, (uint32_t)lane * 64), hi = min(m, (uint32_t)lane * 64 + 64);
+    const uint32_t lo = min(m, (uint32_t)lane * kStripe), hi = min(m, (uint32_t)lane * kStripe + kStripe);
     uint32_t c = hi > lo ? crc_stripe(s, g0 + lo, hi - lo) : 0;
     if (hi > lo) c = dfl::multmodp(m == kPiece ? lane_shift : dfl::x8nmodp(m - hi), c);
     for (int d = 32; d >= 1; d >>= 1) c ^= __shfl_xor(c, d, kW);
@@ -369,8 +381,8 @@ __global__ __launch_bounds__(64) void k_inflate(Args a) {
     if (mi >= a.n) return;
     const dcr_bgzf_member M = a.m[mi];
     for (int i = lane; i < 256; i += kW) s.crc_tab[i] = dfl::crc_byte((uint32_t)i);
-    // x^(8 (4096 - 64 (l + 1))) mod P: the shift of lane l's 64-byte stripe to a piece's end
-    const uint32_t lsh = dfl::x8nmodp(kPiece - 64u * (uint32_t)(lane + 1));
+    // x^(8 (kPiece - kStripe (l + 1))) mod P: the shift of lane l's stripe to a piece's end
+    const uint32_t lsh = dfl::x8nmodp(kPiece - kStripe * (uint32_t)(lane + 1));
 
     Out o;
     o.g = a.out + M.out_off;

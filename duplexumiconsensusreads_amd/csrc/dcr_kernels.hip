@@ -2655,7 +2655,7 @@ constexpr int kM720 = kOv + kWaves * 512;                  // u32 [64] 720720 / 
 #define DCR_LDS_PAD 0
 #endif
 constexpr int kSofs = kM720 + 64 * 4;                      // u32 [10][2]: record-scalar array offsets from sbase, shifts
-constexpr int kLdsBytes = kSofs + 16 * 8 + DCR_LDS_PAD;       // PAD: diagnostic builds only
+constexpr int kLdsBytes = kSofs + 10 * 8 + DCR_LDS_PAD;       // PAD: diagnostic builds only
 static_assert(kStageElems * 2 == 0x1000, "one 4 KiB stage per wave");
 static_assert(16 * (kRowMax + 5) <= 0x800, "a class bank fits 2 KiB");
 static_assert(5 * kLdsBytes <= 160 * 1024, "five blocks (20 waves) per CU");
@@ -3215,7 +3215,10 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
             } else {
             double L4[4] = {1.0, 1.0, 1.0, 1.0};
             double U = 1.0;
-            for (int r = 0; r < R; ++r) {
+            // read r's row at the lane's column: class after the mask (the
+            // table's 'N' rows: class N, or quality below min_base_quality,
+            // :280) and the factors (1 - p', p'/5) of its raw quality
+            auto fetch = [&](int r, uint32_t &k, double2 &f) {
                 const int cr = readlane(crv, r);
                 const int x = readlane((int)rm.x, r);
                 const int col = x & 255, len = (x >> 8) & 255;
@@ -3223,13 +3226,31 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
                 const uint32_t code = *(const uint16_t *)(lds + ad);
                 const uint32_t kc = code >> 11;                      // code bank: N 0, A 1, T 2, C 3, G 4
                 const uint32_t q = ((code >> 4) & 127u) - kc;        // raw quality (pad 'N': 2)
-                const uint32_t k = (*(const uint32_t *)(lds + code + 8) & 63u) ? 0u : kc;   // masked rows: 'N'
-                const double2 f = xt[q];                             // (1 - p', p'/5), LDS copy of P's rows
-                const double fm = f.x, fx = f.y;
-                U = U * fx;
+                k = (kc == 0 || (int)q < a.minbq) ? 0u : kc;         // as the table's rows (k_consensus_fast prologue)
+                f = xt[q];                                           // LDS copy of P's rows
+            };
+            // the products in read order (:594-600)
+            auto apply = [&](uint32_t k, double2 f) {
+                U = U * f.y;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) L4[i] = L4[i] * (k == (uint32_t)(i + 1) ? fm : fx);
+                for (int i = 0; i < 4; ++i) L4[i] = L4[i] * (k == (uint32_t)(i + 1) ? f.x : f.y);
                 cnt += k ? 1u << (8 * (k - 1)) : 0u;
+            };
+            // two reads' loads in flight per step (their products stay in order)
+            int r = 0;
+            for (; r + 2 <= R; r += 2) {
+                uint32_t k0, k1;
+                double2 f0, f1;
+                fetch(r, k0, f0);
+                fetch(r + 1, k1, f1);
+                apply(k0, f0);
+                apply(k1, f1);
+            }
+            if (r < R) {
+                uint32_t k0;
+                double2 f0;
+                fetch(r, k0, f0);
+                apply(k0, f0);
             }
             const double L[6] = {L4[0], L4[1], L4[2], L4[3], U, U};
             po = posterior(L, false, P, qthr, true);
