@@ -221,3 +221,57 @@ def test_bgzf_writer_non_regular_outputs(tmp_path):
     w.close()
     th.join(30)
     assert gzip.decompress(got[0]) == data
+
+
+def _ingest_all(path, P, setup):
+    ing = native_io.Ingest(path, P.min_map_quality, P.min_reads, P.max_reads, P.min_base_quality, 2)
+    setup(ing)
+    bases = []
+    while True:
+        hb = native_io.HostBatch(reads=1 << 14, side_bytes=1 << 22)
+        ing.next(hb)
+        bases.append(hb.packed().bases.copy())
+        if hb.end_kind != native_io.END_FULL:
+            break
+    calls = ing.sample_calls()
+    ing.close()
+    return np.concatenate(bases), calls
+
+
+def test_state_gate(c1_bam):
+    """dcr_ingest_set_state_gate: called once, right before the first
+    random.sample call, and sampling then runs from the state it returns --
+    the same reads as an ingest started from that state."""
+    P = ConsensusParams(max_reads=3)
+    want_state = random.Random(99).getstate()
+    want, calls_w = _ingest_all(c1_bam, P, lambda ing: ing.set_rng_state(want_state))
+    seen = []
+
+    def setup(ing):
+        ing.set_rng_state(random.Random(1).getstate())     # a state the gate replaces
+        ing.set_state_gate(lambda: (seen.append(len(ing.sample_calls())), want_state)[1])
+    got, calls_g = _ingest_all(c1_bam, P, setup)
+    assert calls_w and calls_g == calls_w
+    assert seen == [0]                                     # once, before the first call
+    assert np.array_equal(got, want)
+    # an ingest that never samples never calls its gate
+    seen.clear()
+    _ingest_all(c1_bam, ConsensusParams(max_reads=1000), setup)
+    assert seen == []
+
+
+def test_state_gate_error_ends_ingest(c1_bam):
+    P = ConsensusParams(max_reads=3)
+    ing = native_io.Ingest(c1_bam, P.min_map_quality, P.min_reads, P.max_reads, P.min_base_quality, 2)
+
+    def bad():
+        raise RuntimeError("no state")
+    ing.set_state_gate(bad)
+    with pytest.raises(native_io.IOError_):
+        while True:
+            hb = native_io.HostBatch(reads=1 << 14, side_bytes=1 << 22)
+            ing.next(hb)
+            if hb.end_kind != native_io.END_FULL:
+                break
+    assert isinstance(ing.gate_error, RuntimeError)
+    ing.close()
