@@ -5,8 +5,8 @@
 // with the hook set, hands each chunk's members to this kernel instead of
 // inflating them on its host pool.
 //
-// k_inflate: one wavefront per member (a 64-thread workgroup, ~15 KB of LDS,
-// about ten per CU).  Huffman decoding is serial within a member, so the
+// k_inflate: one wavefront per member (a 64-thread workgroup, ~9.3 KB of LDS,
+// about 17 per CU).  Huffman decoding is serial within a member, so the
 // wave decodes it as one scalar stream (bit buffer, positions and tables'
 // results are wave-uniform, held in SGPRs) and uses its 64 lanes for
 // everything around that stream:
@@ -18,10 +18,11 @@
 //     bit buffer reaches them); the bit buffer refilled by v_readlane;
 //   - literals collected one per lane and written 64 at a time, matches
 //     copied by all lanes (a distance below 64 by its period);
-//   - the last 8 KiB of output kept in an LDS ring, the source of every match
-//     of distance <= 8 KiB; the ring is written to HBM in 4 KiB pieces with
-//     dword stores, and the CRC32 of each piece is formed on the way (64-byte
-//     stripes per lane, raw CRCs shifted by x^(8n) mod P and xor-reduced;
+//   - the last kRing bytes of output (4 KiB) kept in an LDS ring, the source
+//     of every match that reaches no further (older ones read HBM); the ring
+//     is written to HBM in pieces of half its size with dword stores, and the
+//     CRC32 of each piece is formed on the way (a stripe per lane, raw CRCs
+//     shifted by x^(8n) mod P and xor-reduced;
 //     zlib's crc32_combine algebra, dcr_deflate.h multmodp);
 //   - ISIZE and CRC32 checked against the member trailer on the device.
 #include <hip/hip_runtime.h>
@@ -66,11 +67,15 @@ struct IStamp {
     }
 };
 
+// LDS per wave sets the waves per CU, and a member's decode is latency-bound:
+// a 4 KiB ring and a 9-bit root table (9.3 KB, 17 waves per CU instead of 10
+// at 8 KiB / 10 bits) inflate a 4,096-member span in 5.65 ms instead of 9.09
+// (35.2 -> 47.5 GB/s over all members in one launch; profiles/r04e)
 #ifndef DINF_RING
-#define DINF_RING 8192    // LDS output history per member (bytes; its size sets the waves per CU)
+#define DINF_RING 4096    // LDS output history per member (bytes)
 #endif
 #ifndef DINF_LB
-#define DINF_LB 10        // literal/length root table bits
+#define DINF_LB 9         // literal/length root table bits
 #endif
 constexpr int kW = 64;
 constexpr int kLB = DINF_LB;               // literal/length root table bits
@@ -315,7 +320,7 @@ __device__ __forceinline__ int slow_decode(Dec &d, const uint16_t *cnt, const ui
 struct Out {
     uint8_t *g;               // member output in HBM
     uint32_t isize;
-    uint32_t opos;            // bytes produced (ring holds [opos - 8 KiB, opos))
+    uint32_t opos;            // bytes produced (ring holds [opos - kRing, opos))
     uint32_t gpos;            // bytes written to HBM
     uint32_t crc;             // raw CRC (init 0) of [0, gpos)
     uint32_t lbuf;            // pending literal of this lane
@@ -330,8 +335,8 @@ __device__ __forceinline__ uint32_t crc_stripe(const WaveLds &s, uint32_t from, 
 
 extern __shared__ __align__(16) unsigned char smem[];
 
-// write ring bytes [g0, g0 + m) to HBM (m <= 4096) and fold them into the raw
-// CRC; one out-of-line copy (called every 4 KiB) keeps the decode loop small
+// write ring bytes [g0, g0 + m) to HBM (m <= kPiece) and fold them into the
+// raw CRC; one out-of-line copy (called every kPiece bytes) keeps the decode loop small
 __device__ __noinline__ uint32_t write_piece(uint8_t *g, uint32_t g0, uint32_t m, uint32_t crc, uint32_t lane_shift,
                                              uint32_t x8n_piece) {
     const WaveLds &s = *reinterpret_cast<const WaveLds *>(smem);
@@ -356,9 +361,9 @@ __device__ __noinline__ uint32_t write_piece(uint8_t *g, uint32_t g0, uint32_t m
 
 // Ring writes past the bytes produced are harmless: positions in
 // [opos, opos + 64) are rewritten before anything reads them, and their ring
-// slots alias bytes older than opos + 64 - 8 KiB, which no match reads
+// slots alias bytes older than opos + 64 - kRing, which no match reads
 // (distances from the ring stay <= kRingDist) and which are already in HBM
-// (gpos > opos - 4 KiB - 322).  So literal flushes and match copies store all
+// (gpos > opos - kPiece - 322).  So literal flushes and match copies store all
 // 64 lanes, with no exec masking.
 constexpr uint32_t kRingDist = kRing - kW;
 

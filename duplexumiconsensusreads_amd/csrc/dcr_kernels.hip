@@ -77,99 +77,6 @@ struct WaveLds {
     double stk_left[24];
 };
 
-// ---- the insertion layout by events (general kernel, records of <= 128 reads
-// with insertion columns).  reconstruct_alignment (:430-547) run as a scan
-// over its events instead of column by column: a column is an insertion column
-// exactly while some read sits at an I op (:476-478).  A read advances one op
-// per normal column once pos >= its start (M/D; only while its sequence lasts,
-// :514), and through its own I runs only at insertion columns; so the I runs
-// of all reads happen in "blocks" of consecutive insertion columns, and the
-// next block starts at the earliest column where some read reaches its next I
-// run.  The wave finds the blocks one event at a time (lane = read), then
-// every column tile is laid out in parallel (lane = column): a normal column
-// t is read r's normal advance a = N(t) - N(s_r) (N: normal columns before),
-// an insertion column of block b at offset o is read r's I run element o when
-// r takes part in b, else '+'.  The overlay lives in the wave's tile scratch.
-constexpr int kEvBlk = 32;               // insertion blocks per record
-constexpr int kEvEnt = 96;               // (read, block) participations per record
-constexpr int kEvReads = 128;            // reads per record (two 64-lane chunks)
-struct EvLds {
-    uint64_t bmask[kEvBlk][2];           // reads taking part in block b
-    // per read: first kept base - the record's staging base; offset of its
-    // runs from the record's run base; kept length | N(s_r) << 16 (the normal
-    // columns before its start column); number of runs
-    uint4 ri[kEvReads];
-    uint16_t bstart[kEvBlk], blen[kEvBlk], beoff[kEvBlk + 1];
-    uint16_t es0[kEvEnt], eL[kEvEnt];    // participation: sequence index of the I run's first base, run length
-};
-
-// The element of read ri in this lane's column of the event layout: -1 and
-// the code in c (pad, '+', '-'), or the sequence index whose base it takes.
-// A normal column is the read's normal advance av = N(t) - N(s_r): its av-th
-// M / D op, after the I runs before it (consumed in their blocks).
-__device__ __forceinline__ int ev_pos(const EvLds &EV, const uint4 ri, const uint32_t *cig0, int r, bool ins_col,
-                                      int bo, int nt, uint64_t mk0, uint64_t mk1, int eo, uint32_t &c, bool &idx_err) {
-    const int len = (int)(ri.z & 0xFFFFu);
-    if (ins_col) {                                       // :478-499
-        const uint64_t mk = r < kWave ? mk0 : mk1;
-        const int rb = r & (kWave - 1);
-        c = kPlus;
-        if (!((mk >> rb) & 1ull)) return -1;
-        const int idx = eo + (r < kWave ? 0 : __popcll(mk0)) + __popcll(mk & ((1ull << rb) - 1ull));
-        if (bo >= (int)EV.eL[idx]) return -1;            // its I run ended inside the block
-        const int is = (int)EV.es0[idx] + bo;
-        if (is >= len) { idx_err = true; c = kPad; return -1; }
-        return is;
-    }
-    c = kPad;
-    const int av = nt - (int)(ri.z >> 16);
-    if (av < 0) return -1;                               // :506-510
-    const int nc = (int)ri.w;
-    const uint32_t *cig = cig0 + ri.y;
-    if (nc == 1 && (cig[0] & 15u) == 0u) return av < len ? av : -1;   // one M run (the usual read)
-    int acc = 0, sq = 0;
-    for (int k = 0; k < nc; ++k) {
-        const uint32_t v = cig[k];
-        const int op = (int)(v & 15u), ln = (int)(v >> 4);
-        if (op == 1) { sq += ln; continue; }             // consumed in its block
-        if (av < acc + ln) {
-            const int is = sq + (op != 2 ? av - acc : 0);
-            if (is >= len) return -1;                    // :540-544
-            if (op == 2) { c = kDel; return -1; }        // :517-524
-            return is;                                   // :528-535
-        }
-        acc += ln;
-        if (op != 2) sq += ln;
-    }
-    if (sq < len) idx_err = true;                        // ops exhausted with bases left (:517)
-    return -1;
-}
-
-// a read's next I run from run index k with md M/D ops and sq bases consumed
-// before it: run index (-1: none reachable), M/D ops before it, length, first
-// base.  A read whose sequence has run out stops at its next M or D op for
-// good (:514, :540); an I run met right at the end of the sequence is reached
-// (its first element raises IndexError, :483).
-struct EvRead { int s, A, k, m, L, s0; };
-__device__ __forceinline__ void ev_next(EvRead &e, const uint32_t *cig, int ncig, int len, int k, int md, int sq) {
-    e.k = -1;
-    for (; k < ncig; ++k) {
-        const uint32_t v = cig[k];
-        const int op = (int)(v & 15u), ln = (int)(v >> 4);
-        if (op == 1) {
-            e.k = k;
-            e.m = md;
-            e.L = ln;
-            e.s0 = sq;
-            return;
-        }
-        if (sq >= len) return;           // stuck at an M / D op
-        if (op != 2 && sq + ln > len) return;   // the sequence runs out inside this M run
-        md += ln;
-        if (op != 2) sq += ln;           // M (and any other op kept as M, :528-535)
-    }
-}
-
 // class of an input base (A/T/C/G/N; anything else is invalid, :580-585)
 __device__ __forceinline__ uint32_t base_class(uint32_t b) {
     // 4-bit class per letter 'A'..'Z' packed in two 64-bit words; 7 = invalid
@@ -1435,95 +1342,6 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
     lr.cl = (myrd.pos - minpos) | (myrd.len << 16);
     lr.sn = (int)(myrd.seq_start - base_al) | (myrd.ncig << 16);
 
-    // ---- insertion layout by events (EvLds, see there): the blocks of
-    // insertion columns, one event per step (lane = read, two 64-read chunks)
-    static_assert(sizeof(EvLds) <= sizeof(W.tile), "the event layout lives in the tile scratch");
-    EvLds &EV = *reinterpret_cast<EvLds *>(&W.tile[0][0]);
-    int ev_nb = 0;
-    bool ev_ok = !FAST && ins && R <= kEvReads && T < 0xFFFF && DCR_ABL < 9;
-    const uint32_t *ev_cig0 = DUPLEX ? a.ss.cigar + a.in.ss_col_off[2 * rec] : a.ws.norm_cig;
-    if (ev_ok) {
-        EvRead ev[2];
-        bool valid[2];
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const int r = c * kWave + lane;
-            valid[c] = r < R;
-            ev[c] = EvRead{0x7fffffff, 0, -1, 0, 0, 0};
-            if (valid[c]) {
-                const ReadRef rd = get_read<DUPLEX>(a, rec, r);
-                ev[c].s = rd.pos - minpos;
-                EV.ri[r] = make_uint4((uint32_t)(rd.seq_start - base_al), (uint32_t)(rd.cig - ev_cig0),
-                                      (uint32_t)rd.len & 0xFFFFu, (uint32_t)rd.ncig);
-                ev_next(ev[c], rd.cig, rd.ncig, rd.len, 0, 0, 0);
-            }
-        }
-        // the next block starts where some read reaches its next I run: at
-        // once when it needs no further normal advance (an I op is current
-        // whatever pos is, :416-427), else after the missing advances, which
-        // only count from its start column on
-        int t = 0, ne = 0;
-        for (;;) {
-            int tr[2];
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-                tr[c] = valid[c] && ev[c].k >= 0
-                            ? (ev[c].m == ev[c].A ? t : max(t, ev[c].s) + (ev[c].m - ev[c].A))
-                            : 0x7fffffff;
-            const int te = wave_min(min(tr[0], tr[1]));
-            if (te >= T) break;
-            if (ev_nb == kEvBlk) { ev_ok = false; break; }
-            bool part[2];
-            int lmax = 0;
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                part[c] = tr[c] == te;
-                // normal columns [t, te) advance the reads that have started
-                ev[c].A += max(0, te - max(t, ev[c].s));
-                lmax = max(lmax, part[c] ? ev[c].L : 0);
-            }
-            const int lb = wave_max(lmax);
-            const uint64_t pm0 = __ballot(part[0]), pm1 = __ballot(part[1]);
-            const int np = __popcll(pm0) + __popcll(pm1);
-            if (ne + np > kEvEnt) { ev_ok = false; break; }
-            if (lane == 0) {
-                EV.bstart[ev_nb] = (uint16_t)te;
-                EV.blen[ev_nb] = (uint16_t)min(lb, T - te);
-                EV.beoff[ev_nb] = (uint16_t)ne;
-                EV.bmask[ev_nb][0] = pm0;
-                EV.bmask[ev_nb][1] = pm1;
-            }
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                if (part[c]) {
-                    const int idx = ne + (c ? __popcll(pm0) : 0) + __popcll((c ? pm1 : pm0) & lanemask_lt(lane));
-                    EV.es0[idx] = (uint16_t)ev[c].s0;
-                    EV.eL[idx] = (uint16_t)ev[c].L;
-                    const ReadRef rd = get_read<DUPLEX>(a, rec, c * kWave + lane);
-                    ev_next(ev[c], rd.cig, rd.ncig, rd.len, ev[c].k + 1, ev[c].m, ev[c].s0 + ev[c].L);
-                }
-            }
-            ne += np;
-            ++ev_nb;
-            t = te + lb;
-        }
-        if (ev_ok) {
-            if (lane == 0) EV.beoff[ev_nb] = (uint16_t)ne;
-            lds_fence();
-            // N(s_r): the normal columns before each read's start column
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                if (valid[c]) {
-                    int ib = 0;
-                    for (int b = 0; b < ev_nb; ++b)
-                        ib += min(max(ev[c].s - (int)EV.bstart[b], 0), (int)EV.blen[b]);
-                    EV.ri[c * kWave + lane].z |= (uint32_t)(ev[c].s - ib) << 16;
-                }
-            }
-        }
-        lds_fence();
-    }
-
     // R > 64 with insertion columns: precompute the insertion-column flags
     // (all reads must be consulted per column, :476-478) and keep per-read
     // layout state in global scratch between column tiles.
@@ -1533,7 +1351,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
     // within 64-read chunk c): the flags pass walks the runs without touching
     // HBM, and the tiles stage each chunk's next 32 bytes per read
     constexpr int kBigCh = 4;
-    const bool regbig = !FAST && ins && big && !DUPLEX && R <= kBigCh * kWave && !ev_ok;
+    const bool regbig = !FAST && ins && big && !DUPLEX && R <= kBigCh * kWave;
     struct SlimRead {
         int pos, len, ncig;
         const uint32_t *cig;
@@ -1581,7 +1399,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
         }
         wave_fence();
     }
-    if (!FAST && ins && big && !DUPLEX && !regbig && !ev_ok) {
+    if (!FAST && ins && big && !DUPLEX && !regbig) {
         for (int c = 0; c < R; c += kWave) {
             const int r = c + lane;
             if (r < R) {
@@ -1666,7 +1484,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
     };
 
     // ---- phases 1+2: column tiles (lane = column)
-    const int tw = ins && !ev_ok ? kTileIns : kWave;       // stepped insertion layout: 32-column tiles
+    const int tw = ins ? kTileIns : kWave;       // insertion layout: 32-column tiles
     for (int c0 = 0; c0 < T; c0 += tw) {
         const int t = c0 + lane;
         const bool live = lane < tw && t < T;
@@ -1712,87 +1530,6 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
                 return e;
             };
             accumulate(A, R, src, s_lut);
-        } else if (ev_ok) {
-            // the event layout: this lane's column is in insertion block bi at
-            // offset bo, or normal with N(t) normal columns before it
-            int insb = 0, bi = -1, bo = 0;
-            for (int b = 0; b < ev_nb; ++b) {
-                const int bs = EV.bstart[b], bl = EV.blen[b];
-                if (t >= bs + bl) insb += bl;
-                else if (t >= bs) { bi = b; bo = t - bs; }
-            }
-            ins_col = live && bi >= 0;
-            const int nt = t - insb;
-            uint64_t mk0 = 0, mk1 = 0;
-            int eo = 0;
-            if (bi >= 0) {
-                mk0 = EV.bmask[bi][0];
-                mk1 = EV.bmask[bi][1];
-                eo = EV.beoff[bi];
-            }
-            if (fits) {
-                // the bases are staged: a read's element is one more LDS read
-                auto src = [&](int r) -> uint32_t {
-                    uint32_t c;
-                    const uint4 ri = EV.ri[r];
-                    const int is = live ? ev_pos(EV, ri, ev_cig0, r, ins_col, bo, nt, mk0, mk1, eo, c, idx_err) : -1;
-                    return is >= 0 ? (uint32_t)W.stage[ri.x + is] : (live ? c : kPad);
-                };
-                tdec = decide_tile(a, R, live, ins_col, src, s_wtab, tco);
-                if (!tdec) accumulate(A, R, src, s_lut);
-            } else {
-                // 32 reads at a time: their codes in this tile's columns into
-                // the (unused) stage, [read][column], four reads' base and
-                // quality loads in flight together; the decision sums first,
-                // the products only when some column stays undecided
-                const uint8_t *gbb = gb + base_al, *gqb = gq + base_al;
-                uint16_t *cb = W.stage;
-                auto stage_group = [&](int g0, int ng) {
-                    lds_fence();
-                    for (int r0 = 0; r0 < ng; r0 += 4) {
-                        int is[4];
-                        uint32_t c[4], so[4];
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const int r = g0 + min(r0 + j, ng - 1);
-                            const uint4 ri = EV.ri[r];
-                            so[j] = ri.x;
-                            is[j] = live ? ev_pos(EV, ri, ev_cig0, r, ins_col, bo, nt, mk0, mk1, eo, c[j], idx_err) : -1;
-                            if (!live) c[j] = kPad;
-                        }
-                        uint32_t bq[4][2];
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const int o = (int)so[j] + max(is[j], 0);
-                            bq[j][0] = is[j] >= 0 ? gbb[o] : 0u;
-                            bq[j][1] = is[j] >= 0 ? gqb[o] : 0u;
-                        }
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if (r0 + j < ng)
-                                cb[((r0 + j) << 6) + lane] =
-                                    (uint16_t)(is[j] >= 0 ? make_code<DUPLEX>(bq[j][0], bq[j][1], minbq) : c[j]);
-                    }
-                    lds_fence();
-                };
-                auto src_cb = [&](int rr) -> uint32_t { return (uint32_t)cb[(rr << 6) + lane]; };
-                if (decide_usable(a, R)) {
-                    DecideSums D;
-                    for (int g0 = 0; g0 < R; g0 += 32) {
-                        const int ng = min(32, R - g0);
-                        stage_group(g0, ng);
-                        for (int rr = 0; rr < ng; ++rr) D.add(src_cb(rr), s_wtab);
-                    }
-                    tdec = decide_end(a, R, live, ins_col, D, tco);
-                }
-                if (!tdec) {
-                    for (int g0 = 0; g0 < R; g0 += 32) {
-                        const int ng = min(32, R - g0);
-                        stage_group(g0, ng);
-                        accumulate(A, ng, src_cb, s_lut);
-                    }
-                }
-            }
         } else if (!big) {
             uint64_t insmask = 0;
             // bytes that do not fit the stage: each read's next 32 bytes (the
@@ -2658,7 +2395,10 @@ constexpr int kSofs = kM720 + 64 * 4;                      // u32 [10][2]: recor
 constexpr int kLdsBytes = kSofs + 10 * 8 + DCR_LDS_PAD;       // PAD: diagnostic builds only
 static_assert(kStageElems * 2 == 0x1000, "one 4 KiB stage per wave");
 static_assert(16 * (kRowMax + 5) <= 0x800, "a class bank fits 2 KiB");
-static_assert(5 * kLdsBytes <= 160 * 1024, "five blocks (20 waves) per CU");
+// five blocks per CU need <= 32,000 B each (measured, DESIGN §3: 32,016 B ran
+// four blocks per CU and took 26 % longer than 31,968 B): 1,280-byte units
+constexpr int kLdsUnit = 1280;
+static_assert(5 * ((kLdsBytes + kLdsUnit - 1) / kLdsUnit) * kLdsUnit <= 160 * 1024, "five blocks (20 waves) per CU");
 
 __device__ __forceinline__ int stage_base(int wave) { return kStage0 + (wave << 12); }
 // pointer-cache slots: every pointer the record loop stores through is read

@@ -18,7 +18,9 @@ import functools
 import io
 import os
 import random
+import time
 
+import numpy as np
 import pytest
 
 from duplexumiconsensusreads_amd import bam, cli, synth
@@ -38,12 +40,25 @@ def _run(inp, out, backend, rng, extra=()):
     return buf.getvalue(), stats
 
 
+def _progress(capsys, msg):
+    """A line on the real terminal while pytest captures output (the long
+    cases would otherwise be silent for minutes)."""
+    with capsys.disabled():
+        print(msg, flush=True)
+
+
 def _compare(out_gpu, out_cpu):
     for suf in SUFFIXES:
         a = bam.bgzf_stream(out_gpu[:-4] + suf)
         b = bam.bgzf_stream(out_cpu[:-4] + suf)
-        assert len(a) == len(b), suf
-        assert a == b, suf
+        if a != b:
+            # a small message: pytest's own diff of two streams of hundreds
+            # of MB would not finish
+            n = min(len(a), len(b))
+            ne = np.frombuffer(a, np.uint8, n) != np.frombuffer(b, np.uint8, n)
+            k = int(ne.argmax()) if ne.any() else n
+            pytest.fail(f"{suf}: lengths {len(a)} / {len(b)}, first difference at byte {k}: "
+                        f"gpu {a[max(0, k - 16):k + 16].hex()} cpu {b[max(0, k - 16):k + 16].hex()}")
 
 
 def test_cli_device_writer_full_c2_input(tmp_path):
@@ -87,28 +102,34 @@ def test_cli_c4_default_max_reads_downsampled(tmp_path):
     _compare(str(tmp_path / "gpu.bam"), str(tmp_path / "cpu.bam"))
 
 
-def test_cli_device_writer_c3_shard(tmp_path):
+def test_cli_device_writer_c3_shard(tmp_path, capsys):
     """One GPU's share of C3 (100 M reads over 8 GPUs: 400 k families, ~12.3 M
     reads) with its insertion layouts, deletions, soft clips and Zipf(1.5)
     subfamily sizes 1..100, at BGZF level 6 and the CLI's default batch: the
     general and exact kernels, the device writer and the device inflate all
     on the product path, byte-compared with the oracle-backend CLI
     (reference :473-545 insertion columns, :191-265 clips, :1519-1631)."""
+    t0 = time.perf_counter()
     inp = str(tmp_path / "c3.bam")
     packed = synth.packed_config(synth.CONFIGS["C3"], 400_000, seed=3)
     synth.write_packed_bam(inp, packed, seed=3, level=6)
     n_fam = packed.n_fam
     del packed
+    _progress(capsys, f"c3 shard: input written in {time.perf_counter() - t0:.1f} s")
     from duplexumiconsensusreads_amd.params import ConsensusParams
     be = cli.default_backend(ConsensusParams())
     assert be.device_writer
     out_gpu = str(tmp_path / "gpu.bam")
     out_cpu = str(tmp_path / "cpu.bam")
+    t0 = time.perf_counter()
     so_gpu, st_gpu = _run(inp, out_gpu, be, random.Random(4))
+    _progress(capsys, f"c3 shard: GPU CLI {time.perf_counter() - t0:.1f} s, {st_gpu['batches']} batches")
     assert st_gpu["batches"] >= 20
     assert st_gpu["consensus_records"] == 2 * n_fam
     oracle = functools.partial(dcr_oracle_c.run, n_threads=min(16, os.cpu_count() or 1))
+    t0 = time.perf_counter()
     so_cpu, st_cpu = _run(inp, out_cpu, oracle, random.Random(4))
+    _progress(capsys, f"c3 shard: oracle CLI {time.perf_counter() - t0:.1f} s")
     assert so_gpu == so_cpu
     assert st_gpu["consensus_bases"] == st_cpu["consensus_bases"]
     _compare(out_gpu, out_cpu)

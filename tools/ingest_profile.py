@@ -1,6 +1,11 @@
 """Host ingest throughput of the native BAM reader (libdcr_io.so) over the
 C2 bench BAM at several thread counts, with per-stage times
-(DCR_INGEST_PROF=1): run on the GPU box's host cores."""
+(DCR_INGEST_PROF=1): run on the GPU box's host cores.
+
+    python3 tools/ingest_profile.py BAM [gpu] [threads ...]
+
+``gpu``: the device inflate hook set first (cli.gpu_inflate), as the CLI
+runs it; the ingest alone, no consensus or writer."""
 import os
 import resource
 import sys
@@ -17,7 +22,12 @@ def main():
         t = time.time()
         synth.write_packed_bam(path, synth.packed_fixed_size(312_500, seed=2), seed=2, level=1)
         print(f"wrote {os.path.getsize(path) / 1e6:.0f} MB in {time.time() - t:.1f} s", flush=True)
-    for th in [int(a) for a in sys.argv[2:]] or [16]:
+    rest = sys.argv[2:]
+    if rest and rest[0] == "gpu":
+        from duplexumiconsensusreads_amd import cli
+        cli.gpu_inflate(0)
+        rest = rest[1:]
+    for th in [int(a) for a in rest] or [16]:
         hbs = [native_io.HostBatch(reads=1 << 19) for _ in range(2)]
         r0 = resource.getrusage(resource.RUSAGE_SELF)
         t0 = time.perf_counter()
