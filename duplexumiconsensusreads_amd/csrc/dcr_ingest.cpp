@@ -911,7 +911,7 @@ class Inflater {
 // DCR_INGEST_PROF=1: seconds per ingest stage, printed to stderr at close
 struct IngestProf {
     bool on = std::getenv("DCR_INGEST_PROF") != nullptr;
-    double wait_chunk = 0, scan = 0, parse = 0, flush = 0, walk_total = 0;
+    double wait_chunk = 0, scan = 0, parse = 0, flush = 0, walk_total = 0, complete = 0;
     int64_t indexed = 0;
     static double now() {
         return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -961,9 +961,10 @@ struct dcr_ingest {
         pk_stop_thread();
         if (prof.on)
             std::fprintf(stderr,
-                         "[ingest] walk %.3f s: chunk wait %.3f, serial scan %.3f, parse %.3f, pack copy %.3f; "
-                         "scanner stage: chain %.3f, parse %.3f; indexed records %lld of %lld\n",
-                         prof.walk_total, prof.wait_chunk, prof.scan, prof.parse, prof.flush, infl ? infl->scan_s : 0.0,
+                         "[ingest] walk %.3f s: chunk wait %.3f, serial scan %.3f, parse %.3f, pack copy %.3f, "
+                         "families %.3f; scanner stage: chain %.3f, parse %.3f; indexed records %lld of %lld\n",
+                         prof.walk_total, prof.wait_chunk, prof.scan, prof.parse, prof.flush, prof.complete,
+                         infl ? infl->scan_s : 0.0,
                          infl ? infl->index_parse_s : 0.0, (long long)prof.indexed, (long long)records);
         infl.reset();             // stops the inflate thread before the file closes
         if (f) std::fclose(f);
@@ -974,7 +975,8 @@ struct dcr_ingest {
     int need(size_t n) {
         while (wend - wpos < n) {
             if (data_eof) return 0;
-            flush_jobs();                           // the jobs point into the current window
+            if (flush_tasks() < 0) return -1;       // the tasks and jobs point into the current window
+            flush_jobs();
             const double tw = prof.on ? IngestProf::now() : 0;
             Chunk *nx = infl->next();
             if (prof.on) prof.wait_chunk += IngestProf::now() - tw;
@@ -1034,22 +1036,26 @@ struct dcr_ingest {
     void pk_start_thread() {
         pk_th = std::thread([this] {
             for (;;) {
-                size_t j0, j1;
+                size_t j0, j1, t0, t1;
                 const uint8_t *w;
                 dcr_host_batch *b;
                 {
                     std::unique_lock<std::mutex> lk(pk_mu);
-                    pk_cv.wait(lk, [&] { return pk_quit || pk_sub > pk_done; });
+                    pk_cv.wait(lk, [&] { return pk_quit || pk_sub > pk_done || tk_sub > tk_done; });
                     if (pk_quit) return;
                     j0 = pk_done;
                     j1 = pk_sub;
+                    t0 = tk_done;
+                    t1 = tk_sub;
                     w = pk_w;
                     b = pk_b;
                 }
-                pack_range(w, b, jobs.data(), j0, j1);
+                if (t1 > t0) run_tasks(w, b, t0, t1);
+                if (j1 > j0) pack_range(w, b, jobs.data(), j0, j1);
                 {
                     std::lock_guard<std::mutex> g(pk_mu);
                     pk_done = j1;
+                    tk_done = t1;
                 }
                 pk_cv.notify_all();
             }
@@ -1075,6 +1081,262 @@ struct dcr_ingest {
         }
         pk_cv.notify_all();
     }
+    // -- deferred family completion --------------------------------------------
+    // A family with nothing to sample (the common case) is reserved by the
+    // walk -- its table entry, names, read / base / CIGAR / side-byte ranges
+    // and column offsets, all sizes known from one pass over its records --
+    // and the rest of complete_family (the UMI and rname checks, the split
+    // and the per-read fields and copies) runs as a task on the packer thread
+    // and its pool while the walk goes on.  Tasks point into the window and
+    // the records, so they are drained (flush_tasks) before either changes,
+    // before a family that samples (the checks of earlier families come
+    // first, :1548-1551) and at the end of a batch; the first task (in input
+    // order) that fails truncates the batch to its reservation and stops
+    // there, exactly where complete_family would have stopped.
+    struct FamTask {
+        uint32_t rb, n;                 // the family's records: pend_recs[rb, rb + n)
+        int32_t t, f;                   // table entry; processed family (-1: filtered)
+        int64_t read_base, base_off[4], cig_off[4];   // per subfamily (split order)
+        int64_t filt_off;               // filtered: its bytes in side_filt
+        // the batch and counters as they were before this family
+        int32_t fam_before;
+        int64_t names_before, exc_before, filt_before, ss_before, ds_before;
+        int64_t c_passed, c_records, c_excluded, c_processed, c_filtered;
+        int err_kind = DCR_ERR_NONE;
+        std::string err;
+    };
+    std::vector<FamTask> tasks;
+    std::vector<const Rec *> pend_recs;
+    size_t tk_sub = 0, tk_done = 0;      // tasks [0, tk_sub) handed over, [0, tk_done) run
+    static constexpr size_t kTkStep = 256;
+
+    void run_task(FamTask &T, const uint8_t *w, dcr_host_batch *b) const {
+        const Rec *const *fr = pend_recs.data() + T.rb;
+        std::string umi2;
+        T.err_kind = check_family(fr, T.n, w, umi2, T.err);
+        if (T.err_kind != DCR_ERR_NONE) return;
+        if (T.f < 0) {                  // filtered: its reads to _filteredfamilies.bam in input order
+            int64_t o = T.filt_off;
+            for (uint32_t i = 0; i < T.n; ++i) {
+                std::memcpy(b->side_filt + o, w + fr[i]->off, fr[i]->len);
+                o += fr[i]->len;
+            }
+            return;
+        }
+        // split_family order: subfamily k's reads in input order after those of k - 1
+        int64_t ri[4], bo[4], co[4];
+        int64_t acc = T.read_base;
+        for (int k = 0; k < 4; ++k) {
+            ri[k] = acc;
+            acc = b->sub_off[4 * T.f + k + 1];
+            bo[k] = T.base_off[k];
+            co[k] = T.cig_off[k];
+        }
+        for (uint32_t j = 0; j < T.n; ++j) {
+            const Rec &rc = *fr[j];
+            const int k = rc.subk;
+            if (k < 0) continue;
+            const uint8_t *r = w + rc.off + 4;
+            const uint32_t l_rn = r[8];
+            const uint32_t n_cig = rd16(r + 12);
+            const int32_t l_seq = rdi32(r + 16);
+            const int64_t i = ri[k]++;
+            b->read_pos[i] = rdi32(r + 4);
+            b->read_mapq[i] = r[9];
+            b->seq_len[i] = l_seq;
+            b->seq_off[i] = bo[k];
+            b->cig_off[i] = (int32_t)co[k];
+            b->cig_n[i] = (int32_t)n_cig;
+            const uint8_t *cig = r + 32 + l_rn;
+            std::memcpy(b->cigar + co[k], cig, 4u * n_cig);
+            const uint8_t *sq = cig + 4u * n_cig;
+            decode_seq(sq, l_seq, b->bases + bo[k]);
+            std::memcpy(b->quals + bo[k], sq + ((l_seq + 1) >> 1), (size_t)l_seq);
+            bo[k] += l_seq;
+            co[k] += n_cig;
+        }
+    }
+    void run_tasks(const uint8_t *w, dcr_host_batch *b, size_t t0, size_t t1) {
+        const size_t chunk = 32;
+        pool->run((t1 - t0 + chunk - 1) / chunk, [&](size_t c) {
+            const size_t te = std::min(t1, t0 + (c + 1) * chunk);
+            for (size_t t = t0 + c * chunk; t < te; ++t) run_task(tasks[t], w, b);
+            return true;
+        });
+    }
+    void kick_tasks(bool force) {
+        if (tasks.size() == tk_sub || (!force && tasks.size() - tk_sub < kTkStep)) return;
+        {
+            std::lock_guard<std::mutex> g(pk_mu);
+            tk_sub = tasks.size();
+            pk_w = wb;
+            pk_b = hb;
+        }
+        pk_cv.notify_all();
+    }
+    // run every queued task; the first failure (input order) cuts the batch
+    // to that family's reservation and stops there.  1 ok, -1 stopped.
+    int flush_tasks() {
+        if (tasks.empty()) return 1;
+        kick_tasks(true);
+        {
+            std::unique_lock<std::mutex> lk(pk_mu);
+            pk_cv.wait(lk, [&] { return tk_done == tk_sub; });
+            tk_sub = tk_done = 0;
+        }
+        int rc = 1;
+        for (FamTask &T : tasks) {
+            if (T.err_kind == DCR_ERR_NONE) continue;
+            dcr_host_batch *b = hb;
+            b->n_tab = T.t;
+            b->n_fam = T.fam_before;
+            b->n_reads = T.read_base;
+            b->n_bases = T.base_off[0];
+            b->n_cigar = T.cig_off[0];
+            b->n_names = T.names_before;
+            b->n_side_exc = T.exc_before;
+            b->n_side_filt = T.filt_before;
+            b->ss_cols = T.ss_before;
+            b->ds_cols = T.ds_before;
+            passed = T.c_passed;
+            records = T.c_records;
+            excluded = T.c_excluded;
+            processed = T.c_processed;
+            filtered = T.c_filtered;
+            rc = stop(T.err_kind, T.err);
+            break;
+        }
+        tasks.clear();
+        pend_recs.clear();
+        return rc;
+    }
+
+    // preprocess_family for a family that samples nothing, deferred (above);
+    // a family that samples, or that the reservation cannot describe, takes
+    // complete_family after the queued tasks.  Returns as complete_family.
+    int queue_family() {
+        dcr_host_batch *b = hb;
+        const Rec &r0 = *fam.front();
+        int64_t nb = 0, nc = 0, filt_bytes = 0;
+        int64_t cnt[4] = {0, 0, 0, 0}, nbk[4] = {0, 0, 0, 0}, nck[4] = {0, 0, 0, 0};
+        int64_t mn[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0};
+        int16_t eqx[4] = {0, 0, 0, 0};
+        const Rec *first[4] = {nullptr, nullptr, nullptr, nullptr};
+        for (const Rec *r : fam) {
+            nb += r->l_seq;
+            nc += r->n_cig;
+            filt_bytes += r->len;
+            const int k = r->subk;
+            if (k < 0) continue;
+            if (!first[k]) {
+                first[k] = r;
+                mn[k] = r->pos;
+                mx[k] = r->end_kept;
+            } else {
+                if (r->pos < mn[k]) mn[k] = r->pos;
+                if (r->end_kept > mx[k]) mx[k] = r->end_kept;
+            }
+            ++cnt[k];
+            nbk[k] += r->l_seq;
+            nck[k] += r->n_cig;
+            if (eqx[k] < 0x7fff && r->eqx) ++eqx[k];
+        }
+        bool samples = false, enough = true;
+        for (int k = 0; k < 4; ++k) {                      // check_number_reads (:157-188)
+            if (cnt[k] < cfg.min_reads) { enough = false; break; }
+            if (cnt[k] > cfg.max_reads) { samples = true; break; }
+        }
+        const size_t l_code = r0.l_code;
+        const int64_t names_need = (int64_t)l_code + 1 + 2 * (int64_t)(r0.l_rx + 1) + 64 * 2;
+        if (samples || pend_recs.size() + fam.size() > pend_recs.capacity() || tasks.size() == tasks.capacity()) {
+            if (flush_tasks() < 0) return -1;
+            return complete_family();
+        }
+        const bool fits = b->n_tab < b->cap_tab && b->n_fam < b->cap_fam &&
+                          b->n_reads + (int64_t)fam.size() <= b->cap_reads && b->n_bases + nb <= b->cap_bases &&
+                          b->n_cigar + nc <= b->cap_cigar && b->n_names + names_need <= b->cap_names &&
+                          b->n_side_filt + filt_bytes <= b->cap_side;
+        if (!fits) {
+            if (b->n_tab == 0 && b->n_side_exc == 0) {
+                if (flush_tasks() < 0) return -1;
+                return fail_capacity("one family exceeds the batch capacities");
+            }
+            return 0;
+        }
+        FamTask T;
+        T.rb = (uint32_t)pend_recs.size();
+        T.n = (uint32_t)fam.size();
+        T.fam_before = b->n_fam;
+        T.names_before = b->n_names;
+        T.exc_before = b->n_side_exc;
+        T.filt_before = b->n_side_filt;
+        T.ss_before = b->ss_cols;
+        T.ds_before = b->ds_cols;
+        T.read_base = b->n_reads;
+        T.c_passed = passed;
+        T.c_records = records;
+        T.c_excluded = excluded;
+        T.c_processed = processed;
+        T.c_filtered = filtered;
+        const int32_t t = b->n_tab++;
+        T.t = t;
+        b->tab_sampled[t] = 0;
+        b->tab_exc_cut[t] = b->n_side_exc;
+        b->tab_filt_cut[t] = b->n_side_filt;
+        b->tab_code[t] = put_name(code_of(r0), l_code);
+        const int64_t code_off = b->tab_code[t];
+        int64_t bo = b->n_bases, co = b->n_cigar;
+        for (int k = 0; k < 4; ++k) {
+            T.base_off[k] = bo;
+            T.cig_off[k] = co;
+            bo += nbk[k];
+            co += nck[k];
+        }
+        if (!enough) {
+            b->tab_kind[t] = DCR_FAM_FILTERED;
+            b->tab_proc[t] = -1;
+            T.f = -1;
+            T.filt_off = b->n_side_filt;
+            b->n_side_filt += filt_bytes;
+            ++filtered;
+        } else {
+            const int32_t f = b->n_fam++;
+            T.f = f;
+            T.filt_off = 0;
+            b->tab_kind[t] = DCR_FAM_PROCESSED;
+            b->tab_proc[t] = f;
+            b->fam_tid[f] = r0.tid;
+            b->fam_code[f] = code_off;
+            for (int k = 0; k < 4; ++k) {
+                b->fam_eqx[4 * f + k] = (uint16_t)eqx[k];
+                b->sub_off[4 * f + k + 1] = b->sub_off[4 * f + k] + cnt[k];
+                const int64_t tt = (std::max<int64_t>(mx[k] - mn[k], 1) + 15) & ~(int64_t)15;
+                b->ss_col_off[4 * f + k + 1] = b->ss_col_off[4 * f + k] + tt;
+            }
+            for (int j = 0; j < 2; ++j) {
+                const int a = 2 * j, c = 2 * j + 1;
+                int64_t tt = std::max(mx[a], mx[c]) - std::min(mn[a], mn[c]);
+                tt = (std::max<int64_t>(tt, 1) + 15) & ~(int64_t)15;
+                b->ds_col_off[2 * f + j + 1] = b->ds_col_off[2 * f + j] + tt;
+            }
+            b->n_reads = b->sub_off[4 * f + 4];
+            b->n_bases = bo;
+            b->n_cigar = co;
+            b->ss_cols = b->ss_col_off[4 * f + 4];
+            b->ds_cols = b->ds_col_off[2 * f + 2];
+            // writer metadata: RX of the read0 of A1 and of B1 (:1367 via add_tags)
+            for (int j = 0; j < 2; ++j) {
+                const Rec *r = first[2 * j];
+                if (!r) b->fam_rx[2 * f + j] = put_name("", 0);
+                else b->fam_rx[2 * f + j] = put_name(rx_of(*r), r->l_rx);
+            }
+            ++processed;
+        }
+        pend_recs.insert(pend_recs.end(), fam.begin(), fam.end());
+        tasks.push_back(std::move(T));
+        return 1;
+    }
+
     void flush_jobs() {
         if (jobs.empty()) return;
         const double tf = prof.on ? IngestProf::now() : 0;
@@ -1140,6 +1402,10 @@ struct dcr_ingest {
 
     int prefetch_records() {
         constexpr size_t kRQ = 16384;
+        // queued families may point into rq (the serial scan's records): drain
+        // them before rq is refilled; the scanner's records of a chunk stay
+        // put until need() gives the chunk back, which drains them itself
+        if (rqp == rq.data() && flush_tasks() < 0) return -1;
         materialize_family();
         if (rq.size() < kRQ) { rq.resize(kRQ); rq_off.resize(kRQ); }
         rq_pos = rq_n = 0;
@@ -1224,6 +1490,66 @@ struct dcr_ingest {
         return std::memcmp(code_of(a), code_of(b), a.l_code) == 0;
     }
 
+    // check_family_UMIs (:100-113), every RX is umi1 or its swapped halves,
+    // then check_family_rnames (:116-128), over the family's records fr[0, n)
+    // in window w.  Returns DCR_ERR_NONE or the error kind with its message.
+    int check_family(const Rec *const *fr, size_t n, const uint8_t *w, std::string &umi2, std::string &msg) const {
+        const Rec &r0 = *fr[0];
+        auto rx_at = [&](const Rec &r) { return r.l_rx <= sizeof r.rx ? r.rx : (const char *)(w + r.off + r.o_rx); };
+        auto code_at = [&](const Rec &r) { return r.l_code <= sizeof r.code ? r.code : (const char *)(w + r.off + r.o_mi); };
+        if (r0.rx_type != 'Z') { msg = "'int' object has no attribute 'split'"; return DCR_ERR_ATTRIBUTE; }
+        const char *umi1 = rx_at(r0);
+        const size_t l1 = r0.l_rx;
+        const char *d1p = (const char *)std::memchr(umi1, '-', l1);
+        if (!d1p) { msg = "list index out of range"; return DCR_ERR_INDEX; }
+        const size_t d1 = (size_t)(d1p - umi1);
+        const char *d2p = (const char *)std::memchr(umi1 + d1 + 1, '-', l1 - d1 - 1);
+        const size_t e2 = d2p ? (size_t)(d2p - umi1) : l1;
+        umi2.assign(umi1 + d1 + 1, e2 - d1 - 1);
+        umi2 += '-';
+        umi2.append(umi1, d1);
+        // both forms zero-padded to the inline width: four-word compares
+        constexpr size_t kRx = sizeof(Rec::rx);
+        const bool inl = l1 <= kRx;
+        uint64_t w1[kRx / 8] = {0}, w2[kRx / 8] = {0};
+        if (inl) {
+            std::memcpy(w1, umi1, l1);
+            std::memcpy(w2, umi2.data(), umi2.size());   // same length as umi1
+        }
+        auto same = [&](const Rec *r, const uint64_t *wv) {
+            uint64_t x[kRx / 8];
+            std::memcpy(x, r->rx, kRx);
+            return ((x[0] ^ wv[0]) | (x[1] ^ wv[1]) | (x[2] ^ wv[2]) | (x[3] ^ wv[3])) == 0;
+        };
+        for (size_t i = 0; i < n; ++i) {
+            const Rec *r = fr[i];
+            if (r->rx_type != 'Z') { msg = "RX tag is not a string"; return DCR_ERR_ATTRIBUTE; }
+            const char *x = rx_at(*r);
+            bool eq1, eq2;
+            if (inl && r->l_rx == l1) {
+                eq1 = same(r, w1);
+                eq2 = !eq1 && l1 == umi2.size() && same(r, w2);
+            } else {
+                eq1 = r->l_rx == l1 && std::memcmp(x, umi1, l1) == 0;
+                eq2 = !eq1 && r->l_rx == umi2.size() && std::memcmp(x, umi2.data(), r->l_rx) == 0;
+            }
+            if (!eq1 && !eq2) {
+                msg = "ERROR: family " + std::string(code_at(r0), r0.l_code) +
+                      " has different UMI tags. \n Please check output file of previous step of the pipeline "
+                      "(fgbio GroupReadsByUmi)";
+                return DCR_ERR_EXIT;
+            }
+        }
+        for (size_t i = 1; i < n; ++i)
+            if (fr[i]->tid != r0.tid) {
+                msg = "ERROR: family " + std::string(code_at(r0), r0.l_code) +
+                      " has difference rnames (e.g. chromosome numbers). \n Please check output file of previous "
+                      "step of the pipeline (fgbio GroupReadsByUmi)";
+                return DCR_ERR_EXIT;
+            }
+        return DCR_ERR_NONE;
+    }
+
     std::vector<const Rec *> sub[4];
 
     // preprocess_family up to the read loop (:1248-1264), then pack or file
@@ -1248,54 +1574,11 @@ struct dcr_ingest {
                 return fail_capacity("one family exceeds the batch capacities");
             return 0;
         }
-        // check_family_UMIs (:100-113): every RX is umi1 or its swapped halves
-        if (r0.rx_type != 'Z') return stop(DCR_ERR_ATTRIBUTE, "'int' object has no attribute 'split'");
-        const char *umi1 = rx_of(r0);
-        const size_t l1 = r0.l_rx;
-        const char *d1p = (const char *)std::memchr(umi1, '-', l1);
-        if (!d1p) return stop(DCR_ERR_INDEX, "list index out of range");
-        const size_t d1 = (size_t)(d1p - umi1);
-        const char *d2p = (const char *)std::memchr(umi1 + d1 + 1, '-', l1 - d1 - 1);
-        const size_t e2 = d2p ? (size_t)(d2p - umi1) : l1;
-        umi2_.assign(umi1 + d1 + 1, e2 - d1 - 1);
-        umi2_ += '-';
-        umi2_.append(umi1, d1);
-        // both forms zero-padded to the inline width: four-word compares
-        constexpr size_t kRx = sizeof(Rec::rx);
-        const bool inl = l1 <= kRx;
-        uint64_t w1[kRx / 8] = {0}, w2[kRx / 8] = {0};
-        if (inl) {
-            std::memcpy(w1, umi1, l1);
-            std::memcpy(w2, umi2_.data(), umi2_.size());   // same length as umi1
+        {
+            std::string msg;
+            const int kind = check_family(fam.data(), fam.size(), wb, umi2_, msg);
+            if (kind != DCR_ERR_NONE) return stop(kind, msg);
         }
-        auto same = [&](const Rec *r, const uint64_t *w) {
-            uint64_t x[kRx / 8];
-            std::memcpy(x, r->rx, kRx);
-            return ((x[0] ^ w[0]) | (x[1] ^ w[1]) | (x[2] ^ w[2]) | (x[3] ^ w[3])) == 0;
-        };
-        for (const Rec *r : fam) {
-            if (r->rx_type != 'Z') return stop(DCR_ERR_ATTRIBUTE, "RX tag is not a string");
-            const char *x = rx_of(*r);
-            bool eq1, eq2;
-            if (inl && r->l_rx == l1) {
-                eq1 = same(r, w1);
-                eq2 = !eq1 && l1 == umi2_.size() && same(r, w2);
-            } else {
-                eq1 = r->l_rx == l1 && std::memcmp(x, umi1, l1) == 0;
-                eq2 = !eq1 && r->l_rx == umi2_.size() && std::memcmp(x, umi2_.data(), r->l_rx) == 0;
-            }
-            if (!eq1 && !eq2)
-                return stop(DCR_ERR_EXIT, "ERROR: family " + std::string(code, l_code) +
-                                              " has different UMI tags. \n Please check output file of previous "
-                                              "step of the pipeline (fgbio GroupReadsByUmi)");
-        }
-        // check_family_rnames (:116-128)
-        for (size_t i = 1; i < fam.size(); ++i)
-            if (fam[i]->tid != r0.tid)
-                return stop(DCR_ERR_EXIT, "ERROR: family " + std::string(code, l_code) +
-                                              " has difference rnames (e.g. chromosome numbers). \n Please check "
-                                              "output file of previous step of the pipeline (fgbio "
-                                              "GroupReadsByUmi)");
         // split_family (:132-154), the subfamily of each read from parse_at
         for (auto &sv : sub) sv.clear();
         for (const Rec *r : fam)
@@ -1426,12 +1709,17 @@ struct dcr_ingest {
         b->ds_col_off[0] = 0;
         cap_err = 0;
         if (jobs.capacity() < (size_t)b->cap_reads) jobs.reserve((size_t)b->cap_reads);
+        // the queued families never reallocate under the packer (queue_family
+        // drains them first when they would)
+        if (tasks.capacity() < (size_t)b->cap_tab) tasks.reserve((size_t)b->cap_tab);
+        if (pend_recs.capacity() < (size_t)b->cap_reads) pend_recs.reserve((size_t)b->cap_reads);
         if (errored || finished) {
             b->end_kind = errored ? DCR_END_ERROR : DCR_END_EOF;
             return fail(DCR_IO_EARG, "the input has already ended");
         }
         const double tw = prof.on ? IngestProf::now() : 0;
         int rc = walk();
+        if (flush_tasks() < 0 && rc >= 0) rc = -1;
         flush_jobs();
         if (prof.on) prof.walk_total += IngestProf::now() - tw;
         hb = nullptr;
@@ -1452,7 +1740,7 @@ struct dcr_ingest {
                     // end of input: the last family (:1610-1631)
                     if (!started && !mid_end) return stop(DCR_ERR_TYPE, "'NoneType' object is not subscriptable");
                     if (!fam.empty()) {
-                        const int c = complete_family();
+                        const int c = queue_family();
                         if (c <= 0) return c;
                         fam.clear();
                     }
@@ -1462,6 +1750,9 @@ struct dcr_ingest {
                 }
             }
             const Rec &r = rqp[rq_pos];
+            // a record that stops the reference comes after every queued
+            // family: their checks first
+            if ((r.perr || r.pf < 0 || (r.pf > 0 && r.mi_type != 'Z')) && flush_tasks() < 0) return -1;
             if (r.perr) { g_err = kParseErr[r.perr]; return -1; }
             if (r.pf < 0) return stop(kFilterMsg[r.fmsg].kind, kFilterMsg[r.fmsg].msg);
             if (r.pf == 0) {
@@ -1480,9 +1771,12 @@ struct dcr_ingest {
             }
             if (r.mi_type != 'Z') return stop(DCR_ERR_ATTRIBUTE, "'int' object has no attribute 'split'");
             if (!fam.empty() && !same_code(r, *fam.front())) {
-                const int c = complete_family();
+                const double tc = prof.on ? IngestProf::now() : 0;
+                const int c = queue_family();
+                if (prof.on) prof.complete += IngestProf::now() - tc;
                 if (c <= 0) return c;      // 0: batch full, the read stays unconsumed
                 fam.clear();
+                kick_tasks(false);
                 kick_jobs(false);
             }
             ++passed;

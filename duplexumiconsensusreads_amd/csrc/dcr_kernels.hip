@@ -1458,7 +1458,12 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
     auto stage_window = [&](bool on, int64_t seq_start, int is0) {
         if (!on) return;
         const int64_t o = seq_start + is0 - base_al;      // >= 0: base_al is the first read's byte
-        const int64_t left = (DUPLEX ? a.in.ss_cols : a.in.n_bases) - base_al;
+        // the range in whole dwords: a buffer load returns 0 for a dword that
+        // reaches past it, which would zero the last bases of the batch's last
+        // read (the arrays are padded to 256 bytes, so the rounded-up dword is
+        // ours to read)
+        const int64_t total = DUPLEX ? a.in.ss_cols : a.in.n_bases;
+        const int64_t left = ((total + 3) & ~(int64_t)3) - base_al;
         const int nrec = (int)min(left, (int64_t)0x7FFFFFF0);
         const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void *)(gb + base_al), (short)0, nrec,
                                                                             0x00020000);

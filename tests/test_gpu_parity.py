@@ -256,3 +256,40 @@ def test_gpu_deep_records_edge_bytes(ctx, seed, minbq, rate):
     finally:
         ctx.set_params(ConsensusParams())
 
+
+
+@pytest.mark.parametrize("tail", [0, 1, 2, 3])
+def test_gpu_insertion_layout_batch_end_tail(ctx, tail):
+    """The batch's last record has an insertion layout whose bytes do not fit
+    the stage, so its reads' next 32 bases are staged by range-checked dword
+    loads; the batch's bases end `tail` bytes into a dword.  A buffer load
+    returns 0 for a dword that reaches past its range, which had zeroed the
+    last read's final bases (one column's depth off by one in the C3 shard,
+    tools/c3shard_diff.py).  Every tail against the oracle."""
+    from types import SimpleNamespace as NS
+
+    from duplexumiconsensusreads_amd.batch import pack_families
+    rng = np.random.default_rng(7 + tail)
+
+    def read(L, cig, pos=100):
+        seq = "".join("ACGT"[i] for i in rng.integers(0, 4, L))
+        return NS(reference_start=pos, mapping_quality=40, query_sequence=seq,
+                  query_qualities=[int(q) for q in rng.choice([37, 37, 37, 25], L)], cigartuples=cig)
+    # subfamily 3 (the batch's last reads): 30 reads sharing one template, one
+    # with an insertion, the last read's length setting the tail
+    tmpl = "".join("ACGT"[i] for i in rng.integers(0, 4, 160))
+    sub3 = []
+    for j in range(30):
+        L = 151 if j < 29 else 152 + tail            # 32 reads of 151 bases before it
+        r = read(L, [(0, L)])
+        r.query_sequence = tmpl[:L]
+        sub3.append(r)
+    sub3[7].cigartuples = [(0, 100), (1, 1), (0, 50)]
+    fam = [[read(151, [(0, 151)])], [read(151, [(0, 151)])], [read(151, [(0, 151)])], sub3]
+    packed = pack_families([fam])
+    assert packed.n_bases % 4 == tail
+    params = ConsensusParams()
+    ctx.set_params(params)
+    got = ctx.run_host(packed)
+    want = dcr_oracle_c.run(packed, params)
+    assert_same(packed, got, want)

@@ -65,7 +65,7 @@ def main():
         print("  first differing byte", k, flush=True)
         # the record holding byte k: walk the block_size chain (after the header)
         import struct
-        hl = 12 + struct.unpack_from("<i", a, 8)[0]
+        hl = 12 + struct.unpack_from("<i", a, 4)[0]
         nref = struct.unpack_from("<i", a, hl - 4)[0]
         p = hl
         for _ in range(nref):
@@ -85,9 +85,32 @@ def main():
             if ra != rb:
                 print("  record", n, flush=True)
                 for key in sorted(set(ra) | set(rb)):
-                    if ra.get(key) != rb.get(key):
+                    if ra.get(key) == rb.get(key):
+                        continue
+                    if key == "tags":
+                        for ta, tb in zip(ra[key], rb[key]):
+                            if ta == tb:
+                                continue
+                            print(f"    tag {ta[0]} / {tb[0]} type {ta[1]} / {tb[1]}", flush=True)
+                            va, vb = ta[2], tb[2]
+                            if isinstance(va, str) and va.startswith("["):
+                                va, vb = eval(va), eval(vb)   # noqa: S307 - our own list tags
+                            if isinstance(va, (list, str)) and isinstance(vb, (list, str)):
+                                ks = [i for i in range(min(len(va), len(vb))) if va[i] != vb[i]]
+                                print(f"      lengths {len(va)} / {len(vb)}, {len(ks)} differ, first at {ks[:10]}",
+                                      flush=True)
+                                for i in ks[:5]:
+                                    print(f"      [{i}] gpu {va[max(0, i - 3):i + 4]} cpu {vb[max(0, i - 3):i + 4]}",
+                                          flush=True)
+                            else:
+                                print(f"      gpu {str(va)[:200]} cpu {str(vb)[:200]}", flush=True)
+                    else:
                         print(f"    {key}: gpu={str(ra.get(key))[:300]}", flush=True)
                         print(f"    {key}: cpu={str(rb.get(key))[:300]}", flush=True)
+                print(f"    gpu record: pos {ra.get('reference_start', ra.get('pos'))} "
+                      f"seq {str(ra.get('query_sequence', ra.get('seq')))[:200]}", flush=True)
+                print(f"    cpu record: pos {rb.get('reference_start', rb.get('pos'))} "
+                      f"seq {str(rb.get('query_sequence', rb.get('seq')))[:200]}", flush=True)
                 break
             n += 1
     sys.exit(1 if bad else 0)
