@@ -975,8 +975,19 @@ struct dcr_ingest {
     int need(size_t n) {
         while (wend - wpos < n) {
             if (data_eof) return 0;
-            if (flush_tasks() < 0) return -1;       // the tasks and jobs point into the current window
-            flush_jobs();
+            // queued families point into this window: a chunk window is
+            // retired (given back once they have run, release_retired); a
+            // window of the leftover buffers waits for them here
+            {
+                const size_t keep0 = fam.empty() ? wpos : std::min(wpos, fam.front()->off);
+                if (!cur || wend - keep0 > Inflater::kHead) {
+                    if (flush_tasks() < 0) return -1;
+                } else {
+                    kick_tasks(true);
+                    release_retired();
+                }
+            }
+            flush_jobs();                           // the pack jobs point into it too
             const double tw = prof.on ? IngestProf::now() : 0;
             Chunk *nx = infl->next();
             if (prof.on) prof.wait_chunk += IngestProf::now() - tw;
@@ -1006,7 +1017,10 @@ struct dcr_ingest {
             wpos = wpos - keep + base;
             wend = base + left + nx->len;
             wb = nbuf;
-            if (cur) infl->give_back(cur);
+            if (cur) {
+                if (tasks.size() > tk_done_seen()) retired.push_back(Retired{cur, tasks.size()});
+                else infl->give_back(cur);
+            }
             ci = 0;
             if (nbuf == nx->data()) cur = nx;       // the chunk's record offsets hold in the window
             else { cur = nullptr; infl->give_back(nx); }
@@ -1050,7 +1064,7 @@ struct dcr_ingest {
                     w = pk_w;
                     b = pk_b;
                 }
-                if (t1 > t0) run_tasks(w, b, t0, t1);
+                if (t1 > t0) run_tasks(b, t0, t1);
                 if (j1 > j0) pack_range(w, b, jobs.data(), j0, j1);
                 {
                     std::lock_guard<std::mutex> g(pk_mu);
@@ -1094,6 +1108,7 @@ struct dcr_ingest {
     // order) that fails truncates the batch to its reservation and stops
     // there, exactly where complete_family would have stopped.
     struct FamTask {
+        const uint8_t *w;               // the window its records' offsets refer to
         uint32_t rb, n;                 // the family's records: pend_recs[rb, rb + n)
         int32_t t, f;                   // table entry; processed family (-1: filtered)
         int64_t read_base, base_off[4], cig_off[4];   // per subfamily (split order)
@@ -1107,6 +1122,23 @@ struct dcr_ingest {
     };
     std::vector<FamTask> tasks;
     std::vector<const Rec *> pend_recs;
+    std::deque<Rec> task_recs;           // copies of queued records that lived in fam_store
+    // chunks whose window queued tasks still read: given back once tasks
+    // [0, upto) have run
+    struct Retired { Chunk *c; size_t upto; };
+    std::deque<Retired> retired;
+    size_t tk_done_seen() {
+        std::lock_guard<std::mutex> g(pk_mu);
+        return tk_done;
+    }
+    void release_retired() {
+        if (retired.empty()) return;
+        const size_t done = tk_done_seen();
+        while (!retired.empty() && retired.front().upto <= done) {
+            infl->give_back(retired.front().c);
+            retired.pop_front();
+        }
+    }
     size_t tk_sub = 0, tk_done = 0;      // tasks [0, tk_sub) handed over, [0, tk_done) run
     static constexpr size_t kTkStep = 256;
 
@@ -1156,11 +1188,11 @@ struct dcr_ingest {
             co[k] += n_cig;
         }
     }
-    void run_tasks(const uint8_t *w, dcr_host_batch *b, size_t t0, size_t t1) {
+    void run_tasks(dcr_host_batch *b, size_t t0, size_t t1) {
         const size_t chunk = 32;
         pool->run((t1 - t0 + chunk - 1) / chunk, [&](size_t c) {
             const size_t te = std::min(t1, t0 + (c + 1) * chunk);
-            for (size_t t = t0 + c * chunk; t < te; ++t) run_task(tasks[t], w, b);
+            for (size_t t = t0 + c * chunk; t < te; ++t) run_task(tasks[t], tasks[t].w, b);
             return true;
         });
     }
@@ -1184,6 +1216,8 @@ struct dcr_ingest {
             pk_cv.wait(lk, [&] { return tk_done == tk_sub; });
             tk_sub = tk_done = 0;
         }
+        for (const Retired &r : retired) infl->give_back(r.c);
+        retired.clear();
         int rc = 1;
         for (FamTask &T : tasks) {
             if (T.err_kind == DCR_ERR_NONE) continue;
@@ -1208,6 +1242,7 @@ struct dcr_ingest {
         }
         tasks.clear();
         pend_recs.clear();
+        task_recs.clear();
         return rc;
     }
 
@@ -1332,8 +1367,20 @@ struct dcr_ingest {
             }
             ++processed;
         }
-        pend_recs.insert(pend_recs.end(), fam.begin(), fam.end());
+        T.w = wb;
+        // records materialized into fam_store move with the next window
+        // (need() rewrites their offsets): the task keeps copies
+        const Rec *fs0 = fam_store.data(), *fs1 = fs0 + fam_store.size();
+        for (const Rec *r : fam) {
+            if (r >= fs0 && r < fs1) {
+                task_recs.push_back(*r);
+                pend_recs.push_back(&task_recs.back());
+            } else {
+                pend_recs.push_back(r);
+            }
+        }
         tasks.push_back(std::move(T));
+        if (tasks.size() - tk_sub >= kTkStep) release_retired();
         return 1;
     }
 

@@ -275,3 +275,32 @@ def test_state_gate_error_ends_ingest(c1_bam):
                 break
     assert isinstance(ing.gate_error, RuntimeError)
     ing.close()
+
+
+def test_ingest_many_chunks_reproduces_the_source_batch(tmp_path):
+    """A BAM of ~3.2 M reads (a dozen 32 MiB inflate chunks, so families
+    straddle chunk windows and the serial-scan buffer) read back through the
+    native ingest in 512 k-read batches: the packed reads of every batch,
+    concatenated, are exactly the batch the BAM was written from.  Families
+    are completed on the packer thread while the walk moves on, and the
+    chunk windows their records point into are retired only after them."""
+    src = synth.packed_fixed_size(100_000, seed=9)
+    path = str(tmp_path / "many.bam")
+    synth.write_packed_bam(path, src, seed=9, level=1)
+    ing = native_io.Ingest(path, 20, 1, 100, 20, 4)
+    got = {k: [] for k in ("read_pos", "seq_len", "cig_n", "bases", "quals")}
+    n_fam = 0
+    while True:
+        hb = native_io.HostBatch(reads=1 << 19)
+        ing.next(hb)
+        pk = hb.packed()
+        n_fam += pk.n_fam
+        for k in got:
+            got[k].append(getattr(pk, k).copy())
+        if hb.end_kind != native_io.END_FULL:
+            assert hb.end_kind == native_io.END_EOF
+            break
+    ing.close()
+    assert n_fam == src.n_fam
+    for k, v in got.items():
+        assert np.array_equal(np.concatenate(v), getattr(src, k)), k
