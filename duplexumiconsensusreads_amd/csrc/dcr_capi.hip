@@ -341,7 +341,7 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     const size_t o_ins = o;  o = align_up(o + (size_t)std::max<int64_t>(s->ss_cols, 1));
     const size_t o_st = o;   o = align_up(o + sizeof(int4) * (size_t)std::max<int64_t>(s->n_reads, 1));
     const size_t o_err = o;  o = align_up(o + 64);
-    const size_t o_stamp = o; o = align_up(o + 32 * sizeof(unsigned long long));
+    const size_t o_stamp = o; o = align_up(o + 64 * sizeof(unsigned long long));
     const size_t n_rec = (size_t)std::max<int64_t>(4LL * s->n_fam, 1);
     const size_t o_ovf = o;  o = align_up(o + sizeof(int) * n_rec);
     const size_t o_xl = o;   o = align_up(o + sizeof(int) * n_rec);
@@ -540,11 +540,11 @@ int dcr_last_timing(dcr_ctx *c, float *ms4) {
 
 // diagnostic (not in include/dcr.h): phase cycle counters of DCR_STAMP builds
 int dcr_debug_stamps(dcr_ctx *c, unsigned long long *out, int n, int reset) {
-    if (!c || !out || n > 32) return fail(DCR_EARG, "bad argument");
+    if (!c || !out || n > 64) return fail(DCR_EARG, "bad argument");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipMemcpy(out, c->w.stamps, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
-    if (reset) HIP_TRY(hipMemset(c->w.stamps, 0, sizeof(unsigned long long) * 32));
+    if (reset) HIP_TRY(hipMemset(c->w.stamps, 0, sizeof(unsigned long long) * 64));
     return DCR_OK;
 }
 

@@ -3428,7 +3428,8 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
     }
     if (!EXACT && npend) flush(lane0);
     if (DCR_STAMP && lane0 == 0)
-        for (int k = 0; k < 10; ++k) atomicAdd(&a.stamps[k + (DUPLEX ? 16 : 0)], (unsigned long long)sp.acc[k]);
+        for (int k = 0; k < 10; ++k)   // fast ss 0-9, ds 16-25; exact ss 32-41, ds 48-57
+            atomicAdd(&a.stamps[k + (DUPLEX ? 16 : 0) + (EXACT ? 32 : 0)], (unsigned long long)sp.acc[k]);
 }
 
 // persistent: drains the general list written by k_recmeta.  A wave takes

@@ -13,7 +13,9 @@ from duplexumiconsensusreads_amd.device import DeviceBatch  # noqa: E402
 from duplexumiconsensusreads_amd.params import ConsensusParams, build_dcr_params  # noqa: E402
 
 nfam, path = int(sys.argv[1]), sys.argv[2]
-packed = synth.packed_fixed_size(nfam, seed=3)
+cfg = os.environ.get("ABL_CONFIG", "C2")
+packed = (synth.packed_fixed_size(nfam, seed=3) if cfg == "C2"
+          else synth.packed_config(synth.CONFIGS[cfg], nfam, seed=3, max_reads=1000))
 db = DeviceBatch(packed)
 P = build_dcr_params(ConsensusParams())
 lib = ctypes.CDLL(path)
@@ -26,10 +28,10 @@ lib.dcr_sync.argtypes = [ctypes.c_void_p]
 lib.dcr_last_kernel_timing.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 lib.dcr_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
 ctx = lib.dcr_create(0, ctypes.byref(P))
-st = (ctypes.c_ulonglong * 32)()
+st = (ctypes.c_ulonglong * 64)()
 run = lambda: lib.dcr_run_batch(ctx, ctypes.byref(db.batch_struct), ctypes.byref(db.ss_struct), ctypes.byref(db.ds_struct))
 assert run() == 0 and lib.dcr_sync(ctx) in (0, 3)
-lib.dcr_debug_stamps(ctx, st, 32, 1)
+lib.dcr_debug_stamps(ctx, st, 64, 1)
 K = 3
 kt = [0.0] * 7
 for _ in range(K):
@@ -37,10 +39,11 @@ for _ in range(K):
     ms = (ctypes.c_float * 9)()
     lib.dcr_last_kernel_timing(ctx, ms)
     kt = [a + b for a, b in zip(kt, ms)]
-lib.dcr_debug_stamps(ctx, st, 32, 0)
+lib.dcr_debug_stamps(ctx, st, 64, 0)
 names = ["prefetch wait", "codes into LDS", "prefetch issue", "trim, fence", "products",
          "finalize", "depth reductions", "column stores", "mean", "record scalars"]
-for kind, base, nrec, kidx in (("single-strand", 0, 4 * nfam, 2), ("duplex", 16, 2 * nfam, 5)):
+for kind, base, nrec, kidx in (("single-strand fast", 0, 4 * nfam, 1), ("duplex fast", 16, 2 * nfam, 5),
+                               ("single-strand exact", 32, 4 * nfam, 2), ("duplex exact", 48, 2 * nfam, 6)):
     tot = sum(st[base + k] for k in range(10))
     print(f"{kind}: kernel {kt[kidx] / K:.3f} ms; cycles per record per wave (s_memtime ticks):")
     for k in range(10):
