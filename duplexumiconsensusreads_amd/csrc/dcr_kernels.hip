@@ -2819,7 +2819,7 @@ __device__ __forceinline__ double div1000(int k) {
 template <bool DUPLEX, int NT, bool EXACT>
 __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &m, const Staged &sg, uint8_t *lds,
                                               const int stage_addr, const int ov_addr, const int rm_addr, const int lane,
-                                              Stamps &sp, const double2 *xt, const uint32_t *r1) {
+                                              Stamps &sp, const double2 *xt, const uint32_t *r1, const double *qt) {
     const int64_t rec = m.rec;
     const int64_t off = m.off;
     const int R = (int)(m.w & 127u);
@@ -2929,85 +2929,97 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     uint16_t *chq = (uint16_t *)(lds + rm_addr);
     if (exact) {
         const dcr_params *P = lds_ptr<const dcr_params>(lds, fk::kPParams);
-        const double *qthr = P->qthresh;
+        const double *qthr = EXACT ? qt : P->qthresh;     // EXACT: LDS copy of the quality table
         bool fail = false;             // '+' / '-' call or int(-inf) quality: general kernel
-#pragma unroll 1
-        for (int tt = 0; tt < NT; ++tt) {
-            const bool mine = (und >> tt) & 1u;
-            if (__ballot(mine) == 0) continue;
-            const int t = 64 * tt + lane;
-            Posterior po;
-            uint32_t cnt = 0;          // 8-bit row counts of A T C G
-            if (!DUPLEX && R == 1) {
-                // one read: the column's posterior is a function of its row
-                // (class after the mask, raw quality), tabulated per block in
-                // the kernel's prologue by this loop's products and posterior()
-                const int cr = readlane(crv, 0);
-                const int x = readlane((int)rm.x, 0);
-                const int col = x & 255, len = (x >> 8) & 255;
+        // the lane's column results: posterior and 8-bit row counts of A T C G
+        Posterior po[NT];
+        uint32_t cnt[NT];
+        uint32_t tiles = 0;                               // tiles holding an undecided column (uniform)
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) tiles |= (uint32_t)(__ballot((und >> tt) & 1u) != 0) << tt;
+        if (!DUPLEX && R == 1) {
+            // one read: the column's posterior is a function of its row
+            // (class after the mask, raw quality), tabulated per block in
+            // the kernel's prologue by the products below and posterior()
+            const int cr = readlane(crv, 0);
+            const int x = readlane((int)rm.x, 0);
+            const int col = x & 255, len = (x >> 8) & 255;
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) {
+                if (!((tiles >> tt) & 1u)) continue;
+                const int t = 64 * tt + lane;
                 const uint32_t ad = (uint32_t)(t - col) < (uint32_t)len ? (uint32_t)(cr + 2 * t) : (uint32_t)fk::kSent;
                 const uint32_t code = *(const uint16_t *)(lds + ad);
                 const uint32_t kc = code >> 11;
                 const uint32_t q = ((code >> 4) & 127u) - kc;
-                const uint32_t k = (*(const uint32_t *)(lds + code + 8) & 63u) ? 0u : kc;
+                const uint32_t k = (kc == 0 || (int)q < a.minbq) ? 0u : kc;   // as the table's rows
                 const uint32_t te = r1[k * 128u + q];
-                po.ch = (int)(te & 255u);
-                po.q = (int)((te >> 8) & 1023u) - 1;
-                po.best = (int)((te >> 18) & 7u);
-                po.masked = (te >> 21) & 1u;
-                po.overflow = (te >> 22) & 1u;
-                cnt = k ? 1u << (8 * (k - 1)) : 0u;
-            } else {
-            double L4[4] = {1.0, 1.0, 1.0, 1.0};
-            double U = 1.0;
-            // read r's row at the lane's column: class after the mask (the
-            // table's 'N' rows: class N, or quality below min_base_quality,
-            // :280) and the factors (1 - p', p'/5) of its raw quality
-            auto fetch = [&](int r, uint32_t &k, double2 &f) {
+                po[tt].ch = (int)(te & 255u);
+                po[tt].q = (int)((te >> 8) & 1023u) - 1;
+                po[tt].best = (int)((te >> 18) & 7u);
+                po[tt].masked = (te >> 21) & 1u;
+                po[tt].overflow = (te >> 22) & 1u;
+                cnt[tt] = k ? 1u << (8 * (k - 1)) : 0u;
+            }
+        } else {
+            // the products in read order (:594-600), every tile at once: per
+            // read, its rows at the NT columns of the lane are independent
+            // loads (the tiles' chains overlap instead of running one tile
+            // after another)
+            double L4[NT][4], U[NT];
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) {
+                U[tt] = 1.0;
+                cnt[tt] = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) L4[tt][i] = 1.0;
+            }
+            for (int r = 0; r < R; ++r) {
                 const int cr = readlane(crv, r);
                 const int x = readlane((int)rm.x, r);
                 const int col = x & 255, len = (x >> 8) & 255;
-                const uint32_t ad = (uint32_t)(t - col) < (uint32_t)len ? (uint32_t)(cr + 2 * t) : (uint32_t)fk::kSent;
-                const uint32_t code = *(const uint16_t *)(lds + ad);
-                const uint32_t kc = code >> 11;                      // code bank: N 0, A 1, T 2, C 3, G 4
-                const uint32_t q = ((code >> 4) & 127u) - kc;        // raw quality (pad 'N': 2)
-                k = (kc == 0 || (int)q < a.minbq) ? 0u : kc;         // as the table's rows (k_consensus_fast prologue)
-                f = xt[q];                                           // LDS copy of P's rows
-            };
-            // the products in read order (:594-600)
-            auto apply = [&](uint32_t k, double2 f) {
-                U = U * f.y;
+                uint32_t k[NT];
+                double2 f[NT];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) L4[i] = L4[i] * (k == (uint32_t)(i + 1) ? f.x : f.y);
-                cnt += k ? 1u << (8 * (k - 1)) : 0u;
-            };
-            // two reads' loads in flight per step (their products stay in order)
-            int r = 0;
-            for (; r + 2 <= R; r += 2) {
-                uint32_t k0, k1;
-                double2 f0, f1;
-                fetch(r, k0, f0);
-                fetch(r + 1, k1, f1);
-                apply(k0, f0);
-                apply(k1, f1);
+                for (int tt = 0; tt < NT; ++tt) {
+                    if (!((tiles >> tt) & 1u)) continue;
+                    const int t = 64 * tt + lane;
+                    const uint32_t ad = (uint32_t)(t - col) < (uint32_t)len ? (uint32_t)(cr + 2 * t) : (uint32_t)fk::kSent;
+                    const uint32_t code = *(const uint16_t *)(lds + ad);
+                    const uint32_t kc = code >> 11;                  // code bank: N 0, A 1, T 2, C 3, G 4
+                    const uint32_t q = ((code >> 4) & 127u) - kc;    // raw quality (pad 'N': 2)
+                    // class after the mask: the table's 'N' rows are class N
+                    // or a quality below min_base_quality (:280)
+                    k[tt] = (kc == 0 || (int)q < a.minbq) ? 0u : kc;
+                    f[tt] = xt[q];                                   // (1 - p', p'/5), LDS copy of P's rows
+                }
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt) {
+                    if (!((tiles >> tt) & 1u)) continue;
+                    U[tt] = U[tt] * f[tt].y;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) L4[tt][i] = L4[tt][i] * (k[tt] == (uint32_t)(i + 1) ? f[tt].x : f[tt].y);
+                    cnt[tt] += k[tt] ? 1u << (8 * (k[tt] - 1)) : 0u;
+                }
             }
-            if (r < R) {
-                uint32_t k0;
-                double2 f0;
-                fetch(r, k0, f0);
-                apply(k0, f0);
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) {
+                if (!((tiles >> tt) & 1u)) continue;
+                const double L[6] = {L4[tt][0], L4[tt][1], L4[tt][2], L4[tt][3], U[tt], U[tt]};
+                po[tt] = posterior(L, false, P, qthr, true);
             }
-            const double L[6] = {L4[0], L4[1], L4[2], L4[3], U, U};
-            po = posterior(L, false, P, qthr, true);
-            }
-            if (mine) {
-                fail |= po.overflow || (!po.masked && po.best > 3);
+        }
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            const int t = 64 * tt + lane;
+            if ((und >> tt) & 1u) {
+                fail |= po[tt].overflow || (!po[tt].masked && po[tt].best > 3);
                 const uint32_t w = *(const uint16_t *)(ov + 2 * t);
                 const int d = (int)(w & 63u);
-                const int nb = po.best <= 3 ? (int)((cnt >> (8 * po.best)) & 255u) : 0;
-                const int e = po.masked ? d : R - nb;               // rows != the consensus character
+                const int nb = po[tt].best <= 3 ? (int)((cnt[tt] >> (8 * po[tt].best)) & 255u) : 0;
+                const int e = po[tt].masked ? d : R - nb;           // rows != the consensus character
                 *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6));
-                chq[t] = (uint16_t)((uint32_t)po.ch | ((uint32_t)po.q << 8));
+                chq[t] = (uint16_t)((uint32_t)po[tt].ch | ((uint32_t)po[tt].q << 8));
             }
         }
         lds_fence();
@@ -3249,7 +3261,7 @@ __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
 // columns in the reference's double arithmetic.  The common kernel thus keeps
 // none of the exact path's code or registers.
 template <bool DUPLEX, bool EXACT>
-__global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArgs a) {
+__global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : 5) void k_consensus_fast(FastArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[fk::kLdsBytes];
     // Record assignment, XCD-aware: the blocks of one group (blockIdx % 8,
     // the blocks that share an XCD and its L2) take one contiguous range of
@@ -3274,6 +3286,10 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
     }
     // EXACT: the likelihood factors of quality rows 0..127 (the exact columns'
     // per-read products read them once per row; the common kernel keeps none)
+    // EXACT: the quality table's boundaries (phred_from_table reads two per column)
+    __shared__ double s_qt[EXACT ? DCR_MAX_QTHRESH : 1];
+    if (EXACT)
+        for (int i = threadIdx.x; i < DCR_MAX_QTHRESH; i += fk::kBlockThreads) s_qt[i] = a.P->qthresh[i];
     __shared__ double2 s_xt[EXACT ? 128 : 1];
     if (EXACT)
         for (int i = threadIdx.x; i < 128; i += fk::kBlockThreads) s_xt[i] = make_double2(a.P->match[i], a.P->mismatch[i]);
@@ -3411,10 +3427,10 @@ __global__ __launch_bounds__(fk::kBlockThreads, 5) void k_consensus_fast(FastArg
             send_to_general<DUPLEX>(a, m0, sg.rm, lds, lane);
         } else if (sg.state == 0) {
             bool done;
-            if (sg.T <= 64) done = finish_record<DUPLEX, 1, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1);
-            else if (sg.T <= 128) done = finish_record<DUPLEX, 2, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1);
-            else if (sg.T <= 192) done = finish_record<DUPLEX, 3, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1);
-            else done = finish_record<DUPLEX, 4, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1);
+            if (sg.T <= 64) done = finish_record<DUPLEX, 1, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt);
+            else if (sg.T <= 128) done = finish_record<DUPLEX, 2, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt);
+            else if (sg.T <= 192) done = finish_record<DUPLEX, 3, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt);
+            else done = finish_record<DUPLEX, 4, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt);
             if (!EXACT && !done) {
                 if (lane == npend) pend = i;
                 if (++npend == kWave) flush(lane);
