@@ -426,6 +426,8 @@ class _Driver:
         ready = queue.Queue()
         stop = threading.Event()
 
+        first = [True]
+
         def ingest():
             try:
                 while not stop.is_set():
@@ -433,7 +435,27 @@ class _Driver:
                     if hb is None:
                         return
                     t0 = time.perf_counter()
-                    self.ing.next(hb)
+                    if first[0] and hb.s.cap_reads >= (1 << 18):
+                        # the first batch at an eighth of the capacities: the
+                        # device starts on it while the rest of the pipeline
+                        # fills (batch boundaries never change the outputs); a
+                        # family too large for it takes the full batch
+                        first[0] = False
+                        caps = (hb.s.cap_fam, hb.s.cap_tab, hb.s.cap_reads, hb.s.cap_cigar, hb.s.cap_bases)
+                        hb.s.cap_fam, hb.s.cap_tab = caps[0] // 8, caps[1] // 8
+                        hb.s.cap_reads, hb.s.cap_cigar, hb.s.cap_bases = caps[2] // 8, caps[3] // 8, caps[4] // 8
+                        try:
+                            self.ing.next(hb)
+                        except native_io.IOError_ as e:
+                            if "exceeds the batch capacities" not in str(e):
+                                raise
+                            (hb.s.cap_fam, hb.s.cap_tab, hb.s.cap_reads, hb.s.cap_cigar, hb.s.cap_bases) = caps
+                            self.ing.next(hb)
+                        finally:
+                            (hb.s.cap_fam, hb.s.cap_tab, hb.s.cap_reads, hb.s.cap_cigar, hb.s.cap_bases) = caps
+                    else:
+                        first[0] = False
+                        self.ing.next(hb)
                     t1 = time.perf_counter()
                     self.stats["ingest_s"] += t1 - t0
                     if self.trace is not None:

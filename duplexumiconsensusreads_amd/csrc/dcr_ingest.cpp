@@ -405,6 +405,73 @@ struct Chunk {
     std::vector<Rec> recs;          // boundary in this chunk and ending in it (off from buf start)
 };
 
+// Record-index vectors of released chunks, kept for the next ingest of the
+// process (as HugeCache keeps the chunk buffers): freeing four ~13 MB vectors
+// per ingest unmapped their pages inside every CLI pass (~18 ms of a close)
+class RecsCache {
+  public:
+    static RecsCache &get() {
+        static RecsCache c;
+        return c;
+    }
+    std::vector<Rec> take() {
+        std::lock_guard<std::mutex> g(mu_);
+        if (spare_.empty()) return {};
+        std::vector<Rec> v = std::move(spare_.back());
+        spare_.pop_back();
+        return v;
+    }
+    void give(std::vector<Rec> &&v) {
+        std::lock_guard<std::mutex> g(mu_);
+        if (spare_.size() >= 16 || v.capacity() == 0) return;
+        v.clear();                          // keeps the capacity
+        spare_.push_back(std::move(v));
+    }
+
+  private:
+    std::mutex mu_;
+    std::vector<std::vector<Rec>> spare_;
+};
+
+// Thread pools of closed ingests, kept for the next ones of the process: a
+// pool's threads are joined when it is destroyed, and on a loaded machine
+// their wake-ups made an ingest's close take 6-14 ms per pool (measured; the
+// CLI closes an ingest per pass).  A pool is handed to one ingest at a time.
+class PoolCache {
+  public:
+    static PoolCache &get() {
+        static PoolCache *c = new PoolCache;     // never destroyed: its threads end with the process
+        return *c;
+    }
+    std::unique_ptr<Pool> take(int n) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            for (size_t i = 0; i < spare_.size(); ++i)
+                if (spare_[i]->size() == std::max(1, n)) {
+                    std::unique_ptr<Pool> p = std::move(spare_[i]);
+                    spare_.erase(spare_.begin() + (long)i);
+                    return p;
+                }
+        }
+        return std::unique_ptr<Pool>(new Pool(n));
+    }
+    void give(std::unique_ptr<Pool> p) {
+        if (!p) return;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            if (spare_.size() < 16) {
+                spare_.push_back(std::move(p));
+                return;
+            }
+        }
+        p.reset();                                // more than enough kept: this one joins its threads
+    }
+
+  private:
+    std::mutex mu_;
+    std::vector<std::unique_ptr<Pool>> spare_;
+};
+
 // the GPU inflate hook (dcr_io_set_inflate_hook), copied by each Inflater
 std::mutex g_hook_mu;
 dcr_inflate_hook g_hook{};
@@ -428,9 +495,11 @@ class Inflater {
     // stop end_uoff bytes into the data of the block at end_coff
     Inflater(FILE *f, int n_threads, const RecParser &rp, bool ranged = false, uint64_t start_coff = 0,
              uint32_t start_uoff = 0, int64_t end_coff = -1, uint32_t end_uoff = 0, bool host_only = false)
-        : f_(f), pool_(env_threads("DCR_INFLATE_THREADS", n_threads)),
-          spool_(env_threads("DCR_SCAN_THREADS", std::max(1, n_threads / 2))), rp_(rp), end_coff_(end_coff),
+        : f_(f), pool_(PoolCache::get().take(env_threads("DCR_INFLATE_THREADS", n_threads))),
+          spool_(PoolCache::get().take(env_threads("DCR_SCAN_THREADS", std::max(1, n_threads / 2)))), rp_(rp),
+          end_coff_(end_coff),
           end_uoff_(end_uoff) {
+        for (auto &c : chunks_) c.recs = RecsCache::get().take();
         if (ranged) {
             st_ = kRec;
             skip_ = start_uoff;
@@ -498,12 +567,26 @@ class Inflater {
         stop_members_ = true;
         if (mth_.joinable()) mth_.join();
         if (stream_) hook_.stream_close(stream_);          // before the mapping it reads goes away
-        if (map_) munmap((void *)map_, map_len_);
+        // unmapping a whole input (page-table teardown, ~25 ms per 0.5 GB)
+        // need not hold up the caller: a detached thread does it, 16 MiB at
+        // a time, so it never holds the address-space lock for long (frees
+        // and the next open's mmap would otherwise wait for all of it)
+        if (map_) {
+            uint8_t *p = (uint8_t *)map_;
+            const size_t len = map_len_;
+            std::thread([p, len] {
+                constexpr size_t kSlice = (size_t)16 << 20;
+                for (size_t o = 0; o < len; o += kSlice) munmap(p + o, std::min(kSlice, len - o));
+            }).detach();
+        }
         if (hook_.host_free) {
             for (auto &c : chunks_)
                 if (c.pin) hook_.host_free(hook_.user, c.pin);
             if (stage_pin_) hook_.host_free(hook_.user, stage_pin_);
         }
+        for (auto &c : chunks_) RecsCache::get().give(std::move(c.recs));
+        PoolCache::get().give(std::move(pool_));
+        PoolCache::get().give(std::move(spool_));
     }
     bool gpu() const { return gpu_; }
 
@@ -702,7 +785,7 @@ class Inflater {
         c.recs.resize(offs_.size());
         const uint8_t *base = c.data();
         const size_t chunk = 512;
-        spool_.run((offs_.size() + chunk - 1) / chunk, [&](size_t k) {
+        spool_->run((offs_.size() + chunk - 1) / chunk, [&](size_t k) {
             const size_t e = std::min(offs_.size(), (k + 1) * chunk);
             for (size_t i = k * chunk; i < e; ++i)
                 c.recs[i].perr = (uint8_t)rp_.parse_at(base, kHead + offs_[i], c.recs[i]);
@@ -815,7 +898,7 @@ class Inflater {
             uint8_t *stage = stage_pin_ ? stage_pin_ : stage_.data();
             if (nb > stage_cap_) { c.err = "BGZF chunk larger than its staging buffer"; return; }
             const size_t piece = (size_t)1 << 20;
-            pool_.run((nb + piece - 1) / piece, [&](size_t q) {
+            pool_->run((nb + piece - 1) / piece, [&](size_t q) {
                 const size_t a = q * piece, m = std::min(piece, nb - a);
                 std::memcpy(stage + a, src + g0 + a, m);
                 return true;
@@ -835,7 +918,7 @@ class Inflater {
                 t_gpu = now() - t0;
             });
             const double th = now();
-            if (k < n) ok = pool_.run(n - k, [&](size_t i) { return host_inflate(k + i); });
+            if (k < n) ok = pool_->run(n - k, [&](size_t i) { return host_inflate(k + i); });
             t_host = now() - th;
             gt.join();
             if (rc != 0) {
@@ -849,7 +932,7 @@ class Inflater {
                 frac_ = 0.95;
             }
         } else {
-            ok = pool_.run(blks.size(), host_inflate);
+            ok = pool_->run(blks.size(), host_inflate);
         }
         if (!ok) { c.err = "BGZF block failed to inflate or CRC mismatch"; return; }
         c.len = total;
@@ -865,7 +948,7 @@ class Inflater {
     }
 
     FILE *f_;
-    Pool pool_, spool_;
+    std::unique_ptr<Pool> pool_, spool_;   // from PoolCache, given back in the destructor
     RecParser rp_;
     int64_t end_coff_;
     uint32_t end_uoff_;
@@ -968,6 +1051,8 @@ struct dcr_ingest {
                          infl ? infl->index_parse_s : 0.0, (long long)prof.indexed, (long long)records);
         infl.reset();             // stops the inflate thread before the file closes
         if (f) std::fclose(f);
+        PoolCache::get().give(std::move(pool));
+        PoolCache::get().give(std::move(ppool));
     }
 
     // make at least n bytes available at wpos (keeping the open family);
@@ -1997,8 +2082,8 @@ static dcr_ingest *open_impl(const char *path, const dcr_ingest_cfg *cfg, bool r
     // box) their threads only preempt the serial stages (inflate thread,
     // walk) and draw quota throttling (profiles/r02pool: 192-194 -> 217-224 M
     // consensus bases/s with 8 + 8 instead of 16 + 16)
-    ing->pool.reset(new Pool(env_threads("DCR_PACK_THREADS", std::max(1, pick_threads(cfg->n_threads) / 2))));
-    ing->ppool.reset(new Pool(std::max(1, std::min(4, pick_threads(cfg->n_threads) / 4))));
+    ing->pool = PoolCache::get().take(env_threads("DCR_PACK_THREADS", std::max(1, pick_threads(cfg->n_threads) / 2)));
+    ing->ppool = PoolCache::get().take(std::max(1, std::min(4, pick_threads(cfg->n_threads) / 4)));
     ing->pk_start_thread();
     ing->rp.min_map_quality = cfg->min_map_quality;
     ing->rp.min_base_quality = cfg->min_base_quality;
