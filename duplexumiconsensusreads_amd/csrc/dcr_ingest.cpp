@@ -175,7 +175,6 @@ struct Rec {
     int8_t subk;                     // split_family subfamily (:132-154): A1 B1 A2 B2 = 0..3, -1 none
     int64_t end_kept;                // pos + length after clip removal (the T bound)
     char code[24];                   // the MI prefix, when l_code <= 24 (else read from the window)
-    char rx[32];                     // RX, when l_rx <= 32
 };
 
 const char *const kParseErr[] = {"", "malformed BAM record (l_seq < 0)",
@@ -276,9 +275,7 @@ struct RecParser {
         }
         // inline copies, zero-padded: the walk compares them as whole words
         std::memset(rc.code, 0, sizeof rc.code);
-        std::memset(rc.rx, 0, sizeof rc.rx);
         if (rc.mi_type == 'Z' && rc.l_code <= sizeof rc.code) std::memcpy(rc.code, base + rc.o_mi, rc.l_code);
-        if (rc.rx_type == 'Z' && rc.l_rx <= sizeof rc.rx) std::memcpy(rc.rx, base + rc.o_rx, rc.l_rx);
         int msg = 0;
         rc.pf = (int8_t)filters(wb, rc, msg);
         rc.fmsg = (uint8_t)msg;
@@ -1610,7 +1607,7 @@ struct dcr_ingest {
     const char *code_of(const Rec &r) const {
         return r.l_code <= sizeof r.code ? r.code : (const char *)at(r, r.o_mi);
     }
-    const char *rx_of(const Rec &r) const { return r.l_rx <= sizeof r.rx ? r.rx : (const char *)at(r, r.o_rx); }
+    const char *rx_of(const Rec &r) const { return (const char *)at(r, r.o_rx); }
     bool same_code(const Rec &a, const Rec &b) const {
         if (a.l_code != b.l_code) return false;
         if (a.l_code <= sizeof a.code) {            // zero-padded inline copies: three words
@@ -1627,7 +1624,7 @@ struct dcr_ingest {
     // in window w.  Returns DCR_ERR_NONE or the error kind with its message.
     int check_family(const Rec *const *fr, size_t n, const uint8_t *w, std::string &umi2, std::string &msg) const {
         const Rec &r0 = *fr[0];
-        auto rx_at = [&](const Rec &r) { return r.l_rx <= sizeof r.rx ? r.rx : (const char *)(w + r.off + r.o_rx); };
+        auto rx_at = [&](const Rec &r) { return (const char *)(w + r.off + r.o_rx); };
         auto code_at = [&](const Rec &r) { return r.l_code <= sizeof r.code ? r.code : (const char *)(w + r.off + r.o_mi); };
         if (r0.rx_type != 'Z') { msg = "'int' object has no attribute 'split'"; return DCR_ERR_ATTRIBUTE; }
         const char *umi1 = rx_at(r0);
@@ -1640,31 +1637,12 @@ struct dcr_ingest {
         umi2.assign(umi1 + d1 + 1, e2 - d1 - 1);
         umi2 += '-';
         umi2.append(umi1, d1);
-        // both forms zero-padded to the inline width: four-word compares
-        constexpr size_t kRx = sizeof(Rec::rx);
-        const bool inl = l1 <= kRx;
-        uint64_t w1[kRx / 8] = {0}, w2[kRx / 8] = {0};
-        if (inl) {
-            std::memcpy(w1, umi1, l1);
-            std::memcpy(w2, umi2.data(), umi2.size());   // same length as umi1
-        }
-        auto same = [&](const Rec *r, const uint64_t *wv) {
-            uint64_t x[kRx / 8];
-            std::memcpy(x, r->rx, kRx);
-            return ((x[0] ^ wv[0]) | (x[1] ^ wv[1]) | (x[2] ^ wv[2]) | (x[3] ^ wv[3])) == 0;
-        };
         for (size_t i = 0; i < n; ++i) {
             const Rec *r = fr[i];
             if (r->rx_type != 'Z') { msg = "RX tag is not a string"; return DCR_ERR_ATTRIBUTE; }
             const char *x = rx_at(*r);
-            bool eq1, eq2;
-            if (inl && r->l_rx == l1) {
-                eq1 = same(r, w1);
-                eq2 = !eq1 && l1 == umi2.size() && same(r, w2);
-            } else {
-                eq1 = r->l_rx == l1 && std::memcmp(x, umi1, l1) == 0;
-                eq2 = !eq1 && r->l_rx == umi2.size() && std::memcmp(x, umi2.data(), r->l_rx) == 0;
-            }
+            const bool eq1 = r->l_rx == l1 && std::memcmp(x, umi1, l1) == 0;
+            const bool eq2 = !eq1 && r->l_rx == umi2.size() && std::memcmp(x, umi2.data(), r->l_rx) == 0;
             if (!eq1 && !eq2) {
                 msg = "ERROR: family " + std::string(code_at(r0), r0.l_code) +
                       " has different UMI tags. \n Please check output file of previous step of the pipeline "
