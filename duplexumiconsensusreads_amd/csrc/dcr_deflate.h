@@ -30,6 +30,7 @@
 //       that is smaller) is written with plain byte stores instead.
 #pragma once
 #include <stdint.h>
+#include <type_traits>
 #include <string.h>
 
 #if defined(__HIPCC__)
@@ -62,9 +63,21 @@ namespace dfl {
 #define DFL_MW 4                           // dwords per side per match-extension step
 #endif
 constexpr int kT = DFL_T;                 // lanes per block
-constexpr uint32_t kMaxIn = 0xff00;       // input bytes per BGZF block
+#ifndef DFL_MAXIN
+#define DFL_MAXIN 0xff00
+#endif
+constexpr uint32_t kMaxIn = DFL_MAXIN;    // input bytes per BGZF block
 #ifndef DFL_HB
 #define DFL_HB 11
+#endif
+#ifndef DFL_CRCS
+#define DFL_CRCS 8                         // device CRC32 slice-by-N from LDS tables, N = 4 or 8 (0: bit by bit)
+#endif
+#ifndef DFL_SPEC
+#define DFL_SPEC 1                         // device parse: batched table warm-up, p + 1 preloaded (parse_dev)
+#endif
+#ifndef DFL_XQ
+#define DFL_XQ 1                           // device match extension: one candidate queue per lane (0: candidate by candidate)
 #endif
 constexpr int kHB = DFL_HB;
 constexpr int kHN = 1 << kHB;
@@ -87,6 +100,9 @@ struct alignas(16) Shared {
         };
         uint32_t stage[(3 * kHN * 4 + kT * 2 * kLS * 2) / 4];   // P5: the compressed member (after P2)
     };
+#if DFL_CRCS
+    uint32_t crc_t[DFL_CRCS][256];        // slice-by-N CRC32 tables, filled once per workgroup (k_deflate)
+#endif
     uint32_t lit_freq[288], dist_freq[32];
     uint8_t lit_len[288], dist_len[32], cl_len[19];
     uint16_t lit_code[288], dist_code[32], cl_code[19];   // bit-reversed (LSB-first) codes
@@ -285,6 +301,15 @@ DFL_HD inline void lt_insert(uint16_t *t, uint32_t h, uint32_t p) {
     t[set] = (uint16_t)(p + 1);
 }
 
+// candidate i for a lane-varying i: c0..c3 from the tables, then p - 1 .. p - 4
+// (a select tree: a chain of selects over an array became an indexed load
+// from private memory)
+DFL_HD inline uint32_t cand_at(uint32_t i, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t p) {
+    const uint32_t lo = i & 1 ? c1 : c0, hi = i & 1 ? c3 : c2;
+    const uint32_t t = i & 2 ? hi : lo;
+    return i < 4 ? t : p + 3 - i;
+}
+
 // greedy parse of [lo, hi): v.lit(byte) / v.match(len, dist).  Candidates
 // for position p, in this order: the lane's two latest positions with the
 // same hash set (its table holds the previous sub-block and its own
@@ -299,8 +324,188 @@ DFL_HD inline void lt_insert(uint16_t *t, uint32_t h, uint32_t p) {
 // four bytes compared together (one LDS round trip each), so a literal costs
 // three round trips; only candidates that match >= 4 bytes are extended, in
 // candidate order, skipping any that cannot beat the best so far.
+#if DFL_DEVICE && DFL_SPEC
+// The device parse: the same decisions as parse() below, scheduled for
+// fewer dependent LDS round trips per lane.
+//  - The recency table is warmed 8 positions per round trip: the 8 sets'
+//    dwords are loaded together and a set repeated within the batch takes
+//    the earlier position in registers (the stores then go out in order).
+//  - The dwords around p stay in registers (W0..W3: dwords pi-1 .. pi+2);
+//    a literal step shifts them by a dword at most, loading the next one
+//    ahead, so only a match reloads them.
+//  - Each step also loads the set dword and the block-hash candidates of
+//    p + 1; after a literal they are the next step's (the set dword with
+//    this step's insert forwarded when p + 1 falls in the same set), so a
+//    literal run costs one round trip per position (its candidates' bytes).
+template <class V>
+DFL_HD inline void parse_dev(Shared &s, uint32_t n, int lane, uint32_t lo, uint32_t hi, V &v) {
+    uint16_t *t = s.lt[lane];
+    uint32_t *t32 = reinterpret_cast<uint32_t *>(t);
+    const uint32_t *wi = reinterpret_cast<const uint32_t *>(s.in);
+DFL_UNROLL
+    for (int i = 0; i < kLS; ++i) t32[i] = 0;
+    {
+        const uint32_t S = hi - lo;
+#ifdef DFL_ABL_NOWARM                      // ablation: no table warm-up
+        for (uint32_t qb = lo; qb < lo; qb += 8) {
+#else
+        for (uint32_t qb = lo >= S ? lo - S : 0; qb < lo; qb += 8) {
+#endif
+            const uint32_t di = qb >> 2, o = qb & 3;
+            const uint32_t D0 = wi[di], D1 = wi[di + 1], D2 = wi[di + 2], D3 = wi[di + 3];
+            const uint32_t E[3] = {__builtin_amdgcn_alignbyte(D1, D0, o), __builtin_amdgcn_alignbyte(D2, D1, o),
+                                   __builtin_amdgcn_alignbyte(D3, D2, o)};
+            uint32_t set[8], old[8];
+            bool on[8];
+DFL_UNROLL
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t q = qb + (uint32_t)j;
+                const uint32_t vq = (j & 3) ? __builtin_amdgcn_alignbyte(E[(j >> 2) + 1], E[j >> 2], (uint32_t)(j & 3))
+                                            : E[j >> 2];
+                on[j] = q < lo && q + 4 <= n;
+                set[j] = hash4(vq) & (kLS - 1);
+                old[j] = t32[set[j]];
+            }
+DFL_UNROLL
+            for (int j = 0; j < 8; ++j) {
+                uint32_t w0 = old[j] & 0xffff;
+DFL_UNROLL
+                for (int i = 0; i < j; ++i) w0 = (on[i] && set[i] == set[j]) ? qb + (uint32_t)i + 1 : w0;
+                if (on[j]) t32[set[j]] = (w0 << 16) | (qb + (uint32_t)j + 1);
+            }
+        }
+    }
+    uint32_t p = lo, pi = p >> 2;
+    uint32_t W0 = pi ? wi[pi - 1] : 0u, W1 = wi[pi], W2 = wi[pi + 1], W3 = wi[pi + 2];
+    bool pre = false;
+    uint32_t tw = 0, ca = kNone, cb = kNone;    // preloaded for p: set dword, block candidates
+    while (p < hi) {
+        const uint32_t lim = (hi - p) < 258 ? (hi - p) : 258;
+        const bool hashed = p + 4 <= n;
+        const uint32_t sh = p & 3;
+        const uint32_t vp = __builtin_amdgcn_alignbyte(W2, W1, sh);
+        const uint32_t h = hashed ? hash4(vp) : 0;
+        const uint32_t set = h & (kLS - 1);
+        if (!pre) {
+            tw = t32[set];
+            if (p >= 32768) {
+                ca = s.b_min[h];
+                const uint32_t am = s.a_max[h];
+                cb = am ? am - 1 : kNone;
+            } else {
+                ca = s.a_min[h];
+                cb = kNone;
+            }
+        }
+        // p + 1, speculatively (its bytes are in W1..W3)
+        const uint32_t q = p + 1;
+        const uint32_t vq = sh < 3 ? __builtin_amdgcn_alignbyte(W2, W1, sh + 1) : W2;
+        const uint32_t hq = q + 4 <= n ? hash4(vq) : 0;
+        const uint32_t setq = hq & (kLS - 1);
+        const uint32_t twq = t32[setq];
+        uint32_t caq, cbq;
+        if (q >= 32768) {
+            caq = s.b_min[hq];
+            const uint32_t am = s.a_max[hq];
+            cbq = am ? am - 1 : kNone;
+        } else {
+            caq = s.a_min[hq];
+            cbq = kNone;
+        }
+        uint32_t best = 0, bd = 0;
+        const uint32_t t0 = tw & 0xffff, t1 = tw >> 16;
+        if (lim >= 4) {
+            uint32_t c[8];
+            c[0] = t0 ? t0 - 1 : kNone;
+            c[1] = t1 ? t1 - 1 : kNone;
+            c[2] = ca;
+            c[3] = cb;
+DFL_UNROLL
+            for (int k = 1; k <= 4; ++k) c[3 + k] = p >= (uint32_t)k ? p - (uint32_t)k : kNone;
+            uint32_t ok = 0;
+DFL_UNROLL
+            for (int i = 0; i < 4; ++i)
+                if (c[i] != kNone && c[i] < p && p - c[i] <= 32768 && ld32(s, c[i]) == vp) ok |= 1u << i;
+DFL_UNROLL
+            for (int k = 1; k <= 4; ++k) {
+                const uint32_t off = 4 + sh - (uint32_t)k;
+                const uint32_t vk = off < 4 ? __builtin_amdgcn_alignbyte(W1, W0, off)
+                                            : __builtin_amdgcn_alignbyte(W2, W1, off - 4);
+                if (p >= (uint32_t)k && vk == vp) ok |= 1u << (3 + k);
+            }
+            if (ok) {      // the candidate queue (see parse() below)
+                constexpr int kMW = DFL_MW;
+                const uint32_t lim4 = lim - 4;
+                uint32_t rem = ok & (ok - 1);
+                uint32_t cc = cand_at((uint32_t)__builtin_ctz(ok), c[0], c[1], c[2], c[3], p), l = 0;
+                bool act = true;
+                while (act) {
+                    const uint32_t xa = cc + 4 + l, xb = p + 4 + l;
+                    const uint32_t ia = xa >> 2, ib = xb >> 2, sa = xa & 3, sb = xb & 3;
+                    uint32_t a[kMW + 1], b[kMW + 1];
+DFL_UNROLL
+                    for (int k = 0; k <= kMW; ++k) { a[k] = wi[ia + k]; b[k] = wi[ib + k]; }
+                    uint32_t kk = kMW, xx = 0;
+DFL_UNROLL
+                    for (int k = kMW - 1; k >= 0; --k) {
+                        const uint32_t x = __builtin_amdgcn_alignbyte(a[k + 1], a[k], sa) ^
+                                           __builtin_amdgcn_alignbyte(b[k + 1], b[k], sb);
+                        if (x) { kk = (uint32_t)k; xx = x; }
+                    }
+                    uint32_t L = l + 4 * kMW;
+                    bool fin = L >= lim4;
+                    if (kk < (uint32_t)kMW) { L = l + 4 * kk + ((uint32_t)__builtin_ctz(xx) >> 3); fin = true; }
+                    l += 4 * kMW;
+                    if (fin) {
+                        if (L > lim4) L = lim4;
+                        if (4 + L > best) { best = 4 + L; bd = p - cc; }
+                        if (rem && best < lim) {
+                            cc = cand_at((uint32_t)__builtin_ctz(rem), c[0], c[1], c[2], c[3], p);
+                            rem &= rem - 1;
+                            l = 0;
+                        } else {
+                            act = false;
+                        }
+                    }
+                }
+            }
+        }
+        const uint32_t ins = (t0 << 16) | (p + 1);
+        if (hashed) t32[set] = ins;
+        if (best >= 4) {
+            v.match(best, bd);
+            p += best;
+            pi = p >> 2;
+            W0 = pi ? wi[pi - 1] : 0u;
+            W1 = wi[pi];
+            W2 = wi[pi + 1];
+            W3 = wi[pi + 2];
+            pre = false;
+        } else {
+            v.lit((uint8_t)vp);
+            p = q;
+            tw = (hashed && setq == set) ? ins : twq;
+            ca = caq;
+            cb = cbq;
+            pre = true;
+            if ((q >> 2) != pi) {
+                pi = q >> 2;
+                W0 = W1;
+                W1 = W2;
+                W2 = W3;
+                W3 = wi[pi + 2];
+            }
+        }
+    }
+}
+#endif
+
 template <class V>
 DFL_HD inline void parse(Shared &s, uint32_t n, int lane, uint32_t lo, uint32_t hi, V &v) {
+#if DFL_DEVICE && DFL_SPEC
+    parse_dev(s, n, lane, lo, hi, v);
+    return;
+#endif
     uint16_t *t = s.lt[lane];
     for (int i = 0; i < 2 * kLS; ++i) t[i] = 0;
     const uint32_t S = hi - lo;
@@ -360,6 +565,52 @@ DFL_UNROLL
 #endif
                 if (p >= (uint32_t)k && vk == vp) ok |= 1u << (3 + k);
             }
+#if DFL_DEVICE && DFL_XQ
+            // The candidates with >= 4 matching bytes are extended through one
+            // queue per lane: each iteration is one kMW-dword step of the
+            // lane's current candidate, so a wave runs as many iterations as
+            // its busiest lane needs, not the sum over candidate slots of the
+            // most any lane needs there.  The first longest candidate wins, as
+            // in the loop below (which also skips, by one byte, candidates that
+            // cannot beat the best so far; here they run to their mismatch).
+            if (ok) {
+                constexpr int kMW = DFL_MW;
+                const uint32_t *w = reinterpret_cast<const uint32_t *>(s.in);
+                const uint32_t lim4 = lim - 4;
+                uint32_t rem = ok & (ok - 1);
+                uint32_t cc = cand_at((uint32_t)__builtin_ctz(ok), c[0], c[1], c[2], c[3], p), l = 0;
+                bool act = true;
+                while (act) {
+                    const uint32_t xa = cc + 4 + l, xb = p + 4 + l;
+                    const uint32_t ia = xa >> 2, ib = xb >> 2, sa = xa & 3, sb = xb & 3;
+                    uint32_t a[kMW + 1], b[kMW + 1];
+DFL_UNROLL
+                    for (int k = 0; k <= kMW; ++k) { a[k] = w[ia + k]; b[k] = w[ib + k]; }
+                    uint32_t kk = kMW, xx = 0;
+DFL_UNROLL
+                    for (int k = kMW - 1; k >= 0; --k) {
+                        const uint32_t x = __builtin_amdgcn_alignbyte(a[k + 1], a[k], sa) ^
+                                           __builtin_amdgcn_alignbyte(b[k + 1], b[k], sb);
+                        if (x) { kk = (uint32_t)k; xx = x; }
+                    }
+                    uint32_t L = l + 4 * kMW;
+                    bool fin = L >= lim4;
+                    if (kk < (uint32_t)kMW) { L = l + 4 * kk + ((uint32_t)__builtin_ctz(xx) >> 3); fin = true; }
+                    l += 4 * kMW;
+                    if (fin) {
+                        if (L > lim4) L = lim4;
+                        if (4 + L > best) { best = 4 + L; bd = p - cc; }
+                        if (rem && best < lim) {
+                            cc = cand_at((uint32_t)__builtin_ctz(rem), c[0], c[1], c[2], c[3], p);
+                            rem &= rem - 1;
+                            l = 0;
+                        } else {
+                            act = false;
+                        }
+                    }
+                }
+            }
+#else
 DFL_UNROLL
             for (int i = 0; i < 8; ++i) {
                 if (!((ok >> i) & 1) || best >= lim) continue;
@@ -367,6 +618,7 @@ DFL_UNROLL
                 const uint32_t l = 4 + match_len(s, c[i] + 4, p + 4, lim - 4);
                 if (l > best) { best = l; bd = p - c[i]; }
             }
+#endif
         }
         if (hashed) {                                       // lt_insert(t, h, p)
 #if DFL_DEVICE
@@ -389,6 +641,16 @@ DFL_UNROLL
 struct CountV {            // P2: symbol histogram, extra bits
     Shared &s;
     uint32_t extra = 0;
+#ifdef DFL_ABL_NOCNT                       // ablation (invalid members): the histogram atomics spread over bins
+    int lane;
+    DFL_HD void lit(uint8_t b) { aadd(&s.lit_freq[(b + (uint32_t)lane) & 255], 1); }
+    DFL_HD void match(uint32_t len, uint32_t d) {
+        const Sym L = len_code(len), D = dist_code(d);
+        aadd(&s.lit_freq[257 + (L.sym + (uint32_t)lane) % 29], 1);
+        aadd(&s.dist_freq[(D.sym + (uint32_t)lane) % 30], 1);
+        extra += L.nb + D.nb;
+    }
+#else
     DFL_HD void lit(uint8_t b) { aadd(&s.lit_freq[b], 1); }
     DFL_HD void match(uint32_t len, uint32_t d) {
         const Sym L = len_code(len), D = dist_code(d);
@@ -396,6 +658,7 @@ struct CountV {            // P2: symbol histogram, extra bits
         aadd(&s.dist_freq[D.sym], 1);
         extra += L.nb + D.nb;
     }
+#endif
 };
 
 struct TokV {              // P2: the lane's tokens (kTokE layout)
@@ -500,6 +763,69 @@ struct BitOut {
         }
         acc = 0;
         nacc = 0;
+    }
+};
+
+// The same writer without a branch per symbol (P5 into stage[]): every put
+// stores one word, the completed one or, when none completed, a throwaway
+// into `dummy` (a word of the lane's own nobody reads); a first word shared
+// with the previous lane is kept in a register and or-ed in at flush.
+struct BitOut2 {
+    uint32_t *w, *dummy;
+    uint64_t acc = 0;
+    uint32_t nacc, word, w0, fw = 0;
+    bool pend, shared_first, own_last;    // pend: the shared first word is not complete yet
+    DFL_HD BitOut2(uint32_t *words, uint32_t bitpos, bool own_last_word, uint32_t *dummy_word)
+        : w(words), dummy(dummy_word), nacc(bitpos & 31), word(bitpos >> 5), w0(bitpos >> 5),
+          pend((bitpos & 31) != 0), shared_first((bitpos & 31) != 0), own_last(own_last_word) {}
+    DFL_HD uint32_t pos() const { return word * 32 + nacc; }
+    DFL_HD void put(uint32_t v, uint32_t nb) {     // nb <= 32, v < 2^nb
+        acc |= (uint64_t)v << nacc;
+        nacc += nb;
+        const bool full = nacc >= 32;
+        const uint32_t lo = (uint32_t)acc;
+        *(full && !pend ? &w[word] : dummy) = lo;
+        fw = full && pend ? lo : fw;
+        pend = pend && !full;
+        word += full ? 1u : 0u;
+        acc = full ? acc >> 32 : acc;
+        nacc -= full ? 32u : 0u;
+    }
+    DFL_HD void flush() {
+        if (shared_first && !pend) aor(&w[w0], fw);
+        if (nacc) {
+            if (pend || !own_last) aor(&w[word], (uint32_t)acc);
+            else w[word] = (uint32_t)acc;
+        }
+        acc = 0;
+        nacc = 0;
+    }
+};
+
+// P5 with BitOut2: two literal codes (<= 15 bits each) per put, a length or
+// distance code with its extra bits in one put
+struct EmitV2 {
+    const Shared &s;
+    BitOut2 &o;
+    DFL_HD void lits(uint32_t p, uint32_t run) {
+        uint32_t q = 0;
+        for (; q + 4 <= run; q += 4) {
+            const uint32_t w = ld32(s, p + q);
+            const uint32_t e0 = s.lit_cl[w & 255], e1 = s.lit_cl[(w >> 8) & 255], e2 = s.lit_cl[(w >> 16) & 255],
+                           e3 = s.lit_cl[w >> 24];
+            o.put((e0 & 0xffff) | (e1 & 0xffff) << (e0 >> 16), (e0 >> 16) + (e1 >> 16));
+            o.put((e2 & 0xffff) | (e3 & 0xffff) << (e2 >> 16), (e2 >> 16) + (e3 >> 16));
+        }
+        for (; q < run; ++q) {
+            const uint32_t e = s.lit_cl[s.in[p + q]];
+            o.put(e & 0xffff, e >> 16);
+        }
+    }
+    DFL_HD void match(uint32_t len, uint32_t d) {
+        const Sym L = len_code(len), D = dist_code(d);
+        const uint32_t le = s.lit_cl[257 + L.sym], de = s.dist_cl[D.sym];
+        o.put((le & 0xffff) | L.ev << (le >> 16), (le >> 16) + L.nb);
+        o.put((de & 0xffff) | D.ev << (de >> 16), (de >> 16) + D.nb);
     }
 };
 
@@ -904,7 +1230,8 @@ DFL_HD inline void p3d_codes(Shared &s, int lane) {
     if (lane < 19) s.cl_code[lane] = code_of(s.cl_len, lane, s.next_code[2]);
 }
 
-DFL_HD inline void write_header(const Shared &s, BitOut &o) {
+template <class O>
+DFL_HD inline void write_header(const Shared &s, O &o) {
     o.put(1, 1);          // BFINAL
     o.put(2, 2);          // BTYPE = 10 (dynamic Huffman)
     o.put(s.hlit, 5);
@@ -928,7 +1255,8 @@ DFL_HD inline void put_bytes(uint32_t *w, uint32_t at, uint32_t v, int nb) {
 
 // gzip member header with the BGZF extra field: 1f 8b 08 04 | mtime 0 |
 // xfl 0 | os ff | xlen 6 | 'B' 'C' 2 0 | BSIZE (member bytes - 1)
-DFL_HD inline void put_gzip_header(BitOut &o, uint32_t bsize) {
+template <class O>
+DFL_HD inline void put_gzip_header(O &o, uint32_t bsize) {
     o.put(0x04088b1fu, 32);
     o.put(0, 32);
     o.put(0xff00u, 16);
@@ -964,13 +1292,37 @@ DFL_HD inline void p1_hash(Shared &s, uint32_t n, int lane) {
 DFL_HD inline void p2_count(Shared &s, uint32_t n, int lane, uint32_t *tok) {
     uint32_t lo, hi;
     lane_range(n, lane, lo, hi);
+#ifdef DFL_ABL_NOCNT
+    CountTokV v{CountV{s, 0, lane}, TokV{tok, lane}};
+#else
     CountTokV v{CountV{s}, TokV{tok, lane}};
+#endif
     parse(s, n, lane, lo, hi, v);
     v.t.finish();
     if (v.c.extra) aadd(&s.extra_bits, v.c.extra);
     // CRC32 register of the sub-block (no init / final xor), shifted past the rest
     uint32_t c = 0;
+#if defined(DFL_ABL_NOCRC)
+    (void)c;
+#elif DFL_DEVICE && DFL_CRCS
+    // slice-by-N: N independent table loads per N / 4 dwords
+    uint32_t p = lo;
+    for (; p < hi && (p & 3); ++p) c = s.crc_t[0][(c ^ s.in[p]) & 0xff] ^ (c >> 8);
+    const uint32_t *wi = reinterpret_cast<const uint32_t *>(s.in);
+    for (; p + DFL_CRCS <= hi; p += DFL_CRCS) {
+        const uint32_t a = c ^ wi[p >> 2];
+#if DFL_CRCS == 8
+        const uint32_t b = wi[(p >> 2) + 1];
+        c = s.crc_t[7][a & 255] ^ s.crc_t[6][(a >> 8) & 255] ^ s.crc_t[5][(a >> 16) & 255] ^ s.crc_t[4][a >> 24] ^
+            s.crc_t[3][b & 255] ^ s.crc_t[2][(b >> 8) & 255] ^ s.crc_t[1][(b >> 16) & 255] ^ s.crc_t[0][b >> 24];
+#else
+        c = s.crc_t[3][a & 255] ^ s.crc_t[2][(a >> 8) & 255] ^ s.crc_t[1][(a >> 16) & 255] ^ s.crc_t[0][a >> 24];
+#endif
+    }
+    for (; p < hi; ++p) c = s.crc_t[0][(c ^ s.in[p]) & 0xff] ^ (c >> 8);
+#else
     for (uint32_t p = lo; p < hi; ++p) c = crc_byte((c ^ s.in[p]) & 0xff) ^ (c >> 8);
+#endif
     s.lane_crc[lane] = (hi > lo) ? multmodp(x8nmodp(n - hi), c) : 0;
 }
 DFL_HD inline void p4_bits(Shared &s, uint32_t n, int lane, const uint32_t *tok) {
@@ -1007,11 +1359,24 @@ DFL_HD inline void p4_scan(Shared &s, uint32_t n, uint32_t *out) {
 #else
 #define DFL_INLINE inline
 #endif
+template <bool kStage>
+DFL_HD inline typename std::conditional<kStage, BitOut2, BitOut>::type make_out(uint32_t *w, uint32_t bitpos, bool own_last,
+                                                                              uint32_t *dummy);
+template <>
+DFL_HD inline BitOut2 make_out<true>(uint32_t *w, uint32_t bitpos, bool own_last, uint32_t *dummy) {
+    return BitOut2(w, bitpos, own_last, dummy);
+}
+template <>
+DFL_HD inline BitOut make_out<false>(uint32_t *w, uint32_t bitpos, bool own_last, uint32_t *) {
+    return BitOut(w, bitpos, own_last);
+}
+template <bool kStage>
 DFL_HD DFL_INLINE void p5_emit_to(Shared &s, uint32_t n, int lane, const uint32_t *tok, uint32_t *out);
 DFL_HD inline void p5_emit(Shared &s, uint32_t n, int lane, const uint32_t *tok, uint32_t *out) {
-    if (s.use_stage) p5_emit_to(s, n, lane, tok, s.stage);
-    else p5_emit_to(s, n, lane, tok, out);
+    if (s.use_stage) p5_emit_to<true>(s, n, lane, tok, s.stage);
+    else p5_emit_to<false>(s, n, lane, tok, out);
 }
+template <bool kStage>
 DFL_HD DFL_INLINE void p5_emit_to(Shared &s, uint32_t n, int lane, const uint32_t *tok, uint32_t *out) {
     uint32_t lo, hi;
     lane_range(n, lane, lo, hi);
@@ -1021,12 +1386,16 @@ DFL_HD DFL_INLINE void p5_emit_to(Shared &s, uint32_t n, int lane, const uint32_
         for (uint32_t p = lo; p < hi; ++p) o[p] = s.in[p];
         return;
     }
-    BitOut o(out, lane == 0 ? 0 : s.lane_off[lane], lane == kT - 1);
+    // the member in stage[] (LDS, nearly always): BitOut2 (its throwaway
+    // word the lane's lane_bits entry, read before P5); else BitOut
+    using O = typename std::conditional<kStage, BitOut2, BitOut>::type;
+    using V = typename std::conditional<kStage, EmitV2, EmitV>::type;
+    O o = make_out<kStage>(out, lane == 0 ? 0 : s.lane_off[lane], lane == kT - 1, &s.lane_bits[lane]);
     if (lane == 0) {
         put_gzip_header(o, (s.body_bits + 7) / 8 + 25);
         write_header(s, o);
     }
-    EmitV v{s, o};
+    V v{s, o};
     replay(s, tok, lane, lo, v);
     if (lane == kT - 1) {
         o.put(s.lit_code[256], s.lit_len[256]);

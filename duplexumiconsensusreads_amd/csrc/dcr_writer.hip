@@ -464,6 +464,20 @@ __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
     __shared__ uint64_t t[12];
     uint64_t t0 = 0;
     if (st && lane < 12) t[lane] = 0;
+#if DFL_CRCS
+    static_assert(DFL_CRCS == 4 || DFL_CRCS == 8, "CRC32 slices: 4 or 8");
+    // slice-by-N CRC32 tables, once per workgroup: t[0] the byte table,
+    // t[k][i] = t[k-1][i] >> 8 ^ t[0][t[k-1][i] & 255]
+    for (int i = lane; i < 256; i += dfl::kT) s.crc_t[0][i] = dfl::crc_byte((uint32_t)i);
+    __syncthreads();
+    for (int k = 1; k < DFL_CRCS; ++k) {
+        for (int i = lane; i < 256; i += dfl::kT) {
+            const uint32_t v = s.crc_t[k - 1][i];
+            s.crc_t[k][i] = (v >> 8) ^ s.crc_t[0][v & 255];
+        }
+        __syncthreads();
+    }
+#endif
     auto stamp = [&](int k) {
         if (st && lane == 0) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
@@ -524,7 +538,9 @@ __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
         p4_scan_wg(s, n, lane, slot);
         __syncthreads();
         stamp(7);
+#ifndef DFL_ABL_NOEMIT
         dfl::p5_emit(s, n, lane, tok, slot);
+#endif
         __syncthreads();
         dfl::p6_copy(s, lane, slot);
         stamp(8);

@@ -3,7 +3,8 @@ formatting and BGZF deflate on the GPU) against the host writer
 (csrc/dcr_format.cpp over the kernel outputs of dcr_submit) on the same
 batches: the decompressed record stream must be byte-identical, every BGZF
 block a valid member with the right CRC32 / ISIZE, and the per-family
-outcomes equal to the host scan's."""
+outcomes equal to the host scan's; the members are the host emulation's
+(dcr_deflate_emulate) byte for byte."""
 import gzip
 import struct
 import zlib
@@ -78,6 +79,11 @@ def test_device_writer_matches_host_writer(tmp_path, kind):
         assert len(got) == res.record_bytes
         assert got == want
         assert fetched == want
+        # the device deflate is the host emulation's algorithm, scheduled for
+        # the GPU (dcr_deflate.h parse_dev, BitOut2): the same members, byte
+        # for byte
+        emu = b"".join(native_io.deflate_emulate(fetched[i:i + 0xff00]) for i in range(0, len(fetched), 0xff00))
+        assert emu == res.bgzf.tobytes()
     assert n_fam > 0
     dev.close()
     host.close()
