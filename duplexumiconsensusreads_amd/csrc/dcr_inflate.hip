@@ -26,6 +26,7 @@
 //     zlib's crc32_combine algebra, dcr_deflate.h multmodp);
 //   - ISIZE and CRC32 checked against the member trailer on the device.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <condition_variable>
 #include <cstring>
@@ -911,6 +912,22 @@ struct dcr_inflate_stream {
     dcr_inflate_stream(dcr_inflater *h, const uint8_t *file) : be{h, *h->slots}, s(be, file) {}
 };
 
+// The span kernels' stream.  DCR_INFLATE_CU_SHARE=k (1..3, diagnostic)
+// masks it to k of every 4 CUs, so batch kernels always find CUs free of
+// inflate waves; unset: every CU.
+static hipError_t span_stream_create(int device, hipStream_t *s) {
+    const char *e = getenv("DCR_INFLATE_CU_SHARE");
+    const int k = e ? atoi(e) : 0;
+    int n_cu = 0;
+    if (k < 1 || k > 3 || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        n_cu <= 0)
+        return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    std::vector<uint32_t> mask((size_t)(n_cu + 31) / 32, 0u);
+    for (int i = 0; i < n_cu; ++i)
+        if (i % 4 < k) mask[(size_t)i / 32] |= 1u << (i % 32);
+    return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+}
+
 extern "C" dcr_inflate_stream *dcr_inflate_stream_open(dcr_inflater *h, const uint8_t *file) {
     if (!h || !file) {
         dcr::set_error(DCR_EARG, "dcr_inflate_stream_open: bad arguments");
@@ -927,7 +944,7 @@ extern "C" dcr_inflate_stream *dcr_inflate_stream_open(dcr_inflater *h, const ui
     }
     InflSlots &S = *h->slots;
     (void)hipSetDevice(h->device);
-    if ((!S.s_k && hipStreamCreateWithFlags(&S.s_k, hipStreamNonBlocking) != hipSuccess) ||
+    if ((!S.s_k && span_stream_create(h->device, &S.s_k) != hipSuccess) ||
         (!S.s_out && hipStreamCreateWithFlags(&S.s_out, hipStreamNonBlocking) != hipSuccess)) {
         std::lock_guard<std::mutex> g(h->mu);
         S.busy = false;
