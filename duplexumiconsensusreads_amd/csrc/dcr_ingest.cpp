@@ -544,6 +544,7 @@ class Inflater {
             if (!c.pin) c.buf.resize(kHead + want_max_ + 0x10000);
             empty_.push_back(&c);
         }
+        if (const char *he = std::getenv("DCR_HOST_CHUNK_EVERY")) host_every_ = std::max(0, std::atoi(he));
         if (gpu_ && map_ && hook_.stream_open) open_stream();
         if (gpu_ && !stream_) {
             stage_cap_ = want_max_ + ((size_t)1 << 20);
@@ -603,10 +604,18 @@ class Inflater {
         const size_t p0 = cbeg_, p_end = cend_;
         mth_ = std::thread([this, p0, p_end] { scan_members(p0, p_end); });
     }
+    // Chunks the host pool inflates beside the device stream (every
+    // host_every_-th, DCR_HOST_CHUNK_EVERY; 0: none): the stream skips their
+    // members, fill() inflates them with libdeflate.  Chunk k is the k-th
+    // fill(); its blocks follow fill()'s rule (whole blocks while the
+    // chunk's output + 64 KiB fits want_: 4 MiB for the first, then
+    // want_max_), which scan_members() replays over the member headers.
+    bool host_chunk(size_t k) const { return host_every_ > 1 && k % (size_t)host_every_ == (size_t)host_every_ - 1; }
     void scan_members(size_t p, const size_t cend) {
         std::vector<dcr_bgzf_member> ms;
         int64_t out = 0;
         size_t batch = 128;
+        size_t ck = 0, ctotal = 0, cwant = want_;    // fill()'s chunking, replayed
         auto flush = [&](bool last) {
             hook_.stream_add(stream_, ms.data(), (int32_t)ms.size(), last ? 1 : 0);
             ms.clear();
@@ -631,9 +640,17 @@ class Inflater {
             if (blen < 12 + xlen + 8 || cend - p < blen) break;
             const uint32_t isize = rd32(h + blen - 4);
             if (isize > 0x10000) break;
-            ms.push_back(dcr_bgzf_member{(int64_t)(p + 12 + xlen), out, (uint32_t)(blen - 12 - xlen - 8), isize,
-                                         rd32(h + blen - 8), 0});
-            out += isize;
+            if (ctotal + 0x10000 > cwant) {
+                ++ck;
+                ctotal = 0;
+                cwant = want_max_;
+            }
+            ctotal += isize;
+            if (!host_chunk(ck)) {
+                ms.push_back(dcr_bgzf_member{(int64_t)(p + 12 + xlen), out, (uint32_t)(blen - 12 - xlen - 8), isize,
+                                             rd32(h + blen - 8), 0});
+                out += isize;
+            }
             const bool last_of_range = end_coff_ >= 0 && p == (uint64_t)end_coff_;
             p += blen;
             if (last_of_range) break;
@@ -873,7 +890,11 @@ class Inflater {
             return libdeflate_crc32(0, dst + b.doff, b.isize) == b.crc;
         };
         bool ok = true;
-        if (stream_ && !blks.empty()) {
+        const bool host_k = stream_ && !blks.empty() && host_chunk(fill_k_);
+        if (!blks.empty()) ++fill_k_;
+        if (host_k) {
+            ok = pool_->run(blks.size(), host_inflate);        // a chunk the stream skipped
+        } else if (stream_ && !blks.empty()) {
             // inflated ahead by the device: copy this chunk's bytes out
             const size_t out_blocks = blks.back().doff + blks.back().isize - kHead;
             const int rc = hook_.stream_fetch(stream_, stream_out_, (int64_t)out_blocks, dst + kHead);
@@ -882,6 +903,13 @@ class Inflater {
                 return;
             }
             stream_out_ += (int64_t)out_blocks;
+            // the chunk's first member against its CRC32: a stream out of step
+            // with this walk (host chunks skipped differently) would hand over
+            // another member's bytes
+            if (host_every_ > 1 && libdeflate_crc32(0, dst + blks[0].doff, blks[0].isize) != blks[0].crc) {
+                c.err = "GPU inflate stream out of step with the reader";
+                return;
+            }
         } else if (gpu_ && !blks.empty()) {
             // the chunk's first k members inflate on the GPU (their compressed
             // bytes copied to page-locked staging by the pool first; CRC32 and
@@ -967,6 +995,8 @@ class Inflater {
     std::atomic<bool> stop_members_{false};
     int64_t stream_out_ = 0;           // output bytes fetched from it so far
     double frac_ = 0.5;                // share of a chunk's members inflated on the GPU
+    int host_every_ = 0;               // every host_every_-th chunk inflated by the host pool (stream mode)
+    size_t fill_k_ = 0;                // chunks filled so far
     bool frac_fixed_ = false;          // DCR_GPU_INFLATE_FRAC set: no adaptation
     HugeBuf cbuf_;
     size_t cbeg_ = 0, cend_ = 0;

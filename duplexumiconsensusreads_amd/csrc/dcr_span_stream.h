@@ -112,6 +112,13 @@ struct Stream {
                 Span sp;
                 sp.m0 = mnext;
                 sp.m1 = std::min((int32_t)m.size(), mnext + want);
+                // a span ends at a gap in the compressed input (members the
+                // reader inflates on the host): its staging copy is contiguous
+                for (int32_t i = sp.m0 + 1; i < sp.m1; ++i)
+                    if (m[i].in_off > m[i - 1].in_off + (int64_t)m[i - 1].in_len + 64) {
+                        sp.m1 = i;
+                        break;
+                    }
                 sp.out0 = m[sp.m0].out_off;
                 sp.out1 = m[sp.m1 - 1].out_off + m[sp.m1 - 1].isize;
                 sp.in0 = m[sp.m0].in_off;
