@@ -76,6 +76,9 @@ constexpr uint32_t kMaxIn = DFL_MAXIN;    // input bytes per BGZF block
 #ifndef DFL_SPEC
 #define DFL_SPEC 1                         // device parse: batched table warm-up, p + 1 preloaded (parse_dev)
 #endif
+#ifndef DFL_CRC_LATE
+#define DFL_CRC_LATE 1                     // device: sub-block CRCs on the waves the code-length phase leaves idle
+#endif
 #ifndef DFL_XQ
 #define DFL_XQ 1                           // device match extension: one candidate queue per lane (0: candidate by candidate)
 #endif
@@ -1289,6 +1292,7 @@ DFL_HD inline void p1_hash(Shared &s, uint32_t n, int lane) {
         else amin(&s.b_min[h], p);
     }
 }
+DFL_HD inline uint32_t sub_crc(const Shared &s, uint32_t n, int l);
 DFL_HD inline void p2_count(Shared &s, uint32_t n, int lane, uint32_t *tok) {
     uint32_t lo, hi;
     lane_range(n, lane, lo, hi);
@@ -1300,7 +1304,17 @@ DFL_HD inline void p2_count(Shared &s, uint32_t n, int lane, uint32_t *tok) {
     parse(s, n, lane, lo, hi, v);
     v.t.finish();
     if (v.c.extra) aadd(&s.extra_bits, v.c.extra);
-    // CRC32 register of the sub-block (no init / final xor), shifted past the rest
+#if !(DFL_DEVICE && DFL_CRC_LATE)
+    s.lane_crc[lane] = sub_crc(s, n, lane);
+#endif
+}
+
+// CRC32 register of sub-block l (no init / final xor), shifted past the rest
+// of the block.  On the device it runs during the code-length phase, on the
+// two waves that phase leaves idle (k_deflate, DFL_CRC_LATE).
+DFL_HD inline uint32_t sub_crc(const Shared &s, uint32_t n, int l) {
+    uint32_t lo, hi;
+    lane_range(n, l, lo, hi);
     uint32_t c = 0;
 #if defined(DFL_ABL_NOCRC)
     (void)c;
@@ -1323,7 +1337,7 @@ DFL_HD inline void p2_count(Shared &s, uint32_t n, int lane, uint32_t *tok) {
 #else
     for (uint32_t p = lo; p < hi; ++p) c = crc_byte((c ^ s.in[p]) & 0xff) ^ (c >> 8);
 #endif
-    s.lane_crc[lane] = (hi > lo) ? multmodp(x8nmodp(n - hi), c) : 0;
+    return (hi > lo) ? multmodp(x8nmodp(n - hi), c) : 0;
 }
 DFL_HD inline void p4_bits(Shared &s, uint32_t n, int lane, const uint32_t *tok) {
     uint32_t lo, hi;

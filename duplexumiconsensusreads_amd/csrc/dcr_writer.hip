@@ -521,6 +521,15 @@ __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
         __syncthreads();
         stamp(3);
         dfl::p3c_trees(s, lane);
+#if DFL_CRC_LATE
+        // waves 2 and 3 are idle while lanes 0 and 64 build the two codes:
+        // the sub-block CRCs (two per lane) go there
+        static_assert(dfl::kT == 256, "DFL_CRC_LATE assumes four waves");
+        if (lane >= 128) {
+            s.lane_crc[lane - 128] = dfl::sub_crc(s, n, lane - 128);
+            s.lane_crc[lane] = dfl::sub_crc(s, n, lane);
+        }
+#endif
         __syncthreads();
         stamp(4);
         dfl::p3c_assign(s, lane);
