@@ -76,6 +76,9 @@ constexpr uint32_t kMaxIn = DFL_MAXIN;    // input bytes per BGZF block
 #ifndef DFL_SPEC
 #define DFL_SPEC 1                         // device parse: batched table warm-up, p + 1 preloaded (parse_dev)
 #endif
+#ifndef DFL_P1W
+#define DFL_P1W 1                          // device block hash: one dword load per four positions
+#endif
 #ifndef DFL_CRC_LATE
 #define DFL_CRC_LATE 1                     // device: sub-block CRCs on the waves the code-length phase leaves idle
 #endif
@@ -1286,6 +1289,31 @@ DFL_HD inline void p0_clear(Shared &s, int lane) {
 DFL_HD inline void p1_hash(Shared &s, uint32_t n, int lane) {
     uint32_t lo, hi;
     lane_range(n, lane, lo, hi);
+#if DFL_DEVICE && DFL_P1W
+    // a dword at a time: each input dword loaded once (the next one ahead),
+    // its four positions' bytes by funnel shifts
+    {
+        const uint32_t *wi = reinterpret_cast<const uint32_t *>(s.in);
+        const uint32_t end = hi < (n >= 3 ? n - 3 : 0) ? hi : (n >= 3 ? n - 3 : 0);   // p + 4 <= n
+        uint32_t d = lo >> 2;
+        uint32_t A = wi[d], B = wi[d + 1];
+        for (uint32_t p0 = lo & ~3u; p0 < end; p0 += 4) {
+            const uint32_t C = wi[d + 2];
+DFL_UNROLL
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t p = p0 + k;
+                if (p < lo || p >= end) continue;
+                const uint32_t h = hash4(k ? __builtin_amdgcn_alignbyte(B, A, k) : A);
+                if (p < 32768) { amin(&s.a_min[h], p); amax(&s.a_max[h], p + 1); }
+                else amin(&s.b_min[h], p);
+            }
+            A = B;
+            B = C;
+            ++d;
+        }
+        return;
+    }
+#endif
     for (uint32_t p = lo; p < hi && p + 4 <= n; ++p) {
         const uint32_t h = hash4(ld32(s, p));
         if (p < 32768) { amin(&s.a_min[h], p); amax(&s.a_max[h], p + 1); }
