@@ -688,15 +688,31 @@ struct CountTokV {         // P2: both
 };
 
 // the tokens of a lane again, from the token buffer
+#ifndef DFL_TOKPF
+#define DFL_TOKPF 4                        // token entries in flight during a replay (1 or 4)
+#endif
 template <class V>
 DFL_HD inline void replay(const Shared &s, const uint32_t *t, int lane, uint32_t lo, V &v) {
     uint32_t p = lo;
+#if DFL_TOKPF == 4
+    // four entries in flight (the token buffer is in HBM / L2): a ring
+    // shifted by one per entry (entries past the tail hold stale words,
+    // never used)
+    uint32_t x1 = t[lane], x2 = t[kT + lane], x3 = t[2 * kT + lane], x4 = t[3 * kT + lane];
+    for (int e = 0; e < kTokE; ++e) {
+        const uint32_t x = x1;
+        x1 = x2;
+        x2 = x3;
+        x3 = x4;
+        if (e + 4 < kTokE) x4 = t[(e + 4) * kT + lane];
+#else
     uint32_t xn = t[lane];
     for (int e = 0; e < kTokE; ++e) {
         // the next entry's load is in flight while this one is replayed
         // (entries past the tail hold stale words, never used)
         const uint32_t x = xn;
         if (e + 1 < kTokE) xn = t[(e + 1) * kT + lane];
+#endif
         const uint32_t run = (x >> 23) & 255;
         v.lits(p, run);
         p += run;
