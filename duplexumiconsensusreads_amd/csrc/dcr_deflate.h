@@ -79,6 +79,9 @@ constexpr uint32_t kMaxIn = DFL_MAXIN;    // input bytes per BGZF block
 #ifndef DFL_P1W
 #define DFL_P1W 1                          // device block hash: one dword load per four positions
 #endif
+#ifndef DFL_CODES_EARLY
+#define DFL_CODES_EARLY 1                  // device: literal / distance codes on waves 1-3 during the header
+#endif
 #ifndef DFL_CRC_LATE
 #define DFL_CRC_LATE 1                     // device: sub-block CRCs on the waves the code-length phase leaves idle
 #endif
@@ -1238,6 +1241,39 @@ DFL_HD inline void p3c_header(Shared &s) {
 }
 
 // P3d (all lanes): canonical codes
+// the first code of length L from the counts per length (one entry of
+// first_codes_from_counts)
+DFL_HD inline uint32_t first_code_of(const uint32_t *num, uint32_t L) {
+    uint32_t c = 0;
+    for (uint32_t l = 1; l <= L; ++l) c = (c + (l > 1 ? num[l - 1] : 0)) << 1;
+    return c;
+}
+// p3d_codes' literal/length and distance codes on lanes i0, i0 + step, ...
+// (the device runs them on waves 1-3 while wave 0 builds the header)
+DFL_HD inline void p3d_codes_litdist(Shared &s, int i0, int step) {
+    for (int i = i0; i < 288; i += step) {
+        const uint32_t L = s.lit_len[i];
+        uint16_t c = 0;
+        if (i < 286 && L) {
+            uint32_t r = 0;
+            for (int j = 0; j < i; ++j) r += s.lit_len[j] == L;
+            c = (uint16_t)reverse_bits(first_code_of(s.num_lit, L) + r, (int)L);
+        }
+        s.lit_code[i] = c;
+        s.lit_cl[i] = c | L << 16;
+    }
+    for (int i = i0; i < 32; i += step) {
+        const uint32_t L = s.dist_len[i];
+        uint16_t c = 0;
+        if (i < 30 && L) {
+            uint32_t r = 0;
+            for (int j = 0; j < i; ++j) r += s.dist_len[j] == L;
+            c = (uint16_t)reverse_bits(first_code_of(s.num_dist, L) + r, (int)L);
+        }
+        s.dist_code[i] = c;
+        s.dist_cl[i] = c | L << 16;
+    }
+}
 DFL_HD inline void p3d_codes(Shared &s, int lane) {
     for (int i = lane; i < 288; i += kT) {
         const uint16_t c = i < 286 ? code_of(s.lit_len, i, s.next_code[0]) : 0;

@@ -536,9 +536,16 @@ __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
         __syncthreads();
         stamp(10);
         if (lane < kW) p3c_header_wave(s, lane);
+#if DFL_CODES_EARLY
+        else dfl::p3d_codes_litdist(s, lane - kW, dfl::kT - kW);   // waves 1-3, idle during the header
+#endif
         __syncthreads();
         stamp(11);
+#if DFL_CODES_EARLY
+        if (lane < 19) s.cl_code[lane] = dfl::code_of(s.cl_len, lane, s.next_code[2]);
+#else
         dfl::p3d_codes(s, lane);
+#endif
         __syncthreads();
         stamp(5);
         dfl::p4_bits(s, n, lane, tok);
