@@ -450,6 +450,9 @@ __device__ __forceinline__ void p3c_header_wave(dfl::Shared &s, int lane) {
     }
 }
 
+#ifndef DFL_STAGE4
+#define DFL_STAGE4 1      // stage a block 16 bytes per lane per load, four loads in flight
+#endif
 // one workgroup (256 lanes) per BGZF block of the record stream
 __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
     extern __shared__ __align__(16) uint8_t smem[];
@@ -493,6 +496,38 @@ __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
         // stage the block as dwords (block starts are dword-aligned; the
         // record stream's allocation is padded), zero bytes past n
         {
+#if DFL_STAGE4
+            // 16 bytes per lane per load, four loads in flight (block starts
+            // are 16-byte aligned: 0xff00 = 16 * 4080)
+            static_assert(dfl::kMaxIn % 16 == 0 && sizeof(s.in) % 16 == 0, "16-byte staging");
+            const uint4 *src = reinterpret_cast<const uint4 *>(D.stream + off);
+            uint4 *dst = reinterpret_cast<uint4 *>(s.in);
+            const uint32_t nq = (n + 15) / 16, pq = (uint32_t)sizeof(s.in) / 16;
+            auto mask = [&](uint32_t w, uint32_t byte0) -> uint32_t {     // bytes of w at or past n zeroed
+                return byte0 + 4 <= n ? w : byte0 >= n ? 0u : w & ((1u << (8 * (n - byte0))) - 1);
+            };
+            for (uint32_t i0 = lane; i0 < pq; i0 += 4 * dfl::kT) {
+                uint4 v[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t i = i0 + (uint32_t)k * dfl::kT;
+                    v[k] = (i < nq) ? src[i] : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t i = i0 + (uint32_t)k * dfl::kT;
+                    if (i >= pq) continue;
+                    uint4 w = v[k];
+                    if (16 * i + 16 > n) {
+                        w.x = mask(w.x, 16 * i);
+                        w.y = mask(w.y, 16 * i + 4);
+                        w.z = mask(w.z, 16 * i + 8);
+                        w.w = mask(w.w, 16 * i + 12);
+                    }
+                    dst[i] = w;
+                }
+            }
+#else
             const uint32_t *src = reinterpret_cast<const uint32_t *>(D.stream + off);
             uint32_t *dst = reinterpret_cast<uint32_t *>(s.in);
             const uint32_t nw = (n + 3) / 4, pw = (uint32_t)sizeof(s.in) / 4;
@@ -505,6 +540,7 @@ __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
                 }
                 dst[i] = v;
             }
+#endif
         }
         dfl::p0_clear(s, lane);
         __syncthreads();
