@@ -739,26 +739,30 @@ def _run_range(args, params, backend, path, rng, rng_state, rng_range, parts, de
     return res
 
 
-def _count_calls(path, params, rng_range, threads, stop):
+def _count_calls(path, params, rng_range, threads, stop, batch_reads=1 << 19):
     """The (population, size) of every random.sample call of one range, by a
     host-only ingest (host inflate, no device work, batches discarded): the
     calls depend only on the data (family and subfamily sizes), not on the
-    generator's state.  Stops early (partial list, unused) when ``stop`` is
-    set; an input error ends the list where the ingest stops."""
+    generator's state.  Returns None (nothing to publish: the rank's own pass
+    publishes) unless the ingest reached the end of the range or stopped where
+    the reference stops; a stop request also gives None.  Batches are sized as
+    the CLI's (``--batch_reads``), so a family the CLI can hold fits here."""
     ing = native_io.Ingest(path, params.min_map_quality, params.min_reads, params.max_reads,
                            params.min_base_quality, threads, rng_range[0], rng_range[1], host_inflate=True)
+    complete = False
     try:
-        hb = native_io.HostBatch(reads=1 << 18)
+        hb = native_io.HostBatch(reads=max(batch_reads, 1))
         while not stop.is_set():
             ing.next(hb)
             if hb.end_kind != native_io.END_FULL:
+                complete = True              # END_EOF, or END_ERROR: the calls up to the reference's stop
                 break
-    except Exception:  # noqa: BLE001 - the calls up to the stop are the range's calls
-        pass
+    except Exception:  # noqa: BLE001 - an unfinished count is not published
+        complete = False
     finally:
         calls = ing.sample_calls()
         ing.close()
-    return calls
+    return calls if complete else None
 
 
 class _StateExchange:
@@ -776,7 +780,9 @@ class _StateExchange:
 
     _seq = 0
 
-    def __init__(self, dist, rank, world, s0, path, params, rng_range, threads):
+    _FAILED = b"failed"
+
+    def __init__(self, dist, rank, world, s0, path, params, rng_range, threads, batch_reads=1 << 19):
         from datetime import timedelta
         _StateExchange._seq += 1       # every rank opens its exchanges in the same order
         self.store = dist.distributed_c10d._get_default_store()
@@ -792,19 +798,22 @@ class _StateExchange:
         self.th = None
         if rng_range is not None and rank < world - 1:
             # only later ranks read this rank's calls
-            self.th = threading.Thread(target=self._counter, args=(path, params, rng_range, threads),
+            self.th = threading.Thread(target=self._counter, args=(path, params, rng_range, threads, batch_reads),
                                        name="dcr-count", daemon=True)
             self.th.start()
 
     def publish(self, calls):
+        """``calls``: this range's random.sample calls; None marks the rank as
+        failed before it knew them (a later rank's gate then raises instead
+        of waiting for calls that never come)."""
         with self.lock:
             if self.published:
                 return
             self.published = True
-        flat = np.asarray(calls, np.int32).reshape(-1)
-        self.store.set(self.pre + "calls%d" % self.rank, flat.tobytes())
+        val = self._FAILED if calls is None else np.asarray(calls, np.int32).reshape(-1).tobytes()
+        self.store.set(self.pre + "calls%d" % self.rank, val)
 
-    def _counter(self, path, params, rng_range, threads):
+    def _counter(self, path, params, rng_range, threads, batch_reads):
         from datetime import timedelta
         while not self.stop.is_set():
             try:
@@ -815,8 +824,8 @@ class _StateExchange:
         if self.stop.is_set() or self.published:
             return
         self.counted = True
-        calls = _count_calls(path, params, rng_range, threads, self.stop)
-        if not self.stop.is_set():
+        calls = _count_calls(path, params, rng_range, threads, self.stop, batch_reads)
+        if calls is not None and not self.stop.is_set():
             self.publish(calls)
 
     def gate(self):
@@ -828,7 +837,10 @@ class _StateExchange:
             self.store.wait(keys, self.wait_timeout)
         state = self.s0
         for k in keys:
-            flat = np.frombuffer(self.store.get(k), np.int32)
+            val = self.store.get(k)
+            if val == self._FAILED:
+                raise RuntimeError("%s: an earlier rank failed before publishing its random.sample calls" % k)
+            flat = np.frombuffer(val, np.int32)
             state = native_io.py_replay(state, [(int(flat[2 * i]), int(flat[2 * i + 1]))
                                                 for i in range(len(flat) // 2)])
         self.gated_state = state
@@ -939,15 +951,19 @@ def _main_sharded(args, params, backend, rng, stats, group):
     empty = {"status": "ok", "exc_args": (), "calls": [], "counters": None, "stdout": "", "stats": {},
              "sizes": [0, 0, 0]}
     result, used, rounds = empty, None, 0
-    xch = _StateExchange(dist, rank, world, s0, path, params, mine, args.threads)
+    xch = _StateExchange(dist, rank, world, s0, path, params, mine, args.threads, args.batch_reads)
+    done = False
     try:
         if mine is not None:
             result = _run_range(args, params, backend, path, rng, s0, mine, parts, device,
                                 gate=xch.gate if rank > 0 else None)
             used, rounds = (xch.gated_state or s0), 1
-        # this rank's calls for the later ranks (if no count pass published them first)
-        xch.publish(result["calls"])
+        done = True
     finally:
+        # this rank's calls for the later ranks (if no count pass published
+        # them first); a rank that raised before knowing them publishes the
+        # failure marker, so no later rank's gate waits for them
+        xch.publish(result["calls"] if done else None)
         xch.close()
     # a safety net only: with the gate, a rank sampled from its exact state
     while True:

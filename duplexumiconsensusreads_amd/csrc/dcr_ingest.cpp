@@ -1394,7 +1394,10 @@ struct dcr_ingest {
             if (cnt[k] > cfg.max_reads) { samples = true; break; }
         }
         const size_t l_code = r0.l_code;
-        const int64_t names_need = (int64_t)l_code + 1 + 2 * (int64_t)(r0.l_rx + 1) + 64 * 2;
+        // the RX written below is that of the first A1 and B1 read, whose
+        // length the deferred UMI check (run_task) has not yet tied to r0's
+        const int64_t l_rx0 = first[0] ? first[0]->l_rx : 0, l_rx2 = first[2] ? first[2]->l_rx : 0;
+        const int64_t names_need = (int64_t)l_code + 1 + (l_rx0 + 1) + (l_rx2 + 1) + 64 * 2;
         if (samples || pend_recs.size() + fam.size() > pend_recs.capacity() || tasks.size() == tasks.capacity()) {
             if (flush_tasks() < 0) return -1;
             return complete_family();

@@ -304,3 +304,61 @@ def test_ingest_many_chunks_reproduces_the_source_batch(tmp_path):
     assert n_fam == src.n_fam
     for k, v in got.items():
         assert np.array_equal(np.concatenate(v), getattr(src, k)), k
+
+
+def test_ingest_long_mismatched_rx_stays_in_the_names_buffer(tmp_path):
+    """A family whose first A1 / B1 reads carry RX strings much longer than
+    its first record's (the UMI check fails, but only on the packer task,
+    after the walk has reserved the family's names): the reservation counts
+    the RX that is actually written, so a batch near its names capacity ends
+    before the family instead of writing past the buffer, and the family
+    then fails the UMI check in the next batch as the reference does (:110)."""
+    from duplexumiconsensusreads_amd.bam import AlignmentFile, BamHeader
+    from duplexumiconsensusreads_amd.records import AlignedSegment
+
+    def rec(name, flag, mi, rx, pos=100):
+        r = AlignedSegment()
+        r.query_name, r.flag, r.reference_id, r.reference_start = name, flag, 0, pos
+        r.mapping_quality = 60
+        r.cigartuples = [(0, 20)]
+        r.query_sequence = "ACGT" * 5
+        r.query_qualities = [30] * 20
+        r.next_reference_id, r.next_reference_start = 0, pos
+        r.set_tags([("MI", mi), ("RX", rx)])
+        return r
+
+    fams = []
+    for k in range(15):                      # 60 reads, ~6 KB of names
+        rx = "A" * 100 + "-" + "C" * 99
+        fams.append([rec(f"q{k}_{j}", fl, f"{k}/{'A' if fl in (99, 147) else 'B'}", rx)
+                     for j, fl in enumerate((99, 163, 83, 147))])
+    big = "G" * 16450 + "-" + "T" * 16449    # 32,900 bytes per RX
+    fams.append([rec("x0", 147, "15/A", "AC-GT"), rec("x1", 99, "15/A", big), rec("x2", 83, "15/B", big),
+                 rec("x3", 163, "15/B", "AC-GT")])
+    path = str(tmp_path / "longrx.bam")
+    hdr = BamHeader("@HD\tVN:1.6\n@SQ\tSN:chr1\tLN:1000000\n", ["chr1"], [1000000])
+    with AlignmentFile(path, "wb", header=hdr) as out:
+        for fam in fams:
+            for r in fam:
+                out.write(r)
+    guard = 1 << 20
+
+    def guarded(nbytes):
+        buf = np.full(nbytes + guard, 0xA5, np.uint8)
+        guarded.bufs.append((buf, nbytes))
+        return buf[:nbytes]
+    guarded.bufs = []
+    ing = native_io.Ingest(path, 20, 1, 100, 20, 2)
+    kinds = []
+    while True:
+        hb = native_io.HostBatch(reads=64, side_bytes=1 << 20, alloc=guarded)
+        ing.next(hb)
+        kinds.append((hb.s.n_fam, hb.end_kind))
+        if hb.end_kind != native_io.END_FULL:
+            break
+    err = hb.error()
+    ing.close()
+    for buf, n in guarded.bufs:
+        assert (buf[n:] == 0xA5).all(), "write past the batch's arrays"
+    assert kinds[0] == (15, native_io.END_FULL)
+    assert kinds[-1][1] != native_io.END_EOF and "UMI" in err[1].upper(), (kinds, err)
