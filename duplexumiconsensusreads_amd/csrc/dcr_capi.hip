@@ -104,10 +104,12 @@ struct dcr_ctx {
     // fast-kernel constants (fast_constants)
     uint32_t fast_kq = 0, fast_kqlo = 0;
     int fast_maxq = 0, fast_t16 = 0, fast_r_safe = 0, fast_qlo = 0;
+    int fast_t8 = 0, fast_narrow = 0;   // the common fast instantiation's narrow rows (1/8 nat)
     // single-strand records of at most this many reads skip the common fast
     // pass (the exact pass takes them whole); DCR_EXACT_DIRECT_R overrides
     int direct_r = 3;
     uint16_t *d_llr16 = nullptr;   // device [128]
+    uint16_t *d_llr8 = nullptr;    // device [128]
     double *d_e1000 = nullptr;     // device [1001]: k / 1000 (the fast kernel's E)
     uint32_t *d_wtab = nullptr;    // device [DCR_LUT_N] (general kernel's decision pass)
     int n_cu = 256;     // compute units (persistent grid size)
@@ -137,10 +139,14 @@ static int fast_allowed(const dcr_params *p) {
 //              double (e^-700 > DBL_MIN = e^-708.4).
 //              Above it the reference's products can underflow to 0 (S = 0, NaN posterior, call
 //              'A' :613), which the LLR bound does not see: every column then takes the exact path.
+//   llr8[q], t8: the same in 1/8 nat for the common fast instantiation's
+//              narrow rows (dcr_kernels.hip, Evidence8: 15 rows of llr8 <= 273 fit
+//              12 bits); narrow = 0 when some llr8 does not fit (then that
+//              instantiation queues every record for the EXACT one)
 // Returns 0 when the decision cannot be made for these parameters (then every
 // record takes the general kernel).
-static int fast_constants(const dcr_params &hp, uint16_t llr16[128], uint32_t &kq, uint32_t &kqlo, int &maxq,
-                          int &t16, int &r_safe, int &qlo_out) {
+static int fast_constants(const dcr_params &hp, uint16_t llr16[128], uint16_t llr8[128], uint32_t &kq, uint32_t &kqlo,
+                          int &maxq, int &t16, int &t8, int &narrow, int &r_safe, int &qlo_out) {
     const int mb = std::min(std::max(hp.min_base_quality, 0), 255);
     kq = (uint32_t)(255 - mb) * 0x01010101u;
     maxq = hp.max_base_quality;
@@ -148,18 +154,24 @@ static int fast_constants(const dcr_params &hp, uint16_t llr16[128], uint32_t &k
     while (qlo > 0 && hp.mismatch[qlo - 1] > 0.0 && hp.match[qlo - 1] >= hp.mismatch[qlo - 1]) --qlo;
     kqlo = (uint32_t)(0x80 - qlo) * 0x01010101u;
     qlo_out = qlo;
+    narrow = 1;
     for (int q = 0; q < 128; ++q) {
         llr16[q] = 0;
+        llr8[q] = 0;
         if (q >= qlo && q <= 122) {
             const double v = std::floor(16.0 * std::log(hp.match[q] / hp.mismatch[q]) - 1e-6);
             if (!(v <= 1040.0)) return 0;                  // 63 rows must fit a 16-bit field
             llr16[q] = (uint16_t)std::max(v, 0.0);
+            const double v8 = std::floor(8.0 * std::log(hp.match[q] / hp.mismatch[q]) - 1e-6);
+            if (!(v8 <= 273.0)) narrow = 0;                // 15 rows must fit 12 bits
+            else llr8[q] = (uint16_t)std::max(v8, 0.0);
         }
     }
     const int mq = std::min(std::max(hp.max_base_quality, 0), DCR_MAX_QTHRESH - 1);
     const double cc = std::min(std::min(hp.qthresh[mq], 1.0 - hp.post_threshold), 0.25);
     if (!(cc > 1e-12)) return 0;
     t16 = (int)std::ceil(16.0 * std::log(5.0 / cc)) + 1;
+    t8 = (int)std::ceil(8.0 * std::log(5.0 / cc)) + 1;
     double cmax = 0.0;                                 // per-row bound on -ln(factor), either factor
     for (int q = 0; q <= 122; ++q) {
         cmax = std::max(cmax, -std::log(hp.mismatch[q]));
@@ -198,13 +210,14 @@ static int wide_table(const dcr_params &hp, uint32_t wtab[DCR_LUT_N]) {
 }
 
 static int upload_fast(dcr_ctx *c, const dcr_params *params) {
-    uint16_t llr[128];
+    uint16_t llr[128], llr8[128];
     uint32_t wtab[DCR_LUT_N];
-    const int ok = fast_constants(*params, llr, c->fast_kq, c->fast_kqlo, c->fast_maxq, c->fast_t16,
-                                 c->fast_r_safe, c->fast_qlo);
+    const int ok = fast_constants(*params, llr, llr8, c->fast_kq, c->fast_kqlo, c->fast_maxq, c->fast_t16, c->fast_t8,
+                                 c->fast_narrow, c->fast_r_safe, c->fast_qlo);
     c->fast_ok = fast_allowed(params) && ok;
     c->wide_ok = c->fast_ok && wide_table(*params, wtab);
     if (hipMemcpy(c->d_llr16, llr, sizeof(llr), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_llr8, llr8, sizeof(llr8), hipMemcpyHostToDevice) != hipSuccess ||
         (c->wide_ok && hipMemcpy(c->d_wtab, wtab, sizeof(wtab), hipMemcpyHostToDevice) != hipSuccess))
         return fail(DCR_EHIP, "fast-kernel table upload failed");
     return DCR_OK;
@@ -245,6 +258,7 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
         hi_prio_stream(&c->stream) != hipSuccess ||
         hipMalloc(&c->d_params, sizeof(dcr_params)) != hipSuccess ||
         hipMalloc(&c->d_llr16, 128 * sizeof(uint16_t)) != hipSuccess ||
+        hipMalloc(&c->d_llr8, 128 * sizeof(uint16_t)) != hipSuccess ||
         hipMalloc(&c->d_e1000, 1001 * sizeof(double)) != hipSuccess ||
         hipMalloc(&c->d_wtab, DCR_LUT_N * sizeof(uint32_t)) != hipSuccess) {
         fail(DCR_EHIP, "context allocation failed");
@@ -301,6 +315,7 @@ void dcr_destroy(dcr_ctx *c) {
     if (c->ev_fetch) (void)hipEventDestroy(c->ev_fetch);
     if (c->d_params) (void)hipFree(c->d_params);
     if (c->d_llr16) (void)hipFree(c->d_llr16);
+    if (c->d_llr8) (void)hipFree(c->d_llr8);
     if (c->d_e1000) (void)hipFree(c->d_e1000);
     if (c->d_wtab) (void)hipFree(c->d_wtab);
     for (auto &e : c->ev)
@@ -348,6 +363,7 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     const size_t o_deep = o; o = align_up(o + sizeof(int) * n_rec);
     const size_t o_meta = o; o = align_up(o + sizeof(dcr::RecMeta) * n_rec);
     const size_t o_rm = o;   o = align_up(o + sizeof(uint2) * std::max<size_t>((size_t)s->n_reads, n_rec));
+    const size_t o_rows = o; o = align_up(o + sizeof(uint4) * n_rec);
     if (o > c->ws.cap) {
         HIP_TRY(hipStreamSynchronize(c->stream));
         HIP_TRY(c->ws.ensure(o + o / 8));
@@ -371,6 +387,7 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     c->w.ovf = (int *)(b + o_ovf);
     c->w.meta = (dcr::RecMeta *)(b + o_meta);
     c->w.rmeta = (uint2 *)(b + o_rm);
+    c->w.rows = (uint4 *)(b + o_rows);
     return DCR_OK;
 }
 
@@ -406,12 +423,15 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
     auto fast_grid = [&](int64_t n_rec, int k) {
         return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_rec + 127) / 128, (int64_t)c->fast_blocks[k] * c->n_cu));
     };
+    // k_fast_rows: one lane per fast-list entry (the list is at most n_rec long)
+    auto rows_grid = [&](int64_t n_rec) { return (unsigned)std::max<int64_t>(1, (n_rec + 255) / 256); };
     auto fast_args = [&](bool duplex) {
         dcr::FastArgs f{};
         f.gb = duplex ? ss->seq : in->bases;
         f.gq = duplex ? ss->qual : in->quals;
         f.nbytes = duplex ? in->ss_cols : in->n_bases;
         f.meta = c->w.meta;
+        f.rows = c->w.rows;
         f.rmeta = c->w.rmeta;
         f.fast_count = c->w.fast_count + (duplex ? 1 : 0);
         f.info = c->w.info;
@@ -432,6 +452,9 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         f.minbq = duplex ? -1 : c->host_params.min_base_quality;
         f.lo_check = duplex || c->host_params.min_base_quality < c->fast_qlo;
         f.llr16 = c->d_llr16;
+        f.llr8 = c->d_llr8;
+        f.t8 = c->fast_t8;
+        f.narrow = c->fast_narrow;
         f.e1000 = c->d_e1000;
         {
             // record-scalar stores at 32-bit offsets from the lowest array
@@ -480,6 +503,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
             HIP_TRY(hipEventRecord(ev[0], c->stream));
             hipLaunchKernelGGL((dcr::k_consensus_fast<true, false>), dim3(fast_grid(a.n_rec, 1)), dim3(dcr::kFastBlock),
                                0, c->stream, fa);
+            hipLaunchKernelGGL(dcr::k_fast_rows, dim3(rows_grid(a.n_rec)), dim3(256), 0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL((dcr::k_consensus_fast<true, true>), dim3(gx), dim3(dcr::kFastBlock), 0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[2], c->stream));
@@ -492,6 +516,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
             HIP_TRY(hipEventRecord(ev[0], c->stream));
             hipLaunchKernelGGL((dcr::k_consensus_fast<false, false>), dim3(fast_grid(a.n_rec, 0)),
                                dim3(dcr::kFastBlock), 0, c->stream, fa);
+            hipLaunchKernelGGL(dcr::k_fast_rows, dim3(rows_grid(a.n_rec)), dim3(256), 0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             hipLaunchKernelGGL((dcr::k_consensus_fast<false, true>), dim3(gx), dim3(dcr::kFastBlock), 0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[2], c->stream));

@@ -535,10 +535,6 @@ class Inflater {
         }
         // GPU inflate: larger chunks (a launch needs ~1,000 members to fill the device)
         want_max_ = gpu_ ? kWantGpu : kWant;
-        if (const char *fr = std::getenv("DCR_GPU_INFLATE_FRAC")) {
-            frac_ = std::min(1.0, std::max(0.0, std::atof(fr)));
-            frac_fixed_ = true;
-        }
         for (auto &c : chunks_) {
             if (gpu_ && hook_.host_alloc) c.pin = (uint8_t *)hook_.host_alloc(hook_.user, kHead + want_max_ + 0x10000);
             if (!c.pin) c.buf.resize(kHead + want_max_ + 0x10000);
@@ -950,10 +946,10 @@ class Inflater {
                 c.err = rc > 0 ? "BGZF block failed to inflate or CRC mismatch" : "GPU inflate failed";
                 return;
             }
-            if (!frac_fixed_ && k < n && t_gpu > 0 && t_host > 0) {
+            if (k < n && t_gpu > 0 && t_host > 0) {
                 frac_ *= std::sqrt(t_host / t_gpu);
                 frac_ = std::min(0.95, std::max(0.05, frac_));
-            } else if (!frac_fixed_ && k == n && t_gpu > 0) {
+            } else if (k == n && t_gpu > 0) {
                 frac_ = 0.95;
             }
         } else {
@@ -997,7 +993,6 @@ class Inflater {
     double frac_ = 0.5;                // share of a chunk's members inflated on the GPU
     int host_every_ = 0;               // every host_every_-th chunk inflated by the host pool (stream mode)
     size_t fill_k_ = 0;                // chunks filled so far
-    bool frac_fixed_ = false;          // DCR_GPU_INFLATE_FRAC set: no adaptation
     HugeBuf cbuf_;
     size_t cbeg_ = 0, cend_ = 0;
     bool file_eof_ = false;

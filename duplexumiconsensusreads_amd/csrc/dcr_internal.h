@@ -55,6 +55,9 @@ struct Workspace {
     int *xlist;             // [n_rec] exact queue: fast-list indices (k_consensus_fast<., true>)
     unsigned long long *stamps;   // [32] diagnostic phase cycles (DCR_STAMP builds only)
     RecMeta *meta;          // [n_rec] fast list
+    uint4 *rows;            // [n_rec] per fast-list entry: the record's scalars as k_consensus_fast
+                            // decided them (pos, T | D << 8 | M << 16 | MAPQ << 24, mean numerator
+                            // or 0, kind), expanded into dcr_out by k_fast_rows; kind 0 = not decided
     uint2 *rmeta;           // [max(n_reads, 4F)] per read: len | mapq << 8 | (pos - pos of the record's
                             // first read) << 16 (int16), seq_start (low 32 bits)
 };
@@ -77,6 +80,7 @@ struct FastArgs {
     const uint8_t *gb, *gq;         // staged bytes: input reads (single-strand) or single-strand consensus (duplex)
     int64_t nbytes;                 // length of gb / gq (buffer-load range check)
     const RecMeta *meta;            // fast list descriptors
+    uint4 *rows;                    // per fast-list entry: decided scalars (Workspace::rows)
     const uint2 *rmeta;             // per-read words
     const int *fast_count;          // fast-list length
     dcr_read_info *info;            // single-strand: read info of the fast records' reads
@@ -96,7 +100,10 @@ struct FastArgs {
     int r_safe;                     // most reads for which no decided column's L_b can underflow
     int minbq;                      // single-strand: min_base_quality (masked rows in the table); duplex: -1
     int lo_check;                   // some unmasked quality may lie below fast_qlo: check the bytes
-    const uint16_t *llr16;          // [123] per-quality LLR term, 1/16 nat, rounded down
+    const uint16_t *llr16;          // [123] per-quality LLR term, 1/16 nat, rounded down (EXACT's wide rows)
+    const uint16_t *llr8;           // [123] the same in 1/8 nat (the common instantiation's narrow rows)
+    int t8;                         // decision margin in 1/8 nat
+    int narrow;                     // llr8 fits the narrow rows (else the common kernel queues every record)
     const double *e1000;            // [1001] k / 1000 correctly rounded (numpy round(x, 3) = rint(1000 x) / 1000)
     // record scalars (pos, mapq, len, n_cig, n_de, D, M, E lo, E hi, cigar):
     // the lowest of the ten arrays and each one's byte offset from it, when
@@ -110,6 +117,7 @@ struct FastArgs {
 template <bool DUPLEX> __global__ void k_recmeta(Args a);
 __global__ void k_prep_big(Args a);
 template <bool DUPLEX, bool EXACT> __global__ void k_consensus_fast(FastArgs a);
+__global__ void k_fast_rows(FastArgs a);
 template <bool DUPLEX> __global__ void k_consensus_general(Args a);
 template <bool DUPLEX> __global__ void k_decide(Args a);
 __global__ void k_decide_deep(Args a);

@@ -35,17 +35,14 @@
 #ifndef DCR_STAMP
 #define DCR_STAMP 0   // diagnostic builds only (tools/stamps.py): per-phase s_memtime cycle totals
 #endif
-#ifndef DCR_PIPE2
-#define DCR_PIPE2 2   // tiles up to which the products keep two reads in flight
+#ifndef DCR_FAST_OCC
+#define DCR_FAST_OCC 6   // fast kernel (common instantiation): waves per SIMD the launch bounds ask for
 #endif
-#ifndef DCR_STORE_MODE
-#define DCR_STORE_MODE 1  // fast kernel's column stores: 1 32-bit offsets from scalar bases, 0 64-bit lane addresses
+#ifndef DCR_TRIM2
+#define DCR_TRIM2 1   // fast kernel: the 3' trim of C2-shaped records checked from the evidence counts
 #endif
-#ifndef DCR_SCAL_MODE
-#define DCR_SCAL_MODE 1   // fast kernel's record scalars: 1 32-bit offsets from one base, 0 64-bit lane addresses
-#endif
-#ifndef DCR_MEAN_MODE
-#define DCR_MEAN_MODE 0   // fast kernel's E: 0 double estimate of the rational, 1 scalar division, 2 + table load
+#ifndef DCR_ROWS
+#define DCR_ROWS 1    // fast kernel: decided scalars as one 16-byte row per record, expanded by k_fast_rows
 #endif
 #ifndef DCR_ABL
 #define DCR_ABL 0   // diagnostic builds only (tools/ablate.py); fast kernel: 1 staging only, 2 +products,
@@ -2383,42 +2380,64 @@ constexpr int kWaves = kFastWaves;                         // waves per block
 constexpr int kBlockThreads = kFastBlock;
 constexpr int kRowMax = 122;                               // quality rows 0..122
 constexpr uint32_t kPadCode = 16u * 2u;                    // class N, quality 2 (:509-510, :543-544)
+constexpr uint32_t kPadCode8 = 8u * 2u;                    // the same in the narrow table (common instantiation)
 constexpr int kNMax = 0x800;                               // codes below: class N
-constexpr int kTable = 5 * 0x800;                          // 5 class banks of 2 KiB
-constexpr int kStage0 = kTable;                            // 4 KiB per wave
-constexpr int kInvD = kStage0 + kWaves * 0x1000;           // f64 [64] 1 / d
-constexpr int kSent = kInvD + 64 * 8;                      // u16 pad code (out-of-read sentinel)
-constexpr int kPtrs = kSent + 16;                          // u64 [32] pointers (kP* below)
-constexpr int kRm = kPtrs + 32 * 8;                        // per wave: u64 [64] the current record's read words
-constexpr int kMv = kRm + kWaves * kWave * 8;              // per wave: u32 [8] a later record's descriptor
-constexpr int kOv = kMv + kWaves * 32;                     // per wave: u16 [256] column words d | e << 6 | call << 12
-constexpr int kM720 = kOv + kWaves * 512;                  // u32 [64] 720720 / d for depths d <= 16, else 0
+constexpr int kTable = 5 * 0x800;                          // 5 class banks of 2 KiB (narrow: of 1 KiB)
+constexpr int kTable8 = 5 * 0x400;
+constexpr int kPtrs = kTable;                              // u64 [32] pointers (kP* below)
+constexpr int kSent = kPtrs + 32 * 8;                      // u16 pad code (out-of-read sentinel)
+constexpr int kM720 = kSent + 16;                          // u32 [64] 720720 / d for depths d <= 16, else 0
+constexpr int kInvD = kM720 + 64 * 4;                      // f64 [64] 1 / d
+constexpr int kSofs = kInvD + 64 * 8;                      // u32 [10][2]: record-scalar array offsets from sbase, shifts
+constexpr int kMv = kSofs + 10 * 8;                        // per wave: u32 [8] a later record's descriptor
+constexpr int kWave0 = kMv + kWaves * 32;                  // the waves' regions
+static_assert(16 * (kRowMax + 5) <= 0x800, "a class bank fits 2 KiB");
+static_assert(kWave0 % 16 == 0, "16-byte aligned stages");
+// a wave's region: the staged element codes (2 B per byte of the record),
+// the current record's read words (u64 [64]) and, EXACT, the column words
+// (u16 [256], d | e << 6 | call << 12).  The EXACT instantiation stages up to
+// 2,048 bytes against the wide table (16-byte rows): 31,968 B per 4-wave
+// block, four blocks per CU at its 128 VGPRs.  The common instantiation stages
+// records of at most 1,536 bytes (larger ones go to the EXACT queue unstaged)
+// against the narrow table (8-byte rows, 5 KiB, so wave 0's region lies in the
+// table's unused half) and keeps its column words in the codes' space, dead
+// once the evidence is summed: 22,240 B per block, seven blocks (28 waves)
+// per CU.
 #ifndef DCR_LDS_PAD
 #define DCR_LDS_PAD 0
 #endif
-constexpr int kSofs = kM720 + 64 * 4;                      // u32 [10][2]: record-scalar array offsets from sbase, shifts
-constexpr int kLdsBytes = kSofs + 10 * 8 + DCR_LDS_PAD;       // PAD: diagnostic builds only
-static_assert(kStageElems * 2 == 0x1000, "one 4 KiB stage per wave");
-static_assert(16 * (kRowMax + 5) <= 0x800, "a class bank fits 2 KiB");
-// five blocks per CU need <= 32,000 B each (measured, DESIGN §3: 32,016 B ran
-// four blocks per CU and took 26 % longer than 31,968 B): 1,280-byte units
+template <bool EXACT>
+struct Region {
+    static constexpr int kCodes = EXACT ? 0x1000 : 0xC00;
+    static constexpr int kRm = kCodes;                     // offset of the read words
+    static constexpr int kOv = EXACT ? kCodes + 512 : 0;   // offset of the column words
+    static constexpr int kBytes = kCodes + 512 + (EXACT ? 512 : 0);
+    static constexpr int kDw = kCodes / 2 / 4 / kWave;     // staged dwords per lane: 8 / 6
+    static constexpr int kLds = kWave0 + (EXACT ? kWaves : kWaves - 1) * kBytes + DCR_LDS_PAD;   // PAD: diagnostic builds
+    __device__ static constexpr int base(int wave) {       // wave's region
+        return EXACT ? kWave0 + wave * kBytes : (wave == 0 ? kTable8 : kWave0 + (wave - 1) * kBytes);
+    }
+};
+static_assert(kTable8 + Region<false>::kBytes <= kTable, "wave 0's region in the narrow table's unused half");
+// the LDS cliffs (measured, DESIGN §3: 32,016 B ran four 4-wave blocks per CU
+// where 31,968 B ran five, 26 % slower): 1,280-byte units, 128 per CU
 constexpr int kLdsUnit = 1280;
-static_assert(5 * ((kLdsBytes + kLdsUnit - 1) / kLdsUnit) * kLdsUnit <= 160 * 1024, "five blocks (20 waves) per CU");
-
-__device__ __forceinline__ int stage_base(int wave) { return kStage0 + (wave << 12); }
+constexpr int lds_units(int b) { return (b + kLdsUnit - 1) / kLdsUnit; }
+static_assert(4 * lds_units(Region<true>::kLds) <= 128, "EXACT: four blocks per CU");
+static_assert(7 * lds_units(Region<false>::kLds) <= 128 && 7 * Region<false>::kLds <= 160000,
+              "common: seven blocks (28 waves) per CU");
 // pointer-cache slots: every pointer the record loop stores through is read
 // from LDS where it is used, so none is held in scalar registers across the
 // loop (the kernel's arguments no longer spill into VGPR lanes, whose
 // restores are VALU instructions)
 constexpr int kPNormCig = 10, kPCigOff = 11, kPOvf = 12, kPOvfCount = 13, kPXlist = 14, kPXcount = 15;
 constexpr int kPD = 16, kPE = 17, kPSeq = 18, kPQual = 19, kPStatus = 20, kPInfo = 21, kPParams = 22, kPSbase = 23;
-constexpr int kPE1000 = 24, kNPtrs = 25;
+constexpr int kPE1000 = 24, kPRows = 25, kNPtrs = 26;
 }  // namespace fk
 
-constexpr int kStageDw = kStageElems / 4 / kWave;   // staged dwords per lane
-
+template <int NDW>
 struct FastStage {
-    uint32_t vb[kStageDw], vq[kStageDw];   // raw base / quality bytes, dword u * 64 + lane of the record
+    uint32_t vb[NDW], vq[NDW];             // raw base / quality bytes, dword u * 64 + lane of the record
     uint2 rm;                              // this lane's read meta (lane < R)
     uint32_t mv;                           // dword `lane` of a later record's descriptor (lanes < 8)
 };
@@ -2427,9 +2446,9 @@ struct FastStage {
 // loads on a resource based at the record's first byte: dword u * 64 + lane at
 // voffset 4 lane + immediate 256 u, no per-lane address arithmetic, and bytes
 // past the end of the array read as 0 (range-checked) instead of faulting.
-template <bool DUPLEX>
+template <bool DUPLEX, int NDW>
 __device__ __forceinline__ void fast_load(const FastArgs &a, const RecMeta &m, const RecMeta *mlater, int lane,
-                                          FastStage &st) {
+                                          FastStage<NDW> &st) {
     const int ndw = (int)(m.w >> 15);
     // range: the array's last dword read whole (device allocations are padded
     // to at least 16 bytes, as the 16-byte-aligned staging already assumes)
@@ -2440,7 +2459,7 @@ __device__ __forceinline__ void fast_load(const FastArgs &a, const RecMeta &m, c
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void *)(a.gq + m.base_al), (short)0, nrec,
                                                                         0x00020000);
 #pragma unroll
-    for (int u = 0; u < kStageDw; ++u) {
+    for (int u = 0; u < NDW; ++u) {
         if (u * kWave < ndw) {
             st.vb[u] = __builtin_amdgcn_raw_buffer_load_b32(rb, 4 * lane + 256 * u, 0, 0);
             st.vq[u] = __builtin_amdgcn_raw_buffer_load_b32(rq, 4 * lane + 256 * u, 0, 0);
@@ -2465,7 +2484,8 @@ __device__ __forceinline__ void fast_load(const FastArgs &a, const RecMeta &m, c
 // masked (the reference would read it as 'N'): its record takes the general
 // kernel, which reproduces that exactly.  LO: some unmasked quality lies below
 // fast_qlo, so the bytes are checked for it (not with the default flags).
-template <bool DUPLEX, bool LO>
+// NARROW (the common instantiation's table of 8-byte rows): code = (k << 10) | 8 (q + k).
+template <bool DUPLEX, bool LO, bool NARROW>
 __device__ __forceinline__ uint2 make_codes4(uint32_t B, uint32_t Q, uint32_t kq, uint32_t kqlo, uint32_t &bad) {
     const uint32_t h = (B >> 1) & 0x07070707u;
     const uint32_t k = __builtin_amdgcn_perm(0u, 0x04020301u, h);                 // A1 C3 T2 G4 . . . N0
@@ -2480,8 +2500,8 @@ __device__ __forceinline__ uint2 make_codes4(uint32_t B, uint32_t Q, uint32_t kq
     }
     bad |= x | ((((Q + 0x05050505u) | Q) | lo) & 0x80808080u);
     const uint32_t w = k + Q;                                                     // per byte, <= 126
-    const uint32_t hi = ((w >> 4) & 0x07070707u) | (k << 3);
-    const uint32_t lw = (w << 4) & 0xF0F0F0F0u;
+    const uint32_t hi = NARROW ? ((w >> 5) & 0x03030303u) | (k << 2) : ((w >> 4) & 0x07070707u) | (k << 3);
+    const uint32_t lw = NARROW ? (w << 3) & 0xF8F8F8F8u : (w << 4) & 0xF0F0F0F0u;
     return make_uint2(__builtin_amdgcn_perm(hi, lw, 0x05010400u), __builtin_amdgcn_perm(hi, lw, 0x07030602u));
 }
 
@@ -2490,6 +2510,80 @@ struct Evidence {
     uint64_t llr[NT];      // 16-bit fields A T C G: sums of the class rows' rounded-down LLR terms
     uint32_t cnt[NT];      // 6-bit counters: N A T C G
 };
+
+// The narrow evidence (common instantiation, records of at most 15 reads):
+// one 8-byte table row per (class, quality), the class's 16-bit field holding
+// llr8 << 4 | 1 (llr8 = the row's LLR term in 1/8 nat, rounded down, <= 273;
+// the low 4 bits count the class's rows), 'N' and masked rows 0.  A column's
+// sum is then one u64: field k = L_k << 4 | n_k, with no carry between fields
+// (15 rows: 15 * 273 < 2^12, n_k <= 15), and comparing fields compares L_k.
+template <int NT>
+struct Evidence8 {
+    uint64_t f[NT];
+};
+
+template <int NT, bool FULL>
+__device__ __forceinline__ void run_evidence8(Evidence8<NT> &ev, const uint8_t *lds, int R, uint32_t rmx, int crv,
+                                              int lane) {
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) ev.f[tt] = 0;
+    auto codes = [&](int r, uint32_t (&cd)[NT]) {
+        const int rr = min(r, R - 1);
+        const int cr = readlane(crv, rr);          // stage address of the read's column 0
+        if (FULL) {
+            const uint8_t *p = lds + cr + 2 * lane;
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) cd[tt] = *(const uint16_t *)(p + 128 * tt);
+        } else {
+            const int x = readlane((int)rmx, rr);
+            const int col = x & 255, len = (x >> 8) & 255;
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) {
+                const int t = 64 * tt + lane;
+                const uint32_t a = (uint32_t)(t - col) < (uint32_t)len ? (uint32_t)(cr + 2 * t) : (uint32_t)fk::kSent;
+                cd[tt] = *(const uint16_t *)(lds + a);
+            }
+        }
+    };
+    auto rows = [&](const uint32_t (&cd)[NT], uint2 (&f)[NT]) {
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) f[tt] = *(const uint2 *)(lds + cd[tt]);
+    };
+    // two reads per step: no field carries (above), so each 32-bit half is a
+    // three-input add (v_add3_u32)
+    auto add2 = [&](const uint2 (&f)[NT], const uint2 (&g)[NT]) {
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            const uint32_t lo = (uint32_t)ev.f[tt] + f[tt].x + g[tt].x;
+            const uint32_t hi = (uint32_t)(ev.f[tt] >> 32) + f[tt].y + g[tt].y;
+            ev.f[tt] = ((uint64_t)hi << 32) | lo;
+        }
+    };
+    uint32_t c0[NT], c1[NT];
+    codes(0, c0);
+    codes(1, c1);
+    int r = 0;
+    for (; r + 2 <= R; r += 2) {
+        uint2 f0[NT], f1[NT];
+        rows(c0, f0);
+        rows(c1, f1);
+        uint32_t n0[NT], n1[NT];
+        codes(r + 2, n0);
+        codes(r + 3, n1);
+        add2(f0, f1);
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            c0[tt] = n0[tt];
+            c1[tt] = n1[tt];
+        }
+    }
+    if (r < R) {
+        uint2 f0[NT];
+        rows(c0, f0);
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) ev.f[tt] += ((uint64_t)f0[tt].y << 32) | f0[tt].x;
+    }
+}
 
 // Evidence sums in read order (integer, so the order is free).  FULL: every
 // read covers every column (the C2 shape), so a read's codes are one base
@@ -2669,17 +2763,17 @@ struct Stamps {
 // phase 0: element codes of the prefetched bytes into the stage (dword d of
 // the record's bytes -> four codes at stage + 8 d); returns the lanes'
 // invalid-input flags
-template <bool DUPLEX, bool LO>
-__device__ __forceinline__ uint32_t stage_codes(const FastArgs &a, const RecMeta &m, const FastStage &st, uint8_t *lds,
-                                                int stage_addr, int lane) {
+template <bool DUPLEX, bool LO, bool NARROW, int NDW>
+__device__ __forceinline__ uint32_t stage_codes(const FastArgs &a, const RecMeta &m, const FastStage<NDW> &st,
+                                                uint8_t *lds, int stage_addr, int lane) {
     const int ndw = (int)(m.w >> 15);
     uint32_t bad = 0;
 #pragma unroll
-    for (int u = 0; u < kStageDw; ++u) {
+    for (int u = 0; u < NDW; ++u) {
         if (u * kWave < ndw) {
             if (u * kWave + lane < ndw) {
-                const uint2 c = LO ? make_codes4<DUPLEX, true>(st.vb[u], st.vq[u], a.kq, a.kqlo, bad)
-                                   : make_codes4<DUPLEX, false>(st.vb[u], st.vq[u], a.kq, a.kqlo, bad);
+                const uint2 c = LO ? make_codes4<DUPLEX, true, NARROW>(st.vb[u], st.vq[u], a.kq, a.kqlo, bad)
+                                   : make_codes4<DUPLEX, false, NARROW>(st.vb[u], st.vq[u], a.kq, a.kqlo, bad);
                 *(uint2 *)(lds + stage_addr + 8 * (u * kWave + lane)) = c;
             }
         }
@@ -2726,8 +2820,61 @@ __device__ __forceinline__ void send_to_general(const FastArgs &a, const RecMeta
 struct Staged {
     uint2 rm;      // the lane's read meta (single-strand: length after the 3' trim)
     int T;         // columns (:458-459, on the trimmed reads)
-    int state;     // 0 consensus here, 1 general kernel, 2 finished (status written)
+    int state;     // 0 consensus here, 1 general kernel, 2 finished (status written),
+                   // 3 consensus here, 3' trim checked after the evidence (finish_record)
+    uint32_t fl;   // state 3: the lane's read's first | last element code << 16 (loads in flight)
 };
+
+// trim_3prime_N (:292-325) on the staged codes: drop each read's trailing 'N'
+// (sequenced, or masked below min_base_quality, :280): codes of class N, from
+// the end.  T shrinks only when every read reaching it lost its tail; a read
+// left empty ends the record with the status compress_cigarlist([]) raises
+// (:740 via :322).  Returns 2 when that status was written, else 0.
+// an element's table row is an 'N' row (class N, or a quality masked below
+// min_base_quality, :280): wide rows count it in the N counter, narrow rows
+// are all zero
+template <bool NARROW>
+__device__ __forceinline__ bool row_is_n(const uint8_t *lds, uint32_t code) {
+    if (NARROW) {
+        const uint2 r = *(const uint2 *)(lds + code);
+        return (r.x | r.y) == 0u;
+    }
+    return (*(const uint32_t *)(lds + code + 8) & 63u) != 0u;
+}
+
+template <bool DUPLEX, bool NARROW>
+__device__ __forceinline__ int trim_walk(const FastArgs &a, const RecMeta &m, uint2 &rm, int &T, const uint8_t *lds,
+                                         int stage_addr, int lane) {
+    const int R = (int)(m.w & 127u);
+    const int x = (int)rm.x, y = (int)rm.y;
+    const int col = x & 255;
+    int tl = lane < R ? (x >> 8) & 255 : 0;
+    bool go = tl > 0;
+    while (__ballot(go)) {
+        if (go) {
+            const uint32_t code = *(const uint16_t *)(lds + stage_addr + 2 * (y + tl - 1));
+            // an 'N' row: sequenced 'N' or a masked quality (:280, folded into the table)
+            if (row_is_n<NARROW>(lds, code)) --tl; else go = false;
+            go = go && tl > 0;
+        }
+    }
+    if (lane < R && (a.want_info || tl == 0)) {
+        dcr_read_info inf;
+        inf.seq_start = m.base_al + y;
+        inf.len = tl;
+        inf.n_cig = tl > 0 ? 1 : 0;
+        inf.status = tl > 0 ? DCR_ST_OK : DCR_ST_INDEX_ERROR;   // compress_cigarlist([]) :740 via :322
+        inf.has_ins = 0;
+        lds_vptr<dcr_read_info>(lds, fk::kPInfo)[m.g0 + lane] = inf;
+    }
+    rm.x = (rm.x & ~0xFF00u) | ((uint32_t)tl << 8);
+    if (__ballot(lane < R && col + tl == T) == 0) T = wave_max(lane < R ? col + tl : 0);
+    if (__ballot(lane < R && tl == 0)) {
+        fast_status(lds, m.rec, DCR_ST_PREP | DCR_ST_INDEX_ERROR, lane);
+        return 2;
+    }
+    return 0;
+}
 
 // after the codes: 3' trim (single-strand), read info, T; invalid input -> general
 //
@@ -2739,11 +2886,15 @@ struct Staged {
 // :740 via :322), when it shrinks T (every read reaching the last column ends
 // in 'N'), or for the products of undecided columns (the pad quality is 2),
 // which the EXACT instantiation recomputes from scratch with the full trim.
-// QUICK therefore reads each read's first and last element only: a read
-// whose last element is a base keeps its length, one whose first element is
-// a base keeps at least one; when some read ending at T ends in a base, T
-// stays.  Anything else (and invalid input, whose record the general kernel
-// takes with the trimmed lengths) runs the full trim below.
+// A record whose reads all span its T columns (the C2 shape) is left to
+// finish_record (state 3): both conditions show in the evidence counts it
+// builds anyway (every read ends at column T - 1 and starts at column 0), so
+// no code is read back here.  Otherwise QUICK reads each read's first and
+// last element only: a read whose last element is a base keeps its length,
+// one whose first element is a base keeps at least one; when some read
+// ending at T ends in a base, T stays.  Anything else (and invalid input,
+// whose record the general kernel takes with the trimmed lengths) runs the
+// full trim.
 template <bool DUPLEX, bool QUICK>
 __device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &m, uint2 rm, uint32_t bad,
                                               const uint8_t *lds, int stage_addr, int lane) {
@@ -2751,51 +2902,38 @@ __device__ __forceinline__ Staged trim_record(const FastArgs &a, const RecMeta &
     const int R = (int)(m.w & 127u);
     s.T = (int)((m.w >> 7) & 255u);
     s.state = 0;
-    lds_fence();
     const bool any_bad = __ballot(bad != 0) != 0;
     if (!DUPLEX) {
-        // trim_3prime_N (:292-325): drop each read's trailing 'N' (sequenced, or
-        // masked below min_base_quality, :280): codes of class N, from the end
         const int x = (int)rm.x, y = (int)rm.y;
         const int col = x & 255;
-        int tl = lane < R ? (x >> 8) & 255 : 0;
+        const int tl = lane < R ? (x >> 8) & 255 : 0;
         bool full = true;
         if (QUICK && !a.want_info && !any_bad) {
+            if (DCR_TRIM2 && __ballot(lane < R && (col != 0 || tl != s.T)) == 0) {
+                // the first / last codes are only loaded here; finish_record
+                // reads them after the evidence, so no round trip is waited on
+                lds_fence();
+                const int yy = lane < R ? y : 0;
+                const uint32_t cf = *(const uint16_t *)(lds + stage_addr + 2 * yy);
+                const uint32_t cl = *(const uint16_t *)(lds + stage_addr + 2 * (yy + s.T - 1));
+                s.fl = cf | cl << 16;
+                s.rm = rm;
+                s.state = 3;
+                return s;
+            }
+            lds_fence();
             bool lastN = true, firstN = true;
             if (tl > 0) {
                 const uint32_t cl = *(const uint16_t *)(lds + stage_addr + 2 * (y + tl - 1));
                 const uint32_t cf = *(const uint16_t *)(lds + stage_addr + 2 * y);
-                lastN = (*(const uint32_t *)(lds + cl + 8) & 63u) != 0;
-                firstN = (*(const uint32_t *)(lds + cf + 8) & 63u) != 0;
+                lastN = row_is_n<QUICK>(lds, cl);
+                firstN = row_is_n<QUICK>(lds, cf);
             }
             full = __ballot(lane < R && lastN && firstN) != 0 || __ballot(lane < R && col + tl == s.T && !lastN) == 0;
         }
         if (full) {
-            bool go = tl > 0;
-            while (__ballot(go)) {
-                if (go) {
-                    const uint32_t code = *(const uint16_t *)(lds + stage_addr + 2 * (y + tl - 1));
-                    // an 'N' row: sequenced 'N' or a masked quality (:280, folded into the table)
-                    if (*(const uint32_t *)(lds + code + 8) & 63u) --tl; else go = false;
-                    go = go && tl > 0;
-                }
-            }
-            if (lane < R && (a.want_info || tl == 0)) {
-                dcr_read_info inf;
-                inf.seq_start = m.base_al + y;
-                inf.len = tl;
-                inf.n_cig = tl > 0 ? 1 : 0;
-                inf.status = tl > 0 ? DCR_ST_OK : DCR_ST_INDEX_ERROR;   // compress_cigarlist([]) :740 via :322
-                inf.has_ins = 0;
-                lds_vptr<dcr_read_info>(lds, fk::kPInfo)[m.g0 + lane] = inf;
-            }
-            rm.x = (rm.x & ~0xFF00u) | ((uint32_t)tl << 8);
-            // T shrinks only when every read reaching the untrimmed end lost its tail
-            if (__ballot(lane < R && col + tl == s.T) == 0) s.T = wave_max(lane < R ? col + tl : 0);
-            if (__ballot(lane < R && tl == 0)) {
-                fast_status(lds, m.rec, DCR_ST_PREP | DCR_ST_INDEX_ERROR, lane);
-                s.state = 2;
-            }
+            lds_fence();
+            s.state = trim_walk<DUPLEX, QUICK>(a, m, rm, s.T, lds, stage_addr, lane);
         }
     }
     s.rm = rm;
@@ -2816,34 +2954,66 @@ __device__ __forceinline__ double div1000(int k) {
 // Returns false (nothing written) when the record has a column the bound does
 // not decide and this is not the EXACT instantiation: the caller queues it for
 // the EXACT kernel, which computes those columns in the reference's arithmetic.
+// finish_record's outcomes: the caller queues the record for the EXACT
+// instantiation / the record's row was written (or, EXACT, its outputs) /
+// a status was written (nothing else to do)
+constexpr int kFinQueue = 0, kFinDone = 1, kFinStatus = 2;
+
 template <bool DUPLEX, int NT, bool EXACT>
-__device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &m, const Staged &sg, uint8_t *lds,
-                                              const int stage_addr, const int ov_addr, const int rm_addr, const int lane,
-                                              Stamps &sp, const double2 *xt, const uint32_t *r1, const double *qt) {
+__device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m, const Staged &sg, uint8_t *lds,
+                                             const int stage_addr, const int ov_addr, const int rm_addr, const int lane,
+                                             Stamps &sp, const double2 *xt, const uint32_t *r1, const double *qt,
+                                             const int fi) {
     const int64_t rec = m.rec;
     const int64_t off = m.off;
     const int R = (int)(m.w & 127u);
-    const int T = sg.T;
+    int T = sg.T;
     const int minpos = m.minpos;
-    const uint2 rm = sg.rm;
+    uint2 rm = sg.rm;
+    lds_fence();
     if (DCR_ABL == 1) {                 // diagnostic: staging only
         if (lane == 0) a.O.pos[rec] = *(const uint16_t *)(lds + stage_addr + 2 * (int)(rm.y & 7)) + m.d0;
-        return true;
+        return kFinDone;
     }
     const int colr = (int)(rm.x & 255u), lenr = (int)((rm.x >> 8) & 255u);
     const int crv = stage_addr + 2 * ((int)rm.y - colr);
-    Evidence<NT> ev;
-    if (__ballot(lane < R && (colr != 0 || lenr < T)) == 0) run_evidence<NT, true>(ev, lds, R, rm.x, crv, lane);
-    else run_evidence<NT, false>(ev, lds, R, rm.x, crv, lane);
+    Evidence<NT> ev;                     // EXACT: wide rows
+    Evidence8<NT> ev8;                   // common: narrow rows (R <= 15)
+    const bool full_cols = __ballot(lane < R && (colr != 0 || lenr < T)) == 0;
+    if constexpr (EXACT) {
+        if (full_cols) run_evidence<NT, true>(ev, lds, R, rm.x, crv, lane);
+        else run_evidence<NT, false>(ev, lds, R, rm.x, crv, lane);
+    } else {
+        if (full_cols) run_evidence8<NT, true>(ev8, lds, R, rm.x, crv, lane);
+        else run_evidence8<NT, false>(ev8, lds, R, rm.x, crv, lane);
+    }
     sp.mark(5);                          // [4] products
     if (DCR_ABL == 2) {                 // diagnostic: staging + products
         uint32_t x = 0;
 #pragma unroll
-        for (int tt = 0; tt < NT; ++tt) x += (uint32_t)ev.llr[tt] ^ (uint32_t)(ev.llr[tt] >> 32) ^ ev.cnt[tt];
+        for (int tt = 0; tt < NT; ++tt)
+            x += EXACT ? (uint32_t)ev.llr[tt] ^ (uint32_t)(ev.llr[tt] >> 32) ^ ev.cnt[tt]
+                       : (uint32_t)ev8.f[tt] ^ (uint32_t)(ev8.f[tt] >> 32);
         if (lane == 0) a.O.pos[rec] = (int)x;
-        return true;
+        return kFinDone;
     }
-
+    if (!EXACT && !DUPLEX && sg.state == 3) {
+        // the 3' trim of a record whose reads all span [0, T) (trim_record,
+        // QUICK): a read whose last element is a base keeps its length, one
+        // whose first element is a base keeps at least one, and T stays when
+        // some read ends in a base; otherwise the caller trims and comes back.
+        // An element is an 'N' row when its class is N or its quality is
+        // masked (:280): narrow code bank 0, or (code >> 3 & 127) - bank < min_bq.
+        auto is_n = [&](uint32_t c) {
+            const uint32_t k = c >> 10;
+            return k == 0u || (int)(((c >> 3) & 127u) - k) < a.minbq;
+        };
+        const bool lastN = is_n(sg.fl >> 16), firstN = is_n(sg.fl & 0xFFFFu);
+        if (__ballot(lane < R && lastN && firstN) != 0 || __ballot(lane < R && !lastN) == 0) {
+            // rare: the full trim (the evidence is unchanged, T may shrink)
+            if (trim_walk<DUPLEX, true>(a, m, rm, T, lds, stage_addr, lane) == 2) return kFinStatus;
+        }
+    }
     // decide every tile in registers (integer, straight-line): call, depth d
     // and errors e (:970-1021) as the column word d | e << 6 | call << 12
     const double *invd = (const double *)(lds + fk::kInvD);
@@ -2880,37 +3050,47 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     for (int tt = 0; tt < NT; ++tt) {
         const int t = 64 * tt + lane;
         const bool live = tt < NT - 1 || t < T;                      // only the last tile is partial
-        const uint32_t lo = (uint32_t)ev.llr[tt], hi = (uint32_t)(ev.llr[tt] >> 32);
-        // (LA, LC) and (LT, LG) as 16-bit pairs: one packed max / min gives both halves
+        const uint64_t sum = EXACT ? ev.llr[tt] : ev8.f[tt];
+        const uint32_t lo = (uint32_t)sum, hi = (uint32_t)(sum >> 32);
+        // (A, C) and (T, G) fields as 16-bit pairs: one packed max / min gives both halves
         const u16x2 P1 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi, lo, 0x05040100u));
         const u16x2 P2 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi, lo, 0x07060302u));
         const u16x2 M = __builtin_elementwise_max(P1, P2), N = __builtin_elementwise_min(P1, P2);
-        const uint32_t Lb = max((uint32_t)M.x, (uint32_t)M.y);
-        const uint32_t L2 = max(min((uint32_t)M.x, (uint32_t)M.y), max((uint32_t)N.x, (uint32_t)N.y));   // second largest
-        uint32_t kb = (uint32_t)P1.y == Lb ? 2u : 3u;                // the first largest ("ATCG")
-        kb = (uint32_t)P2.x == Lb ? 1u : kb;
-        kb = (uint32_t)P1.x == Lb ? 0u : kb;
-        const uint32_t cnt = ev.cnt[tt];
-        const int d = R - (int)(cnt & 63u);                                       // rows that are not 'N'
-        const int nb = (int)__builtin_amdgcn_ubfe(cnt, 6u * kb + 6u, 6u);
+        const uint32_t top = max((uint32_t)M.x, (uint32_t)M.y);
+        const uint32_t sec = max(min((uint32_t)M.x, (uint32_t)M.y), max((uint32_t)N.x, (uint32_t)N.y));   // second largest
+        uint32_t kb = (uint32_t)P1.y == top ? 2u : 3u;               // the first largest ("ATCG")
+        kb = (uint32_t)P2.x == top ? 1u : kb;
+        kb = (uint32_t)P1.x == top ? 0u : kb;
+        uint32_t Lb, L2;
+        int d, nb;
+        if constexpr (EXACT) {
+            const uint32_t cnt = ev.cnt[tt];
+            Lb = top;
+            L2 = sec;
+            d = R - (int)(cnt & 63u);                                             // rows that are not 'N'
+            nb = (int)__builtin_amdgcn_ubfe(cnt, 6u * kb + 6u, 6u);
+        } else {
+            // fields L << 4 | n: a decided column's call has the unique largest
+            // L, so its field is the largest and carries its row count; the
+            // rows that are not 'N' are the four counts (one byte permute, the
+            // low nibbles, a byte sum)
+            Lb = top >> 4;
+            L2 = sec >> 4;
+            nb = (int)(top & 15u);
+            d = (int)__builtin_amdgcn_sad_u8(__builtin_amdgcn_perm(hi, lo, 0x06040200u) & 0x0F0F0F0Fu, 0u, 0u);
+        }
         const int e = R - nb;                                                     // rows that differ from the call
-        // decided: LLR_b - max(LLR_k, 0) >= (Lb - L2 - (d - nb)) / 16 >= T16 / 16
-        const bool undecided = (int)(Lb - L2) - (d - nb) < a.t16 || force;
+        // decided: LLR_b - max(LLR_k, 0) >= (Lb - L2 - (d - nb)) / u >= margin / u
+        // (u = 16 wide, 8 narrow)
+        const bool undecided = (int)(Lb - L2) - (d - nb) < (EXACT ? a.t16 : a.t8) || force;
         und |= (uint32_t)(live && undecided) << tt;
-        if (EXACT || R > 16) *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (kb << 12));
+        if (EXACT) *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (kb << 12));
         if (!EXACT && DCR_ABL != 5 && t < T16) {
-            if (DCR_STORE_MODE) {
-                const uint32_t ut = (uint32_t)t, ut2 = 2u * ut;
-                *(DCR_G uint16_t *)((DCR_G uint8_t *)pd + ut2) = (uint16_t)d;
-                *(DCR_G uint16_t *)((DCR_G uint8_t *)pe + ut2) = (uint16_t)e;
-                ps[ut] = (uint8_t)(t < T ? __builtin_amdgcn_perm(0u, 0x47435441u, kb) : 0x4Eu);   // "ATCG"[call]
-                pq[ut] = (uint8_t)(t < T ? (uint32_t)a.maxq : 0u);
-            } else {
-                pd[t] = (uint16_t)d;
-                pe[t] = (uint16_t)e;
-                ps[t] = (uint8_t)(t < T ? __builtin_amdgcn_perm(0u, 0x47435441u, kb) : 0x4Eu);
-                pq[t] = (uint8_t)(t < T ? (uint32_t)a.maxq : 0u);
-            }
+            const uint32_t ut = (uint32_t)t, ut2 = 2u * ut;
+            *(DCR_G uint16_t *)((DCR_G uint8_t *)pd + ut2) = (uint16_t)d;
+            *(DCR_G uint16_t *)((DCR_G uint8_t *)pe + ut2) = (uint16_t)e;
+            ps[ut] = (uint8_t)(t < T ? __builtin_amdgcn_perm(0u, 0x47435441u, kb) : 0x4Eu);   // "ATCG"[call]
+            pq[ut] = (uint8_t)(t < T ? (uint32_t)a.maxq : 0u);
         }
         fx += live ? __umul24((uint32_t)e, m720[d]) : 0u;
         dmax = max(dmax, live ? d : -1);
@@ -2923,7 +3103,7 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     // that is not 'N' (:770-790), still one M run (no '+' / '-' rows here).
     int first = 0, last = T - 1;
     const bool exact = __ballot(und) != 0;
-    if (!EXACT && exact) return false;
+    if (!EXACT && exact) return kFinQueue;
     // exact columns' character | quality << 8, as u16 per column in the wave's
     // read-word LDS (free once the read words are in registers)
     uint16_t *chq = (uint16_t *)(lds + rm_addr);
@@ -3038,7 +3218,7 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         first = wave_min(fst);
         last = wave_max(lst);
         // all 'N' (compress_cigarlist([]) :740 raises) or an unrepresentable column
-        if (__ballot(fail) || last < 0) { send_to_general<DUPLEX>(a, m, rm, lds, lane); return true; }
+        if (__ballot(fail) || last < 0) { send_to_general<DUPLEX>(a, m, rm, lds, lane); return kFinStatus; }
         // characters / qualities of the kept span into the (now free) stage, shifted to its start
         lds_fence();
         uint8_t *sb = lds + stage_addr + 0x800;
@@ -3104,10 +3284,12 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     // numpy's; a tie, or any other record, takes the double sum below.
     double E = 0.0;
     uint32_t E_lo = 0, E_hi = 0;         // E's words, scalar registers
-    bool slow = exact || R > 16 || DCR_ABL == 4;
+    uint32_t S = 0;                      // the rational mean's numerator (rows: k_fast_rows rounds it)
+    // (the common instantiation holds records of at most 15 reads)
+    bool slow = EXACT ? (exact || R > 16 || DCR_ABL == 4) : false;
     if (!slow) {
-        const uint32_t S = (uint32_t)wave_sum((int)fx);
-        if (DCR_MEAN_MODE == 0) {
+        S = (uint32_t)wave_sum((int)fx);
+        if (EXACT || !DCR_ROWS) {
             // the rational 25 S / (18018 T) in doubles: k = rint, remainder exact
             const int64_t num = 25 * (int64_t)S;
             const int den = 18018 * T;
@@ -3120,38 +3302,10 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
             const double Ed = div1000(k);
             E_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)__double_as_longlong(Ed));
             E_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)__double_as_longlong(Ed) >> 32));
-        } else {
-            // k = round(25 S / (18018 T)) by restoring division in scalar
-            // registers (S and T are wave-uniform; 25 S < 2^32 for T <= 238,
-            // and the quotient is at most 1000 < 2^10); a tie (2 r = den) or
-            // T > 238 takes the double path
-            const uint32_t num = 25u * S, den = 18018u * (uint32_t)T;
-            uint32_t q = 0, r = num;
-#pragma unroll
-            for (int b = 9; b >= 0; --b) {
-                const uint32_t dv = den << b;
-                if (r >= dv) {
-                    r -= dv;
-                    q |= 1u << b;
-                }
-            }
-            const uint32_t k = q + (2u * r > den ? 1u : 0u);
-            slow = 2u * r == den || k > 1000u || T > 238;
-            if (DCR_MEAN_MODE == 2) {
-                // E = k / 1000 correctly rounded from the host's table (a scalar load)
-                const DCR_C uint2 *tab = (const DCR_C uint2 *)lds_ptr<const uint2>(lds, fk::kPE1000);
-                const uint2 Ew = tab[min(k, 1000u)];
-                E_lo = Ew.x;
-                E_hi = Ew.y;
-            } else {
-                const double Ed = div1000((int)min(k, 1000u));
-                E_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)__double_as_longlong(Ed));
-                E_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)__double_as_longlong(Ed) >> 32));
-            }
+            // the common kernel kept no column words for the double walk: the
+            // EXACT kernel takes the record (a tie is rare)
+            if (!EXACT && slow) return kFinQueue;
         }
-        // the common kernel kept no column words for the double walk: the
-        // EXACT kernel takes the record (a tie is rare)
-        if (!EXACT && slow) return false;
     }
     if (slow) {
     double sum = 0.0;
@@ -3176,6 +3330,8 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     if (__builtin_expect(__builtin_fabs(fr - 0.5) > 1e-9 * (1.0 + y), 1) && DCR_ABL != 4) {
         const double ky = __builtin_rint(y);
         E = ky >= 0.0 && ky <= 1000.0 ? div1000((int)ky) : ky / 1000.0;
+    } else if (!EXACT) {
+        return kFinQueue;                // near a half-integer: the EXACT pass walks numpy's pairwise sum
     } else {
         lds_fence();
         double *et = (double *)(lds + stage_addr);
@@ -3198,6 +3354,30 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
     E_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)__double_as_longlong(E) >> 32));
     }
     sp.mark(9);                          // [8] mean
+    if (!EXACT && DCR_ROWS) {
+        // the record's scalars as one 16-byte row at its fast-list index
+        // (k_fast_rows expands it into the ten dcr_out arrays and rounds the
+        // mean): pos (:790, first = 0 here), T | D << 8 | M << 16 | MAPQ << 24
+        // (len = n_de = T, one M run), S, kind 1; a mean computed here in
+        // doubles (R > 16) is stored directly, kind 2
+        const int mapq = (int)((uint32_t)m.d0 >> 16);
+        uint32_t v = 0;
+        v = write_lane<0>(v, __builtin_amdgcn_readfirstlane((uint32_t)minpos));
+        v = write_lane<1>(v, __builtin_amdgcn_readfirstlane((uint32_t)T | (uint32_t)Dmax << 8 | (uint32_t)Dmin << 16 |
+                                                            (uint32_t)mapq << 24));
+        v = write_lane<2>(v, __builtin_amdgcn_readfirstlane(S));
+        v = write_lane<3>(v, slow ? 2u : 1u);
+        v = write_lane<7>(v, E_lo);
+        v = write_lane<8>(v, E_hi);
+        if (lane < 4) {
+            lds_sgptr<uint32_t>(lds, fk::kPRows)[4 * fi + lane] = v;
+        } else if (slow && (lane == 7 || lane == 8)) {
+            const uint64_t pw = *(const uint64_t *)(lds + fk::kPtrs + 8 * lane);
+            *(DCR_G uint32_t *)((pw & 0x00FFFFFFFFFFFFFFull) + ((uint64_t)rec << (pw >> 56))) = v;
+        }
+        sp.mark(10);                     // [9] record scalars
+        return kFinDone;
+    }
     // the record's scalar fields straight into the dcr_out arrays: lane k
     // stores field k (pos :790, MAPQ, len, n_cig, n_de, D, M, E as two words,
     // the single M run of the kept columns), lane 10 the status byte.  The
@@ -3216,7 +3396,7 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         v = write_lane<7>(v, E_lo);
         v = write_lane<8>(v, E_hi);
         v = write_lane<9>(v, __builtin_amdgcn_readfirstlane((uint32_t)klen << 4));
-        DCR_G uint8_t *sb = DCR_SCAL_MODE ? lds_sgptr<uint8_t>(lds, fk::kPSbase) : nullptr;
+        DCR_G uint8_t *sb = lds_sgptr<uint8_t>(lds, fk::kPSbase);
         if (sb && lane < 10) {
             // the ten arrays lie within 4 GiB above sbase (checked by the
             // host): lane k stores at a 32-bit offset from that one base
@@ -3233,7 +3413,7 @@ __device__ __forceinline__ bool finish_record(const FastArgs &a, const RecMeta &
         }
     }
     sp.mark(10);                         // [9] record scalars
-    return true;
+    return kFinDone;
 }
 
 __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
@@ -3261,8 +3441,9 @@ __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
 // columns in the reference's double arithmetic.  The common kernel thus keeps
 // none of the exact path's code or registers.
 template <bool DUPLEX, bool EXACT>
-__global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : 5) void k_consensus_fast(FastArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[fk::kLdsBytes];
+__global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : DCR_FAST_OCC) void k_consensus_fast(FastArgs a) {
+    using RG = fk::Region<EXACT>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[RG::kLds];
     // Record assignment, XCD-aware: the blocks of one group (blockIdx % 8,
     // the blocks that share an XCD and its L2) take one contiguous range of
     // the list, interleaved over the group's waves, so the records in flight
@@ -3314,11 +3495,18 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : 5) void k_consensus_
     for (int i = threadIdx.x; i < 5 * (fk::kRowMax + 1); i += fk::kBlockThreads) {
         const int k = i / (fk::kRowMax + 1), q = i % (fk::kRowMax + 1);
         const bool nrow = k == 0 || q < a.minbq;          // 'N', or masked below min_base_quality (:280)
-        const uint64_t inc = nrow ? 0ull : (uint64_t)a.llr16[q] << (16 * (k - 1));
-        *(uint4 *)(lds + 0x800 * k + 16 * (q + k)) = make_uint4((uint32_t)inc, (uint32_t)(inc >> 32), nrow ? 1u : 1u << (6 * k), 0u);
+        if (EXACT) {
+            const uint64_t inc = nrow ? 0ull : (uint64_t)a.llr16[q] << (16 * (k - 1));
+            *(uint4 *)(lds + 0x800 * k + 16 * (q + k)) =
+                make_uint4((uint32_t)inc, (uint32_t)(inc >> 32), nrow ? 1u : 1u << (6 * k), 0u);
+        } else {
+            // narrow row (Evidence8): field k - 1 = llr8 << 4 | 1, 'N' rows 0
+            const uint64_t inc = nrow ? 0ull : (uint64_t)(((uint32_t)a.llr8[q] << 4) | 1u) << (16 * (k - 1));
+            *(uint2 *)(lds + 0x400 * k + 8 * (q + k)) = make_uint2((uint32_t)inc, (uint32_t)(inc >> 32));
+        }
     }
     if (threadIdx.x < 64) ((double *)(lds + fk::kInvD))[threadIdx.x] = threadIdx.x == 0 ? 0.0 : 1.0 / (double)threadIdx.x;
-    if (threadIdx.x == 0) *(uint16_t *)(lds + fk::kSent) = (uint16_t)fk::kPadCode;
+    if (threadIdx.x == 0) *(uint16_t *)(lds + fk::kSent) = (uint16_t)(EXACT ? fk::kPadCode : fk::kPadCode8);
     if (threadIdx.x < 64) {
         const int t = threadIdx.x;
         ((uint32_t *)(lds + fk::kM720))[t] = t == 0 || t > 16 ? 0u : 720720u / (uint32_t)t;
@@ -3346,15 +3534,16 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : 5) void k_consensus_
         case fk::kPParams: v = (uint64_t)(uintptr_t)a.P; break;
         case fk::kPSbase: v = (uint64_t)(uintptr_t)a.sbase; break;
         case fk::kPE1000: v = (uint64_t)(uintptr_t)a.e1000; break;
+        case fk::kPRows: v = (uint64_t)(uintptr_t)a.rows; break;
         default: v = scalar_dest(a.O, k); break;
         }
         *(uint64_t *)(lds + fk::kPtrs + 8 * k) = v;
     }
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane0 = threadIdx.x & 63;
-    const int stage_addr = fk::stage_base(wave);
-    const int rm_addr = fk::kRm + wave * kWave * 8;
-    const int ov_addr = fk::kOv + wave * 512;
+    const int stage_addr = RG::base(wave);
+    const int rm_addr = stage_addr + RG::kRm;
+    const int ov_addr = stage_addr + RG::kOv;
     __syncthreads();
     int i = first_i + wave;
     if (i >= hi) return;
@@ -3364,7 +3553,7 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : 5) void k_consensus_
     int i1 = nxt(i), i2 = nxt(i1);
     RecMeta m0 = ML[midx(i)];
     RecMeta m1 = ML[midx(i1)];
-    FastStage st;
+    FastStage<RG::kDw> st;
     fast_load<DUPLEX>(a, m0, ML + midx(i2), lane0, st);
     Stamps sp;
     int pend = 0, npend = 0;           // !EXACT: queued fast-list indices (lane p holds the p-th)
@@ -3386,11 +3575,15 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : 5) void k_consensus_
         // every column decided by the bound (one to three reads stay below
         // maxQ wherever a read is masked or disagrees): they go to the exact
         // queue untouched instead of being staged here and again there
-        const bool direct = !EXACT && !DUPLEX && (int)(m0.w & 127u) <= a.direct_r;
+        // so do records larger than this instantiation's stage (common: more
+        // than 1,536 bytes; the EXACT instantiation stages up to 2,048)
+        // and so do records of more than 15 reads (the narrow rows' counts)
+        const bool direct = !EXACT && ((!DUPLEX && (int)(m0.w & 127u) <= a.direct_r) ||
+                                       (int)(m0.w >> 15) > RG::kDw * kWave || (int)(m0.w & 127u) > 15 || !a.narrow);
         uint32_t bad = 0;
         if (!direct) {
-            bad = a.lo_check ? stage_codes<DUPLEX, true>(a, m0, st, lds, stage_addr, lane)
-                             : stage_codes<DUPLEX, false>(a, m0, st, lds, stage_addr, lane);
+            bad = a.lo_check ? stage_codes<DUPLEX, true, !EXACT>(a, m0, st, lds, stage_addr, lane)
+                             : stage_codes<DUPLEX, false, !EXACT>(a, m0, st, lds, stage_addr, lane);
             // the read words go through LDS: a register copy of them would live
             // across the prefetch's refill of st and force a wait for it at the
             // loop's back edge
@@ -3411,7 +3604,13 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : 5) void k_consensus_
         const uint2 rm = make_uint2((uint32_t)(((int)rw.x >> 16) + (m0.d0 & 0xFFFF)) | (rw.x & 0xFFFFu) << 8,
                                     rw.y - m0.base_al);
         const RecMeta m2 = meta_from_lanes(*(const uint32_t *)(lds + fk::kMv + 32 * wave + 4 * (lane & 7)));   // record i2
+        // a record this kernel does not decide gets an empty row (kind 0:
+        // k_fast_rows leaves its scalars to the kernel that finishes it)
+        auto no_row = [&]() {
+            if (!EXACT && DCR_ROWS && lane == 3) lds_sgptr<uint32_t>(lds, fk::kPRows)[4 * i + 3] = 0u;
+        };
         if (direct) {
+            no_row();
             if (lane == npend) pend = i;
             if (++npend == kWave) flush(lane);
             i += step;
@@ -3425,16 +3624,20 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : 5) void k_consensus_
         sp.mark(4);                    // [3] trim, fence
         if (sg.state == 1) {
             send_to_general<DUPLEX>(a, m0, sg.rm, lds, lane);
-        } else if (sg.state == 0) {
-            bool done;
-            if (sg.T <= 64) done = finish_record<DUPLEX, 1, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt);
-            else if (sg.T <= 128) done = finish_record<DUPLEX, 2, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt);
-            else if (sg.T <= 192) done = finish_record<DUPLEX, 3, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt);
-            else done = finish_record<DUPLEX, 4, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt);
-            if (!EXACT && !done) {
+            no_row();
+        } else if (sg.state == 0 || sg.state == 3) {
+            int fin;
+            if (sg.T <= 64) fin = finish_record<DUPLEX, 1, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt, i);
+            else if (sg.T <= 128) fin = finish_record<DUPLEX, 2, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt, i);
+            else if (sg.T <= 192) fin = finish_record<DUPLEX, 3, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt, i);
+            else fin = finish_record<DUPLEX, 4, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt, i);
+            if (!EXACT && fin != kFinDone) no_row();
+            if (!EXACT && fin == kFinQueue) {
                 if (lane == npend) pend = i;
                 if (++npend == kWave) flush(lane);
             }
+        } else {
+            no_row();
         }
         i += step;
         if (i >= hi) break;
@@ -3446,6 +3649,44 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : 5) void k_consensus_
     if (DCR_STAMP && lane0 == 0)
         for (int k = 0; k < 10; ++k)   // fast ss 0-9, ds 16-25; exact ss 32-41, ds 48-57
             atomicAdd(&a.stamps[k + (DUPLEX ? 16 : 0) + (EXACT ? 32 : 0)], (unsigned long long)sp.acc[k]);
+}
+
+// Expands the rows k_consensus_fast wrote for the records it decided (one
+// lane per fast-list entry; entries are in record order within a wave's
+// range, so the ten stores per lane coalesce across the wave) and rounds the
+// mean: E = round(mean(e/d), 3) (:1015-1018) is the rational
+// 1000 sum(e/d) / T = 25 S / (18018 T) (S = 720720 sum(e/d), exact for depths
+// <= 16) rounded half-even; away from a tie it lies >= 1 / (2 * 18018 T)
+// > 1e-7 from a half-integer, beyond the reference's own double rounding
+// (< 1e-9), so numpy's rint agrees.  A tie is left to the EXACT pass (the
+// double pairwise walk): the record goes on its queue.  Kind 2 rows carry an
+// E the fast kernel stored itself.
+__global__ __launch_bounds__(256) void k_fast_rows(FastArgs a) {
+    const int i = (int)(blockIdx.x * 256u + threadIdx.x);
+    if (i >= *a.fast_count) return;
+    const uint4 row = a.rows[i];
+    if (row.w == 0u) return;
+    const RecMeta m = a.meta[i];
+    const int64_t rec = m.rec;
+    const uint32_t T = row.y & 255u;
+    if (row.w == 1u) {
+        const uint64_t num = 25ull * row.z, den = 18018ull * T;
+        const uint64_t q = num / den, r = num - q * den;
+        if (2 * r == den) {
+            a.xlist[atomicAdd(a.xcount, 1)] = i;
+            return;
+        }
+        a.O.E[rec] = div1000((int)(q + (2 * r > den ? 1u : 0u)));
+    }
+    a.O.pos[rec] = (int32_t)row.x;
+    a.O.mapq[rec] = (int32_t)(row.y >> 24);
+    a.O.len[rec] = (int32_t)T;
+    a.O.n_cig[rec] = 1;
+    a.O.n_de[rec] = (int32_t)T;
+    a.O.D[rec] = (int32_t)((row.y >> 8) & 255u);
+    a.O.M[rec] = (int32_t)((row.y >> 16) & 255u);
+    a.O.cigar[m.off] = T << 4;                   // one M run of the kept columns
+    a.O.status[rec] = DCR_ST_OK;
 }
 
 // persistent: drains the general list written by k_recmeta.  A wave takes
