@@ -105,13 +105,23 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def sscs_algorithmic_bytes(packed):
+def sscs_algorithmic_bytes(packed, padded=False):
     """sum_r(2 len_r + 4 n_cig_r + 4 + 1) + T*(2 + 4) + 16 per
-    subfamily, with T the subfamily's output region (T_ub rounded to 16)."""
+    subfamily, T = max(pos_r + len_r) - min(pos_r) (:458-459, on the input
+    reads' query lengths: 150 on C2).  ``padded``: T is the subfamily's output
+    region instead (T rounded up to 16 columns, the bytes the kernel stores)."""
     per_read = 2 * packed.seq_len.astype(np.int64) + 4 * packed.cig_n.astype(np.int64) + 5
     reads_b = int(per_read.sum())
-    cols = int(packed.ss_col_off[-1])
     n_sub = len(packed.ss_col_off) - 1
+    if padded:
+        cols = int(packed.ss_col_off[-1])
+    else:
+        so = packed.sub_off.astype(np.int64)
+        pos = packed.read_pos.astype(np.int64)
+        end = pos + packed.seq_len.astype(np.int64)
+        nonempty = so[1:] > so[:-1]
+        starts = so[:-1][nonempty]
+        cols = int((np.maximum.reduceat(end, starts) - np.minimum.reduceat(pos, starts)).sum()) if len(starts) else 0
     return reads_b + 6 * cols + 16 * n_sub
 
 
@@ -337,6 +347,9 @@ def main():
     ap.add_argument("--sharded-input-of-rank0", action="store_true",
                     help="strong scaling: ONE input of rank 0's batch only, split over the N ranks")
     ap.add_argument("--in-level", type=int, default=1, help="BGZF compression level of the synthetic input BAM")
+    ap.add_argument("--level6-passes", type=int, default=2,
+                    help="single GPU: timed CLI passes over the same families written at BGZF level 6 "
+                         "(reported beside the headline in config; 0 skips)")
     ap.add_argument("--max-reads", type=int, default=None,
                     help="--max_reads of the CLI runs (default: the reference's 100; C4: 1000, the whole deep "
                          "subfamilies).  Below a config's subfamily sizes the CLI downsamples (random.seed(4)); "
@@ -396,7 +409,7 @@ def main():
         workdir = wd[0]
     else:
         workdir = tempfile.mkdtemp(prefix=f"dcr_bench_r{rank}_", dir=os.environ.get("DCR_BENCH_DIR"))
-    stats, e2e_s = {}, None
+    stats, e2e_s, level6 = {}, None, None
     try:
         if not args.kernel_only:
             bam_path = os.path.join(workdir, "in.bam")
@@ -423,6 +436,21 @@ def main():
                 tdist.barrier()
             log(f"[rank {rank}] {args.steps} CLI passes in {e2e_s:.2f} s: "
                 f"{ {k: v for k, v in stats.items() if k != 'ranks'} }")
+            if args.level6_passes > 0 and not dist and not args.sharded and args.in_level != 6:
+                # the same families from a level-6 input (a BAM as aligners
+                # write it): more inflate work per byte, not the headline
+                bam6 = os.path.join(workdir, "in6.bam")
+                t0 = time.perf_counter()
+                synth.write_packed_bam(bam6, src, seed=args.seed, level=6)
+                log(f"[rank {rank}] wrote {os.path.getsize(bam6) / 1e6:.0f} MB BAM (level 6) in "
+                    f"{time.perf_counter() - t0:.1f} s")
+                os.remove(bam_path)
+                torch.cuda.synchronize()
+                s6, st6 = e2e_passes(bam6, params_args, local, args.level6_passes, 0, workdir)
+                level6 = {"value": st6.get("consensus_bases", 0) * args.level6_passes / s6,
+                          "unit": "consensus bases/s", "passes_s": st6.get("passes_s"),
+                          "input_bytes": os.path.getsize(bam6)}
+                log(f"[rank {rank}] level-6 input: {level6['value'] / 1e6:.1f} M consensus bases/s")
     finally:
         if rank == 0 or not args.sharded:
             shutil.rmtree(workdir, ignore_errors=True)
@@ -451,8 +479,10 @@ def main():
 
     if rank == 0:
         alg = sscs_algorithmic_bytes(packed)
+        alg_padded = sscs_algorithmic_bytes(packed, padded=True)
         if args.config == "C2":
-            dom, dom_label = "k_consensus_fast<ss>", "k_consensus_fast<false, false> (single-strand consensus)"
+            dom, dom_label = "k_consensus_fast<ss>", ("k_consensus_fast<false, false> + k_fast_rows (single-strand "
+                                                      "consensus; the HIP-event slot spans both launches)")
             dom_ms = kavg[dom]
             traffic, tsrc = load_traffic("k_consensus_fast<false, false>", packed.n_fam)
         else:
@@ -481,6 +511,7 @@ def main():
                             f"; ONE input of {packed.n_reads} reads split over the {world} GPU(s) by the sharded CLI")
                            if args.sharded and dist else ""),
                        "value_is": value_kind, "input_bgzf_level": args.in_level, "max_reads": max_reads,
+                       "whole_node_level6_input": level6,
                        "input_reads_per_gpu": (bam_packed if bam_packed is not None else packed).n_reads,
                        "families_per_gpu": packed.n_fam, "reads_per_gpu": packed.n_reads,
                        "input_bases_per_s": (in_bases / slowest) if slowest else None,
@@ -499,6 +530,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": dom_label,
                          "kernel_ms": dom_ms, "algorithmic_bytes_per_launch": alg,
+                         "algorithmic_T": "max(pos + len) - min(pos) per subfamily (SURVEY §8d)",
+                         "achieved_padded": alg_padded / (dom_ms / 1000.0) / 1e9,
+                         "frac_padded": alg_padded / (dom_ms / 1000.0) / 1e9 / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_launch_padded": alg_padded,
                          "traffic_source": (f"profiles/traffic.json ({tsrc.get('source', '')})" if tsrc else None)},
         }
         if not args.no_cpu and world == 1:

@@ -139,10 +139,12 @@ static int fast_allowed(const dcr_params *p) {
 //              double (e^-700 > DBL_MIN = e^-708.4).
 //              Above it the reference's products can underflow to 0 (S = 0, NaN posterior, call
 //              'A' :613), which the LLR bound does not see: every column then takes the exact path.
-//   llr8[q], t8: the same in 1/8 nat for the common fast instantiation's
-//              narrow rows (dcr_kernels.hip, Evidence8: 15 rows of llr8 <= 273 fit
-//              12 bits); narrow = 0 when some llr8 does not fit (then that
-//              instantiation queues every record for the EXACT one)
+//   llrn[q], tn: the same in 1/u nat for the common fast instantiation's
+//              narrow rows (dcr_kernels.hip, Evidence8: 15 rows of at most 273
+//              fit 12 bits), u = 16 when every row fits (default parameters:
+//              qualities capped at max_base_quality 60 give <= 246), else 8, else
+//              4; narrow = 0 when none does (then that instantiation queues every
+//              record for the EXACT one)
 // Returns 0 when the decision cannot be made for these parameters (then every
 // record takes the general kernel).
 static int fast_constants(const dcr_params &hp, uint16_t llr16[128], uint16_t llr8[128], uint32_t &kq, uint32_t &kqlo,
@@ -154,24 +156,30 @@ static int fast_constants(const dcr_params &hp, uint16_t llr16[128], uint16_t ll
     while (qlo > 0 && hp.mismatch[qlo - 1] > 0.0 && hp.match[qlo - 1] >= hp.mismatch[qlo - 1]) --qlo;
     kqlo = (uint32_t)(0x80 - qlo) * 0x01010101u;
     qlo_out = qlo;
-    narrow = 1;
+    double lmax = 0.0;
     for (int q = 0; q < 128; ++q) {
         llr16[q] = 0;
-        llr8[q] = 0;
         if (q >= qlo && q <= 122) {
             const double v = std::floor(16.0 * std::log(hp.match[q] / hp.mismatch[q]) - 1e-6);
             if (!(v <= 1040.0)) return 0;                  // 63 rows must fit a 16-bit field
             llr16[q] = (uint16_t)std::max(v, 0.0);
-            const double v8 = std::floor(8.0 * std::log(hp.match[q] / hp.mismatch[q]) - 1e-6);
-            if (!(v8 <= 273.0)) narrow = 0;                // 15 rows must fit 12 bits
-            else llr8[q] = (uint16_t)std::max(v8, 0.0);
+            lmax = std::max(lmax, std::log(hp.match[q] / hp.mismatch[q]));
         }
+    }
+    // the narrow rows' unit: 15 rows must fit 12 bits
+    int un = 16;
+    while (un > 4 && std::floor(un * lmax - 1e-6) > 273.0) un /= 2;
+    narrow = std::floor(un * lmax - 1e-6) <= 273.0 ? 1 : 0;
+    for (int q = 0; q < 128; ++q) {
+        llr8[q] = 0;
+        if (narrow && q >= qlo && q <= 122)
+            llr8[q] = (uint16_t)std::max(std::floor(un * std::log(hp.match[q] / hp.mismatch[q]) - 1e-6), 0.0);
     }
     const int mq = std::min(std::max(hp.max_base_quality, 0), DCR_MAX_QTHRESH - 1);
     const double cc = std::min(std::min(hp.qthresh[mq], 1.0 - hp.post_threshold), 0.25);
     if (!(cc > 1e-12)) return 0;
     t16 = (int)std::ceil(16.0 * std::log(5.0 / cc)) + 1;
-    t8 = (int)std::ceil(8.0 * std::log(5.0 / cc)) + 1;
+    t8 = (int)std::ceil(un * std::log(5.0 / cc)) + 1;
     double cmax = 0.0;                                 // per-row bound on -ln(factor), either factor
     for (int q = 0; q <= 122; ++q) {
         cmax = std::max(cmax, -std::log(hp.mismatch[q]));

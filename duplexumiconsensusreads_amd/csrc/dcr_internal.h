@@ -101,8 +101,8 @@ struct FastArgs {
     int minbq;                      // single-strand: min_base_quality (masked rows in the table); duplex: -1
     int lo_check;                   // some unmasked quality may lie below fast_qlo: check the bytes
     const uint16_t *llr16;          // [123] per-quality LLR term, 1/16 nat, rounded down (EXACT's wide rows)
-    const uint16_t *llr8;           // [123] the same in 1/8 nat (the common instantiation's narrow rows)
-    int t8;                         // decision margin in 1/8 nat
+    const uint16_t *llr8;           // [123] the same in 1/u nat, u = 16, 8 or 4 (the common instantiation's narrow rows)
+    int t8;                         // decision margin in 1/u nat
     int narrow;                     // llr8 fits the narrow rows (else the common kernel queues every record)
     const double *e1000;            // [1001] k / 1000 correctly rounded (numpy round(x, 3) = rint(1000 x) / 1000)
     // record scalars (pos, mapq, len, n_cig, n_de, D, M, E lo, E hi, cigar):

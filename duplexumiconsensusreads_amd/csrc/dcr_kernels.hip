@@ -36,7 +36,7 @@
 #define DCR_STAMP 0   // diagnostic builds only (tools/stamps.py): per-phase s_memtime cycle totals
 #endif
 #ifndef DCR_FAST_OCC
-#define DCR_FAST_OCC 6   // fast kernel (common instantiation): waves per SIMD the launch bounds ask for
+#define DCR_FAST_OCC 7   // fast kernel (common instantiation): waves per SIMD the launch bounds ask for
 #endif
 #ifndef DCR_TRIM2
 #define DCR_TRIM2 1   // fast kernel: the 3' trim of C2-shaped records checked from the evidence counts
@@ -2417,6 +2417,7 @@ struct Region {
     __device__ static constexpr int base(int wave) {       // wave's region
         return EXACT ? kWave0 + wave * kBytes : (wave == 0 ? kTable8 : kWave0 + (wave - 1) * kBytes);
     }
+    __device__ static constexpr int ov(int wave) { return base(wave) + kOv; }   // column words
 };
 static_assert(kTable8 + Region<false>::kBytes <= kTable, "wave 0's region in the narrow table's unused half");
 // the LDS cliffs (measured, DESIGN §3: 32,016 B ran four 4-wave blocks per CU
@@ -2513,20 +2514,21 @@ struct Evidence {
 
 // The narrow evidence (common instantiation, records of at most 15 reads):
 // one 8-byte table row per (class, quality), the class's 16-bit field holding
-// llr8 << 4 | 1 (llr8 = the row's LLR term in 1/8 nat, rounded down, <= 273;
+// llr8 << 4 | 1 (llr8 = the row's LLR term in 1/u nat, rounded down, <= 273,
+// u = 16 with the default parameters, 8 or 4 for extreme qualities;
 // the low 4 bits count the class's rows), 'N' and masked rows 0.  A column's
 // sum is then one u64: field k = L_k << 4 | n_k, with no carry between fields
 // (15 rows: 15 * 273 < 2^12, n_k <= 15), and comparing fields compares L_k.
 template <int NT>
 struct Evidence8 {
-    uint64_t f[NT];
+    uint32_t lo[NT], hi[NT];   // fields A T | C G (two 32-bit halves: no 64-bit adds)
 };
 
 template <int NT, bool FULL>
 __device__ __forceinline__ void run_evidence8(Evidence8<NT> &ev, const uint8_t *lds, int R, uint32_t rmx, int crv,
                                               int lane) {
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) ev.f[tt] = 0;
+    for (int tt = 0; tt < NT; ++tt) ev.lo[tt] = ev.hi[tt] = 0u;
     auto codes = [&](int r, uint32_t (&cd)[NT]) {
         const int rr = min(r, R - 1);
         const int cr = readlane(crv, rr);          // stage address of the read's column 0
@@ -2554,9 +2556,8 @@ __device__ __forceinline__ void run_evidence8(Evidence8<NT> &ev, const uint8_t *
     auto add2 = [&](const uint2 (&f)[NT], const uint2 (&g)[NT]) {
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt) {
-            const uint32_t lo = (uint32_t)ev.f[tt] + f[tt].x + g[tt].x;
-            const uint32_t hi = (uint32_t)(ev.f[tt] >> 32) + f[tt].y + g[tt].y;
-            ev.f[tt] = ((uint64_t)hi << 32) | lo;
+            ev.lo[tt] += f[tt].x + g[tt].x;
+            ev.hi[tt] += f[tt].y + g[tt].y;
         }
     };
     uint32_t c0[NT], c1[NT];
@@ -2581,7 +2582,10 @@ __device__ __forceinline__ void run_evidence8(Evidence8<NT> &ev, const uint8_t *
         uint2 f0[NT];
         rows(c0, f0);
 #pragma unroll
-        for (int tt = 0; tt < NT; ++tt) ev.f[tt] += ((uint64_t)f0[tt].y << 32) | f0[tt].x;
+        for (int tt = 0; tt < NT; ++tt) {
+            ev.lo[tt] += f0[tt].x;
+            ev.hi[tt] += f0[tt].y;
+        }
     }
 }
 
@@ -2771,11 +2775,14 @@ __device__ __forceinline__ uint32_t stage_codes(const FastArgs &a, const RecMeta
 #pragma unroll
     for (int u = 0; u < NDW; ++u) {
         if (u * kWave < ndw) {
-            if (u * kWave + lane < ndw) {
-                const uint2 c = LO ? make_codes4<DUPLEX, true, NARROW>(st.vb[u], st.vq[u], a.kq, a.kqlo, bad)
-                                   : make_codes4<DUPLEX, false, NARROW>(st.vb[u], st.vq[u], a.kq, a.kqlo, bad);
-                *(uint2 *)(lds + stage_addr + 8 * (u * kWave + lane)) = c;
-            }
+            // every lane of the group converts and stores (the stage holds
+            // NDW * 64 dwords' codes); a dword past the record's is not
+            // checked (no per-lane branch)
+            uint32_t b = 0;
+            const uint2 c = LO ? make_codes4<DUPLEX, true, NARROW>(st.vb[u], st.vq[u], a.kq, a.kqlo, b)
+                               : make_codes4<DUPLEX, false, NARROW>(st.vb[u], st.vq[u], a.kq, a.kqlo, b);
+            bad |= u * kWave + lane < ndw ? b : 0u;
+            *(uint2 *)(lds + stage_addr + 8 * (u * kWave + lane)) = c;
         }
     }
     return bad;
@@ -2993,7 +3000,7 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt)
             x += EXACT ? (uint32_t)ev.llr[tt] ^ (uint32_t)(ev.llr[tt] >> 32) ^ ev.cnt[tt]
-                       : (uint32_t)ev8.f[tt] ^ (uint32_t)(ev8.f[tt] >> 32);
+                       : ev8.lo[tt] ^ ev8.hi[tt];
         if (lane == 0) a.O.pos[rec] = (int)x;
         return kFinDone;
     }
@@ -3027,17 +3034,15 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
     // The column words go to ov only where they are read again: EXACT, and
     // the double mean of records of more than 16 reads.
     const int T16 = ((int)((m.w >> 7) & 255u) + 15) & ~15;
-    DCR_G uint16_t *pd = nullptr, *pe = nullptr;
-    DCR_G uint8_t *ps = nullptr, *pq = nullptr;
-    if (!EXACT) {
-        // per-record bases in scalar registers (from the LDS pointer cache +
-        // the record's column offset); lanes store at 32-bit byte offsets
-        // from them (global_store ... v_off, s_base): no per-lane 64-bit address
-        pd = lds_sgptr<uint16_t>(lds, fk::kPD) + off;
-        pe = lds_sgptr<uint16_t>(lds, fk::kPE) + off;
-        ps = lds_sgptr<uint8_t>(lds, fk::kPSeq) + off;
-        pq = lds_sgptr<uint8_t>(lds, fk::kPQual) + off;
-    }
+    // the common instantiation's column stores: buffer stores on resources
+    // based at the record's region and sized to it (T16 columns), so the last
+    // tile's lanes past the region are dropped by the range check instead of
+    // branching around them (no exec-mask branch in the loop over tiles)
+    // (unused in the EXACT instantiation)
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.d + off), (short)0, 2 * T16, 0x00020000);
+    const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.e + off), (short)0, 2 * T16, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.seq + off), (short)0, T16, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.qual + off), (short)0, T16, 0x00020000);
     // more reads than r_safe: L_b may underflow (fast_constants), no column is decided here
     const bool force = R > a.r_safe;
     int dmax = -1, dmin = 0x7fffffff;
@@ -3050,8 +3055,8 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
     for (int tt = 0; tt < NT; ++tt) {
         const int t = 64 * tt + lane;
         const bool live = tt < NT - 1 || t < T;                      // only the last tile is partial
-        const uint64_t sum = EXACT ? ev.llr[tt] : ev8.f[tt];
-        const uint32_t lo = (uint32_t)sum, hi = (uint32_t)(sum >> 32);
+        const uint32_t lo = EXACT ? (uint32_t)ev.llr[tt] : ev8.lo[tt];
+        const uint32_t hi = EXACT ? (uint32_t)(ev.llr[tt] >> 32) : ev8.hi[tt];
         // (A, C) and (T, G) fields as 16-bit pairs: one packed max / min gives both halves
         const u16x2 P1 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi, lo, 0x05040100u));
         const u16x2 P2 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi, lo, 0x07060302u));
@@ -3081,16 +3086,21 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
         }
         const int e = R - nb;                                                     // rows that differ from the call
         // decided: LLR_b - max(LLR_k, 0) >= (Lb - L2 - (d - nb)) / u >= margin / u
-        // (u = 16 wide, 8 narrow)
+        // (u = 16 wide; narrow: fast_constants' unit)
         const bool undecided = (int)(Lb - L2) - (d - nb) < (EXACT ? a.t16 : a.t8) || force;
         und |= (uint32_t)(live && undecided) << tt;
         if (EXACT) *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (kb << 12));
-        if (!EXACT && DCR_ABL != 5 && t < T16) {
-            const uint32_t ut = (uint32_t)t, ut2 = 2u * ut;
-            *(DCR_G uint16_t *)((DCR_G uint8_t *)pd + ut2) = (uint16_t)d;
-            *(DCR_G uint16_t *)((DCR_G uint8_t *)pe + ut2) = (uint16_t)e;
-            ps[ut] = (uint8_t)(t < T ? __builtin_amdgcn_perm(0u, 0x47435441u, kb) : 0x4Eu);   // "ATCG"[call]
-            pq[ut] = (uint8_t)(t < T ? (uint32_t)a.maxq : 0u);
+        if (!EXACT && DCR_ABL != 5) {
+            // "ATCG"[call] and maxQ; past T (last tile only) 'N' / 0
+            uint32_t letter = __builtin_amdgcn_perm(0u, 0x47435441u, kb), qv = (uint32_t)a.maxq;
+            if (tt == NT - 1) {
+                letter = t < T ? letter : 0x4Eu;
+                qv = t < T ? qv : 0u;
+            }
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)d, rd, 2 * t, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)e, re, 2 * t, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)letter, rs, t, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)qv, rq, t, 0, 0);
         }
         fx += live ? __umul24((uint32_t)e, m720[d]) : 0u;
         dmax = max(dmax, live ? d : -1);
@@ -3358,23 +3368,18 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
         // the record's scalars as one 16-byte row at its fast-list index
         // (k_fast_rows expands it into the ten dcr_out arrays and rounds the
         // mean): pos (:790, first = 0 here), T | D << 8 | M << 16 | MAPQ << 24
-        // (len = n_de = T, one M run), S, kind 1; a mean computed here in
-        // doubles (R > 16) is stored directly, kind 2
+        // (len = n_de = T, one M run), S, kind 1.
         const int mapq = (int)((uint32_t)m.d0 >> 16);
         uint32_t v = 0;
         v = write_lane<0>(v, __builtin_amdgcn_readfirstlane((uint32_t)minpos));
         v = write_lane<1>(v, __builtin_amdgcn_readfirstlane((uint32_t)T | (uint32_t)Dmax << 8 | (uint32_t)Dmin << 16 |
                                                             (uint32_t)mapq << 24));
         v = write_lane<2>(v, __builtin_amdgcn_readfirstlane(S));
-        v = write_lane<3>(v, slow ? 2u : 1u);
-        v = write_lane<7>(v, E_lo);
-        v = write_lane<8>(v, E_hi);
-        if (lane < 4) {
-            lds_sgptr<uint32_t>(lds, fk::kPRows)[4 * fi + lane] = v;
-        } else if (slow && (lane == 7 || lane == 8)) {
-            const uint64_t pw = *(const uint64_t *)(lds + fk::kPtrs + 8 * lane);
-            *(DCR_G uint32_t *)((pw & 0x00FFFFFFFFFFFFFFull) + ((uint64_t)rec << (pw >> 56))) = v;
-        }
+        v = write_lane<3>(v, 1u);
+        // lanes 0-3 (a buffer store on the row's 16 bytes: the other lanes'
+        // words fall outside it, no branch)
+        __builtin_amdgcn_raw_buffer_store_b32(v, __builtin_amdgcn_make_buffer_rsrc((void *)(a.rows + fi), (short)0, 16,
+                                                                                       0x00020000), 4 * lane, 0, 0);
         sp.mark(10);                     // [9] record scalars
         return kFinDone;
     }
@@ -3505,7 +3510,7 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : DCR_FAST_OCC) void k
             *(uint2 *)(lds + 0x400 * k + 8 * (q + k)) = make_uint2((uint32_t)inc, (uint32_t)(inc >> 32));
         }
     }
-    if (threadIdx.x < 64) ((double *)(lds + fk::kInvD))[threadIdx.x] = threadIdx.x == 0 ? 0.0 : 1.0 / (double)threadIdx.x;
+    if (EXACT && threadIdx.x < 64) ((double *)(lds + fk::kInvD))[threadIdx.x] = threadIdx.x == 0 ? 0.0 : 1.0 / (double)threadIdx.x;
     if (threadIdx.x == 0) *(uint16_t *)(lds + fk::kSent) = (uint16_t)(EXACT ? fk::kPadCode : fk::kPadCode8);
     if (threadIdx.x < 64) {
         const int t = threadIdx.x;
@@ -3543,7 +3548,7 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : DCR_FAST_OCC) void k
     const int lane0 = threadIdx.x & 63;
     const int stage_addr = RG::base(wave);
     const int rm_addr = stage_addr + RG::kRm;
-    const int ov_addr = stage_addr + RG::kOv;
+    const int ov_addr = RG::ov(wave);
     __syncthreads();
     int i = first_i + wave;
     if (i >= hi) return;
@@ -3607,7 +3612,9 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : DCR_FAST_OCC) void k
         // a record this kernel does not decide gets an empty row (kind 0:
         // k_fast_rows leaves its scalars to the kernel that finishes it)
         auto no_row = [&]() {
-            if (!EXACT && DCR_ROWS && lane == 3) lds_sgptr<uint32_t>(lds, fk::kPRows)[4 * i + 3] = 0u;
+            if (!EXACT && DCR_ROWS)     // the row's four words zeroed (kind 0), no lane branch
+                __builtin_amdgcn_raw_buffer_store_b32(0u, __builtin_amdgcn_make_buffer_rsrc((void *)(a.rows + i), (short)0, 16,
+                                                                                            0x00020000), 4 * lane, 0, 0);
         };
         if (direct) {
             no_row();
