@@ -3038,11 +3038,12 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
     // based at the record's region and sized to it (T16 columns), so the last
     // tile's lanes past the region are dropped by the range check instead of
     // branching around them (no exec-mask branch in the loop over tiles)
-    // (unused in the EXACT instantiation)
-    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.d + off), (short)0, 2 * T16, 0x00020000);
-    const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.e + off), (short)0, 2 * T16, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.seq + off), (short)0, T16, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.qual + off), (short)0, T16, 0x00020000);
+    // (made where they are used, so their 16 scalar registers are not held
+    // across the tile loop; unused in the EXACT instantiation)
+#define DCR_RSRC_D __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.d + off), (short)0, 2 * T16, 0x00020000)
+#define DCR_RSRC_E __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.e + off), (short)0, 2 * T16, 0x00020000)
+#define DCR_RSRC_S __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.seq + off), (short)0, T16, 0x00020000)
+#define DCR_RSRC_Q __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.qual + off), (short)0, T16, 0x00020000)
     // more reads than r_safe: L_b may underflow (fast_constants), no column is decided here
     const bool force = R > a.r_safe;
     int dmax = -1, dmin = 0x7fffffff;
@@ -3097,10 +3098,10 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
                 letter = t < T ? letter : 0x4Eu;
                 qv = t < T ? qv : 0u;
             }
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)d, rd, 2 * t, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)e, re, 2 * t, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)letter, rs, t, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)qv, rq, t, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)d, DCR_RSRC_D, 2 * t, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)e, DCR_RSRC_E, 2 * t, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)letter, DCR_RSRC_S, t, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)qv, DCR_RSRC_Q, t, 0, 0);
         }
         fx += live ? __umul24((uint32_t)e, m720[d]) : 0u;
         dmax = max(dmax, live ? d : -1);
