@@ -171,13 +171,14 @@ def write_config_bam(path, cfg: SynthConfig, n_families=None, seed=None):
     return path
 
 
-def write_packed_bam(path, packed, seed=0, level=1, n_threads=0, chunk_families=1 << 16, header=True):
+def write_packed_bam(path, packed, seed=0, level=1, n_threads=0, chunk_families=1 << 16, header=True, fam_id0=0):
     """Write the families of a packed batch (``packed_fixed_size`` /
     ``packed_config``) as a duplex BAM through the native record writer
     (include/dcr_io.h dcr_synth_write): the bench's 10 M+-read inputs.  UMIs
     are random per family (seeded); every read passes the reference's filters
     (paired, proper, MAPQ >= 20 as generated).  header=False: the records'
-    BGZF blocks only (plus the EOF block), a piece of a larger BAM."""
+    BGZF blocks only (plus the EOF block), a piece of a larger BAM; fam_id0:
+    the MI code of its first family (pieces of one BAM keep codes distinct)."""
     from . import native_io
     from .batch import PackedBatch
     hdr = BamHeader_bytes() if header else b""
@@ -197,7 +198,7 @@ def write_packed_bam(path, packed, seed=0, level=1, n_threads=0, chunk_families=
         part.bases, part.quals = packed.bases, packed.quals
         part.n_fam, part.n_reads = f1 - f0, r1 - r0
         umis = _ACGT[rng.integers(0, 4, 16 * (f1 - f0))]
-        w.write_synthetic(part, umis, fam_id0=f0, n_threads=n_threads)
+        w.write_synthetic(part, umis, fam_id0=fam_id0 + f0, n_threads=n_threads)
     w.close()
     return path
 
