@@ -5,6 +5,8 @@
 // the ingest's own sources under -fsanitize=thread or address
 // (tests/native/Makefile) so races and lifetime errors of the stream path
 // show up on the CPU; tests/test_stream_protocol.py compares the two hashes.
+// DCR_TEST_PASSES=n runs n ingests one after another in the process (the
+// bench's CLI passes share one inflater), printing a line per pass.
 //   usage: ingest_driver BAM HOOK [READS_PER_BATCH]
 #include <cstdio>
 #include <cstdlib>
@@ -41,6 +43,9 @@ int main(int argc, char **argv) {
         dcr_test_stream_hook(&hook);
         if (dcr_io_set_inflate_hook(&hook) != 0) return 3;
     }
+    const char *np = std::getenv("DCR_TEST_PASSES");
+    const int passes = np && std::atoi(np) > 0 ? std::atoi(np) : 1;
+    for (int pass = 0; pass < passes; ++pass) {
     dcr_ingest_cfg cfg{20, 1, 100, 20, 0, 0};
     dcr_ingest *ing = dcr_ingest_open(argv[1], &cfg);
     if (!ing) {
@@ -128,5 +133,7 @@ int main(int argc, char **argv) {
                 batches, hb.end_kind, (long long)c[4], (long long)c[0], (long long)c[1], (long long)c[2],
                 (long long)c[3], (unsigned long long)h, gpu, (long long)s[0], (long long)s[1], (long long)s[2],
                 (long long)s[3]);
+    std::fflush(stdout);
+    }
     return 0;
 }

@@ -102,3 +102,79 @@ def test_stream_ingest_under_sanitizers_16_16_pools(drivers, bams, kind):
         got, err = _run(exe, bam, 1, env, timeout=600)
         assert "WARNING: ThreadSanitizer" not in err and "ERROR: AddressSanitizer" not in err, err[-4000:]
         _same(ref, got)
+
+
+# ---- round 3's protocol, for the one unexplained bench exit ------------------
+# tests/native/Makefile (target r3) extracts round 3's ingest from this
+# repository's history (git 205281c) and links it with r3_stream_host.cpp, a
+# host restatement of round 3's span protocol (dcr_inflate.hip:797-1057 at
+# that commit).  What each suspect does under it, on the CPU:
+#   * a late member-scanner start (the start-offset race): the stream serves a
+#     later member's bytes at offset 0, the header check fails and the open
+#     returns "not a BAM file" at once -- a Python RuntimeError with a
+#     traceback, not a silent exit;
+#   * 16 scanner + 16 pack threads, several passes sharing one inflater: the
+#     same batches as the host pool, no heap error under AddressSanitizer, and
+#     ThreadSanitizer reports only the start-offset race;
+#   * small BGZF blocks: the fetch/producer deadlock -- a hang, not an exit.
+# None of the three ends a process silently within seconds
+# (profiles/r03o/pool_ab_16_16_2_failed.log); DESIGN §5 records what remains.
+
+def _git_has_round3():
+    try:
+        subprocess.run(["git", "-C", ROOT, "cat-file", "-e", "205281c:duplexumiconsensusreads_amd/csrc/dcr_ingest.cpp"],
+                       check=True, capture_output=True)
+        return True
+    except (OSError, subprocess.CalledProcessError):
+        return False
+
+
+@pytest.fixture(scope="module")
+def r3_drivers():
+    if not _git_has_round3():
+        pytest.skip("round 3's sources are not in this checkout's history")
+    subprocess.run(["make", "-s", "-C", NATIVE, "-j3", "r3"], check=True)
+    return BUILD
+
+
+R3_POOLS = {"DCR_SCAN_THREADS": "16", "DCR_PACK_THREADS": "16", "ASAN_OPTIONS": "detect_leaks=0 exitcode=67",
+            "TSAN_OPTIONS": "halt_on_error=0 exitcode=66"}
+
+
+def _run_raw(exe, bam, env_extra, timeout):
+    env = dict(os.environ)
+    env.update(R3_POOLS)
+    env.update(env_extra)
+    return subprocess.run([exe, bam, "1"], capture_output=True, text=True, timeout=timeout, env=env)
+
+
+@pytest.mark.parametrize("kind", ["", "_asan"])
+def test_round3_late_member_scan_is_a_clean_open_error(r3_drivers, bams, kind):
+    big, _ = bams
+    r = _run_raw(os.path.join(r3_drivers, "r3_driver" + kind), big, {"DCR_R3_LATE_MS": "5"}, 120)
+    assert r.returncode == 4, (r.returncode, r.stdout[-1000:], r.stderr[-3000:])
+    assert r.stderr.strip() == "open: not a BAM file", r.stderr[-3000:]
+
+
+def test_round3_16_16_pools_several_passes(r3_drivers, bams):
+    big, _ = bams
+    ref, _ = _run(os.path.join(r3_drivers, "ingest_driver"), big, 0)
+    for kind in ("", "_asan"):
+        r = _run_raw(os.path.join(r3_drivers, "r3_driver" + kind), big,
+                     {"DCR_TEST_PASSES": "3", "DCR_R3_COPY_US": "200"}, 600)
+        assert r.returncode == 0 and "ERROR: AddressSanitizer" not in r.stderr, (r.returncode, r.stderr[-3000:])
+        lines = r.stdout.strip().splitlines()
+        assert len(lines) == 3
+        for ln in lines:
+            f = ln.split()
+            _same(ref, dict(zip(f[0::2], f[1::2])))
+    # ThreadSanitizer: the start-offset race and nothing else
+    r = _run_raw(os.path.join(r3_drivers, "r3_driver_tsan"), big, {"DCR_TEST_PASSES": "2"}, 600)
+    reports = r.stderr.count("WARNING: ThreadSanitizer")
+    assert reports >= 1 and r.stderr.count("Inflater::scan_members") >= reports, r.stderr[-4000:]
+
+
+def test_round3_small_blocks_hang(r3_drivers, bams):
+    _, small = bams
+    with pytest.raises(subprocess.TimeoutExpired):
+        _run_raw(os.path.join(r3_drivers, "r3_driver"), small, {}, 15)
