@@ -72,6 +72,9 @@ struct IStamp {
 // a 4 KiB ring and a 9-bit root table (9.3 KB, 17 waves per CU instead of 10
 // at 8 KiB / 10 bits) inflate a 4,096-member span in 5.65 ms instead of 9.09
 // (35.2 -> 47.5 GB/s over all members in one launch; profiles/r04e)
+#ifndef DINF_WG_PER_CU
+#define DINF_WG_PER_CU 0  // k_inflate launch grid cap per CU (0: one workgroup per member)
+#endif
 #ifndef DINF_RING
 #define DINF_RING 4096    // LDS output history per member (bytes)
 #endif
@@ -380,15 +383,10 @@ __device__ __forceinline__ void keep_room(Out &o, const Args &a, uint32_t lane_s
     }
 }
 
-__global__ __launch_bounds__(64) void k_inflate(Args a) {
-    WaveLds &s = *reinterpret_cast<WaveLds *>(smem);
+// one member, decoded by the calling wave
+__device__ __forceinline__ void inflate_one(const Args &a, WaveLds &s, const int mi, const uint32_t lsh) {
     const int lane = lane_id();
-    const int mi = blockIdx.x;
-    if (mi >= a.n) return;
     const dcr_bgzf_member M = a.m[mi];
-    for (int i = lane; i < 256; i += kW) s.crc_tab[i] = dfl::crc_byte((uint32_t)i);
-    // x^(8 (kPiece - kStripe (l + 1))) mod P: the shift of lane l's stripe to a piece's end
-    const uint32_t lsh = dfl::x8nmodp(kPiece - kStripe * (uint32_t)(lane + 1));
 
     Out o;
     o.g = a.out + M.out_off;
@@ -608,6 +606,21 @@ __global__ __launch_bounds__(64) void k_inflate(Args a) {
     }
 }
 
+// Wave w takes members w, w + gridDim.x, ...  The grid is one workgroup per
+// member (DINF_WG_PER_CU 0).  A bounded resident grid (4 or 2 waves per CU)
+// lets the batch kernels beside a span start at once (k_recmeta<ss> per batch
+// 864 -> 44 us) but the serial member decode is latency-bound, so fewer waves
+// inflate slower (117 -> 266 / 390 ms of kernel time per pass) and the whole
+// node loses (357 -> 268 / 204 M consensus bases/s, profiles/r05r).
+__global__ __launch_bounds__(64) void k_inflate(Args a) {
+    WaveLds &s = *reinterpret_cast<WaveLds *>(smem);
+    const int lane = lane_id();
+    for (int i = lane; i < 256; i += kW) s.crc_tab[i] = dfl::crc_byte((uint32_t)i);
+    // x^(8 (kPiece - kStripe (l + 1))) mod P: the shift of lane l's stripe to a piece's end
+    const uint32_t lsh = dfl::x8nmodp(kPiece - kStripe * (uint32_t)(lane + 1));
+    for (int mi = (int)blockIdx.x; mi < a.n; mi += (int)gridDim.x) inflate_one(a, s, mi, lsh);
+}
+
 }  // namespace dinf
 
 // ---- host side ---------------------------------------------------------------
@@ -636,6 +649,7 @@ struct InflSlots {
 
 struct dcr_inflater {
     int device = 0;
+    int grid_cap = 1 << 30;           // k_inflate workgroups per launch (resident waves)
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     uint8_t *d_in = nullptr, *d_out = nullptr, *d_st = nullptr;
@@ -694,6 +708,7 @@ dcr_inflater *dcr_inflater_create(int device) {
         return nullptr;
     }
     h->base.x8n_piece = dfl::x8nmodp(dinf::kPiece);
+    if (DINF_WG_PER_CU > 0) h->grid_cap = DINF_WG_PER_CU * std::max(1, prop.multiProcessorCount);
     return h;
 }
 
@@ -749,7 +764,8 @@ int dcr_inflater_run(dcr_inflater *h, const uint8_t *in, int64_t in_bytes, const
     a.dbg = h->d_dbg;
     a.n = n;
     (void)hipEventRecord(h->ev0, s);
-    hipLaunchKernelGGL(dinf::k_inflate, dim3((unsigned)n), dim3(64), sizeof(dinf::WaveLds), s, a);
+    hipLaunchKernelGGL(dinf::k_inflate, dim3((unsigned)std::min(n, h->grid_cap)), dim3(64), sizeof(dinf::WaveLds), s,
+                       a);
     if ((e = hipGetLastError()) != hipSuccess) return -hip_fail(e, "k_inflate launch");
     (void)hipEventRecord(h->ev1, s);
     if ((e = hipMemcpyAsync(out, h->d_out, (size_t)out_bytes, hipMemcpyDeviceToHost, s)) != hipSuccess ||
@@ -868,7 +884,8 @@ struct HipSpanBackend {
                 hipSuccess ||
             hipEventRecord(start, S.s_k) != hipSuccess)
             return false;
-        hipLaunchKernelGGL(dinf::k_inflate, dim3((unsigned)n), dim3(64), sizeof(dinf::WaveLds), S.s_k, a);
+        hipLaunchKernelGGL(dinf::k_inflate, dim3((unsigned)std::min(n, h->grid_cap)), dim3(64), sizeof(dinf::WaveLds),
+                           S.s_k, a);
         return hipGetLastError() == hipSuccess &&
                hipMemcpyAsync(S.h_st[slot], S.d_st[slot], (size_t)n, hipMemcpyDeviceToHost, S.s_k) == hipSuccess &&
                hipEventRecord(done, S.s_k) == hipSuccess;
@@ -912,22 +929,6 @@ struct dcr_inflate_stream {
     dcr_inflate_stream(dcr_inflater *h, const uint8_t *file) : be{h, *h->slots}, s(be, file) {}
 };
 
-// The span kernels' stream.  DCR_INFLATE_CU_SHARE=k (1..3, diagnostic)
-// masks it to k of every 4 CUs, so batch kernels always find CUs free of
-// inflate waves; unset: every CU.
-static hipError_t span_stream_create(int device, hipStream_t *s) {
-    const char *e = getenv("DCR_INFLATE_CU_SHARE");
-    const int k = e ? atoi(e) : 0;
-    int n_cu = 0;
-    if (k < 1 || k > 3 || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
-        n_cu <= 0)
-        return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-    std::vector<uint32_t> mask((size_t)(n_cu + 31) / 32, 0u);
-    for (int i = 0; i < n_cu; ++i)
-        if (i % 4 < k) mask[(size_t)i / 32] |= 1u << (i % 32);
-    return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
-}
-
 extern "C" dcr_inflate_stream *dcr_inflate_stream_open(dcr_inflater *h, const uint8_t *file) {
     if (!h || !file) {
         dcr::set_error(DCR_EARG, "dcr_inflate_stream_open: bad arguments");
@@ -944,7 +945,7 @@ extern "C" dcr_inflate_stream *dcr_inflate_stream_open(dcr_inflater *h, const ui
     }
     InflSlots &S = *h->slots;
     (void)hipSetDevice(h->device);
-    if ((!S.s_k && span_stream_create(h->device, &S.s_k) != hipSuccess) ||
+    if ((!S.s_k && hipStreamCreateWithFlags(&S.s_k, hipStreamNonBlocking) != hipSuccess) ||
         (!S.s_out && hipStreamCreateWithFlags(&S.s_out, hipStreamNonBlocking) != hipSuccess)) {
         std::lock_guard<std::mutex> g(h->mu);
         S.busy = false;

@@ -38,6 +38,9 @@
 #ifndef DCR_FAST_OCC
 #define DCR_FAST_OCC 7   // fast kernel (common instantiation): waves per SIMD the launch bounds ask for
 #endif
+#ifndef DCR_EXACT_OCC
+#define DCR_EXACT_OCC 4  // fast kernel (EXACT instantiation): waves per SIMD the launch bounds ask for
+#endif
 #ifndef DCR_TRIM2
 #define DCR_TRIM2 1   // fast kernel: the 3' trim of C2-shaped records checked from the evidence counts
 #endif
@@ -2411,7 +2414,8 @@ struct Region {
     static constexpr int kCodes = EXACT ? 0x1000 : 0xC00;
     static constexpr int kRm = kCodes;                     // offset of the read words
     static constexpr int kOv = EXACT ? kCodes + 512 : 0;   // offset of the column words
-    static constexpr int kBytes = kCodes + 512 + (EXACT ? 512 : 0);
+    static constexpr int kList = kCodes + 1024;            // EXACT: u8 [256] the undecided columns, compacted
+    static constexpr int kBytes = kCodes + 512 + (EXACT ? 512 + 256 : 0);
     static constexpr int kDw = kCodes / 2 / 4 / kWave;     // staged dwords per lane: 8 / 6
     static constexpr int kLds = kWave0 + (EXACT ? kWaves : kWaves - 1) * kBytes + DCR_LDS_PAD;   // PAD: diagnostic builds
     __device__ static constexpr int base(int wave) {       // wave's region
@@ -2968,7 +2972,8 @@ constexpr int kFinQueue = 0, kFinDone = 1, kFinStatus = 2;
 
 template <bool DUPLEX, int NT, bool EXACT>
 __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m, const Staged &sg, uint8_t *lds,
-                                             const int stage_addr, const int ov_addr, const int rm_addr, const int lane,
+                                             const int stage_addr, const int ov_addr, const int rm_addr, const int list_addr,
+                                             const int lane,
                                              Stamps &sp, const double2 *xt, const uint32_t *r1, const double *qt,
                                              const int fi) {
     const int64_t rec = m.rec;
@@ -3122,13 +3127,13 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
         const dcr_params *P = lds_ptr<const dcr_params>(lds, fk::kPParams);
         const double *qthr = EXACT ? qt : P->qthresh;     // EXACT: LDS copy of the quality table
         bool fail = false;             // '+' / '-' call or int(-inf) quality: general kernel
-        // the lane's column results: posterior and 8-bit row counts of A T C G
-        Posterior po[NT];
-        uint32_t cnt[NT];
-        uint32_t tiles = 0;                               // tiles holding an undecided column (uniform)
-#pragma unroll
-        for (int tt = 0; tt < NT; ++tt) tiles |= (uint32_t)(__ballot((und >> tt) & 1u) != 0) << tt;
         if (!DUPLEX && R == 1) {
+            // the lane's column results: posterior and 8-bit row counts of A T C G
+            Posterior po[NT];
+            uint32_t cnt[NT];
+            uint32_t tiles = 0;                           // tiles holding an undecided column (uniform)
+#pragma unroll
+            for (int tt = 0; tt < NT; ++tt) tiles |= (uint32_t)(__ballot((und >> tt) & 1u) != 0) << tt;
             // one read: the column's posterior is a function of its row
             // (class after the mask, raw quality), tabulated per block in
             // the kernel's prologue by the products below and posterior()
@@ -3152,65 +3157,88 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
                 po[tt].overflow = (te >> 22) & 1u;
                 cnt[tt] = k ? 1u << (8 * (k - 1)) : 0u;
             }
-        } else {
-            // the products in read order (:594-600), every tile at once: per
-            // read, its rows at the NT columns of the lane are independent
-            // loads (the tiles' chains overlap instead of running one tile
-            // after another)
-            double L4[NT][4], U[NT];
 #pragma unroll
             for (int tt = 0; tt < NT; ++tt) {
-                U[tt] = 1.0;
-                cnt[tt] = 0;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) L4[tt][i] = 1.0;
+                const int t = 64 * tt + lane;
+                if ((und >> tt) & 1u) {
+                    fail |= po[tt].overflow || (!po[tt].masked && po[tt].best > 3);
+                    const uint32_t w = *(const uint16_t *)(ov + 2 * t);
+                    const int d = (int)(w & 63u);
+                    const int nb = po[tt].best <= 3 ? (int)((cnt[tt] >> (8 * po[tt].best)) & 255u) : 0;
+                    const int e = po[tt].masked ? d : R - nb;           // rows != the consensus character
+                    *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6));
+                    chq[t] = (uint16_t)((uint32_t)po[tt].ch | ((uint32_t)po[tt].q << 8));
+                }
             }
-            for (int r = 0; r < R; ++r) {
-                const int cr = readlane(crv, r);
-                const int x = readlane((int)rm.x, r);
-                const int col = x & 255, len = (x >> 8) & 255;
-                uint32_t k[NT];
-                double2 f[NT];
+        } else {
+            // the undecided columns compacted (u8 list in LDS, lane order):
+            // only ceil(n / 64) tiles of products and posteriors instead of
+            // every tile holding one such column (a record with a few
+            // undecided columns spread over three tiles ran all three)
+            uint8_t *ul = lds + list_addr;
+            int nund = 0;
 #pragma unroll
-                for (int tt = 0; tt < NT; ++tt) {
-                    if (!((tiles >> tt) & 1u)) continue;
-                    const int t = 64 * tt + lane;
+            for (int tt = 0; tt < NT; ++tt) {
+                const bool u = (und >> tt) & 1u;
+                const uint64_t bm = __ballot(u);
+                const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+                if (u) ul[nund + pre] = (uint8_t)(64 * tt + lane);
+                nund += __popcll(bm);
+            }
+            lds_fence();
+            // one compacted tile at a time (a record rarely has more than 64
+            // undecided columns): the products in read order (:594-600), two
+            // reads per step so their row loads overlap, then the posterior
+            for (int ct = 0; 64 * ct < nund; ++ct) {
+                const int t = 64 * ct + lane < nund ? (int)ul[64 * ct + lane] : -1;
+                double L4[4] = {1.0, 1.0, 1.0, 1.0}, U = 1.0;
+                uint32_t cn = 0;
+                auto row = [&](int r, uint32_t &k, double2 &f) {
+                    const int cr = readlane(crv, r);
+                    const int x = readlane((int)rm.x, r);
+                    const int col = x & 255, len = (x >> 8) & 255;
                     const uint32_t ad = (uint32_t)(t - col) < (uint32_t)len ? (uint32_t)(cr + 2 * t) : (uint32_t)fk::kSent;
                     const uint32_t code = *(const uint16_t *)(lds + ad);
                     const uint32_t kc = code >> 11;                  // code bank: N 0, A 1, T 2, C 3, G 4
                     const uint32_t q = ((code >> 4) & 127u) - kc;    // raw quality (pad 'N': 2)
                     // class after the mask: the table's 'N' rows are class N
                     // or a quality below min_base_quality (:280)
-                    k[tt] = (kc == 0 || (int)q < a.minbq) ? 0u : kc;
-                    f[tt] = xt[q];                                   // (1 - p', p'/5), LDS copy of P's rows
+                    k = (kc == 0 || (int)q < a.minbq) ? 0u : kc;
+                    f = xt[q];                                       // (1 - p', p'/5), LDS copy of P's rows
+                };
+                auto mul = [&](uint32_t k, double2 f) {
+                    U = U * f.y;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) L4[i] = L4[i] * (k == (uint32_t)(i + 1) ? f.x : f.y);
+                    cn += k ? 1u << (8 * (k - 1)) : 0u;
+                };
+                int r = 0;
+                for (; r + 1 < R; r += 2) {
+                    uint32_t k0, k1;
+                    double2 f0, f1;
+                    row(r, k0, f0);
+                    row(r + 1, k1, f1);
+                    mul(k0, f0);
+                    mul(k1, f1);
                 }
-#pragma unroll
-                for (int tt = 0; tt < NT; ++tt) {
-                    if (!((tiles >> tt) & 1u)) continue;
-                    U[tt] = U[tt] * f[tt].y;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) L4[tt][i] = L4[tt][i] * (k[tt] == (uint32_t)(i + 1) ? f[tt].x : f[tt].y);
-                    cnt[tt] += k[tt] ? 1u << (8 * (k[tt] - 1)) : 0u;
+                if (r < R) {
+                    uint32_t k0;
+                    double2 f0;
+                    row(r, k0, f0);
+                    mul(k0, f0);
                 }
-            }
-#pragma unroll
-            for (int tt = 0; tt < NT; ++tt) {
-                if (!((tiles >> tt) & 1u)) continue;
-                const double L[6] = {L4[tt][0], L4[tt][1], L4[tt][2], L4[tt][3], U[tt], U[tt]};
-                po[tt] = posterior(L, false, P, qthr, true);
-            }
-        }
-#pragma unroll
-        for (int tt = 0; tt < NT; ++tt) {
-            const int t = 64 * tt + lane;
-            if ((und >> tt) & 1u) {
-                fail |= po[tt].overflow || (!po[tt].masked && po[tt].best > 3);
-                const uint32_t w = *(const uint16_t *)(ov + 2 * t);
-                const int d = (int)(w & 63u);
-                const int nb = po[tt].best <= 3 ? (int)((cnt[tt] >> (8 * po[tt].best)) & 255u) : 0;
-                const int e = po[tt].masked ? d : R - nb;           // rows != the consensus character
-                *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6));
-                chq[t] = (uint16_t)((uint32_t)po[tt].ch | ((uint32_t)po[tt].q << 8));
+                const double L[6] = {L4[0], L4[1], L4[2], L4[3], U, U};
+                const Posterior po = posterior(L, false, P, qthr, true);
+                if (t >= 0) {
+                    fail |= po.overflow || (!po.masked && po.best > 3);
+                    const uint32_t w = *(const uint16_t *)(ov + 2 * t);
+                    const int d = (int)(w & 63u);
+                    const int nb = po.best <= 3 ? (int)((cn >> (8 * po.best)) & 255u) : 0;
+                    const int e = po.masked ? d : R - nb;               // rows != the consensus character
+                    *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6));
+                    chq[t] = (uint16_t)((uint32_t)po.ch | ((uint32_t)po.q << 8));
+                }
             }
         }
         lds_fence();
@@ -3447,7 +3475,7 @@ __device__ __forceinline__ RecMeta meta_from_lanes(uint32_t v) {
 // columns in the reference's double arithmetic.  The common kernel thus keeps
 // none of the exact path's code or registers.
 template <bool DUPLEX, bool EXACT>
-__global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : DCR_FAST_OCC) void k_consensus_fast(FastArgs a) {
+__global__ __launch_bounds__(fk::kBlockThreads, EXACT ? DCR_EXACT_OCC : DCR_FAST_OCC) void k_consensus_fast(FastArgs a) {
     using RG = fk::Region<EXACT>;
     __shared__ __attribute__((aligned(16))) uint8_t lds[RG::kLds];
     // Record assignment, XCD-aware: the blocks of one group (blockIdx % 8,
@@ -3550,6 +3578,7 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : DCR_FAST_OCC) void k
     const int stage_addr = RG::base(wave);
     const int rm_addr = stage_addr + RG::kRm;
     const int ov_addr = RG::ov(wave);
+    const int list_addr = stage_addr + RG::kList;      // EXACT only
     __syncthreads();
     int i = first_i + wave;
     if (i >= hi) return;
@@ -3635,10 +3664,10 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? 4 : DCR_FAST_OCC) void k
             no_row();
         } else if (sg.state == 0 || sg.state == 3) {
             int fin;
-            if (sg.T <= 64) fin = finish_record<DUPLEX, 1, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt, i);
-            else if (sg.T <= 128) fin = finish_record<DUPLEX, 2, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt, i);
-            else if (sg.T <= 192) fin = finish_record<DUPLEX, 3, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt, i);
-            else fin = finish_record<DUPLEX, 4, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, lane, sp, s_xt, s_r1, s_qt, i);
+            if (sg.T <= 64) fin = finish_record<DUPLEX, 1, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, list_addr, lane, sp, s_xt, s_r1, s_qt, i);
+            else if (sg.T <= 128) fin = finish_record<DUPLEX, 2, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, list_addr, lane, sp, s_xt, s_r1, s_qt, i);
+            else if (sg.T <= 192) fin = finish_record<DUPLEX, 3, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, list_addr, lane, sp, s_xt, s_r1, s_qt, i);
+            else fin = finish_record<DUPLEX, 4, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, list_addr, lane, sp, s_xt, s_r1, s_qt, i);
             if (!EXACT && fin != kFinDone) no_row();
             if (!EXACT && fin == kFinQueue) {
                 if (lane == npend) pend = i;

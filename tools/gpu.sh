@@ -59,11 +59,12 @@ for step in "$@"; do
       IFS=: read -r cfg lib <<< "$val"
       ABL_CONFIG=$cfg run "stamps_$cfg" 300 python3 -u tools/stamps.py 312500 "$PWD/$L/$lib" || exit 1 ;;
     kt)
+      k=$(( ${k:-0} + 1 )); sfx=$([ "$k" = 1 ] && echo "" || echo "$k")
       # shellcheck disable=SC2086
-      run kt 600 rocprofv3 --kernel-trace --stats -d "$O/kt" -o kt --output-format csv -- python3 bench.py $val || exit 1
-      find "$O/kt" -name "*kernel_trace.csv" -exec python3 tools/kt_grid.py {} \; > "$O/kernel_grid.csv" || exit 1
-      find "$O/kt" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats.csv" \;
-      grep '^{' "$O/kt.txt" | tail -1 > "$O/bench_kt.json" ;;
+      run "kt$sfx" 600 rocprofv3 --kernel-trace --stats -d "$O/kt$sfx" -o kt --output-format csv -- python3 bench.py $val || exit 1
+      find "$O/kt$sfx" -name "*kernel_trace.csv" -exec python3 tools/kt_grid.py {} \; > "$O/kernel_grid$sfx.csv" || exit 1
+      find "$O/kt$sfx" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats$sfx.csv" \;
+      grep '^{' "$O/kt$sfx.txt" | tail -1 > "$O/bench_kt$sfx.json" ;;
     traffic) run traffic 600 bash tools/gpu_traffic.sh "$TAG" || exit 1 ;;
     pmc)
       IFS=: read -r ctrs lib <<< "$val"
