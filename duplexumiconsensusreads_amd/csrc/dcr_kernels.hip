@@ -2758,7 +2758,7 @@ __device__ __forceinline__ Tp *lds_ptr(const uint8_t *lds, int slot) {
 // diagnostic phase clock (DCR_STAMP builds): cycles per phase, summed per wave
 struct Stamps {
     uint64_t t_prev = 0;
-    uint64_t acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     __device__ __forceinline__ void mark(int k) {
         if (DCR_STAMP) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
@@ -2776,17 +2776,20 @@ __device__ __forceinline__ uint32_t stage_codes(const FastArgs &a, const RecMeta
                                                 uint8_t *lds, int stage_addr, int lane) {
     const int ndw = (int)(m.w >> 15);
     uint32_t bad = 0;
+    uint8_t *sp = lds + stage_addr + 8 * lane;       // group u at the immediate offset 512 u
 #pragma unroll
     for (int u = 0; u < NDW; ++u) {
         if (u * kWave < ndw) {
             // every lane of the group converts and stores (the stage holds
             // NDW * 64 dwords' codes); a dword past the record's is not
-            // checked (no per-lane branch)
+            // checked: only the group holding the record's last dword
+            // compares lanes (a uniform branch, no per-lane one)
             uint32_t b = 0;
             const uint2 c = LO ? make_codes4<DUPLEX, true, NARROW>(st.vb[u], st.vq[u], a.kq, a.kqlo, b)
                                : make_codes4<DUPLEX, false, NARROW>(st.vb[u], st.vq[u], a.kq, a.kqlo, b);
-            bad |= u * kWave + lane < ndw ? b : 0u;
-            *(uint2 *)(lds + stage_addr + 8 * (u * kWave + lane)) = c;
+            const int lim = (u + 1) * kWave <= ndw ? kWave : ndw - u * kWave;   // uniform
+            bad |= lane < lim ? b : 0u;
+            *(uint2 *)(sp + 512 * u) = c;
         }
     }
     return bad;
@@ -3056,6 +3059,7 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
     // in fixed point, exact for depths <= 16 (720720 = lcm(1..16); < 2^32 over
     // 240 columns)
     uint32_t fx = 0;
+    int fxd = 0;                       // EXACT: the exact columns' change to fx (their e, d == 0 -> e/d = 1)
     const uint32_t *m720 = (const uint32_t *)(lds + fk::kM720);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
@@ -3103,10 +3107,11 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
                 letter = t < T ? letter : 0x4Eu;
                 qv = t < T ? qv : 0u;
             }
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)d, DCR_RSRC_D, 2 * t, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)e, DCR_RSRC_E, 2 * t, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)letter, DCR_RSRC_S, t, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)qv, DCR_RSRC_Q, t, 0, 0);
+            // the tile's offset as the scalar offset (no per-tile vector add)
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)d, DCR_RSRC_D, 2 * lane, 128 * tt, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)e, DCR_RSRC_E, 2 * lane, 128 * tt, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)letter, DCR_RSRC_S, lane, 64 * tt, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)qv, DCR_RSRC_Q, lane, 64 * tt, 0);
         }
         fx += live ? __umul24((uint32_t)e, m720[d]) : 0u;
         dmax = max(dmax, live ? d : -1);
@@ -3118,6 +3123,7 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
     // below maxQ.  The kept span then runs from the first to the last column
     // that is not 'N' (:770-790), still one M run (no '+' / '-' rows here).
     int first = 0, last = T - 1;
+    sp.mark(12);                         // [11] decision (of [5] finalize)
     const bool exact = __ballot(und) != 0;
     if (!EXACT && exact) return kFinQueue;
     // exact columns' character | quality << 8, as u16 per column in the wave's
@@ -3166,6 +3172,7 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
                     const int d = (int)(w & 63u);
                     const int nb = po[tt].best <= 3 ? (int)((cnt[tt] >> (8 * po[tt].best)) & 255u) : 0;
                     const int e = po[tt].masked ? d : R - nb;           // rows != the consensus character
+                    fxd += (d == 0 ? 720720 : e * (int)m720[d]) - (int)((w >> 6) & 63u) * (int)m720[d];
                     *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6));
                     chq[t] = (uint16_t)((uint32_t)po[tt].ch | ((uint32_t)po[tt].q << 8));
                 }
@@ -3236,11 +3243,13 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
                     const int d = (int)(w & 63u);
                     const int nb = po.best <= 3 ? (int)((cn >> (8 * po.best)) & 255u) : 0;
                     const int e = po.masked ? d : R - nb;               // rows != the consensus character
+                    fxd += (d == 0 ? 720720 : e * (int)m720[d]) - (int)((w >> 6) & 63u) * (int)m720[d];
                     *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6));
                     chq[t] = (uint16_t)((uint32_t)po.ch | ((uint32_t)po.q << 8));
                 }
             }
         }
+        sp.mark(11);                     // [10] products and posteriors (of [5] finalize)
         lds_fence();
         // kept span: first / last column whose character is not 'N'
         int fst = 0x7fffffff, lst = -1;
@@ -3315,7 +3324,8 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
     // sits that close to a half-integer; a DPP tree sum decides, and the exact
     // pairwise walk (over the e/d columns written into the now free stage) runs
     // only near such a boundary.
-    // Every column decided and R <= 16: the mean is the rational
+    // R <= 16 (every column decided, or the exact columns' e folded into fx by
+    // fxd above): the mean is the rational
     // 1000 sum(e/d) / T = 25 fx / (18018 T) exactly (fx = 720720 sum(e/d)), and
     // its rounding is read off the integer remainder.  A value that is not a
     // tie lies >= 1 / (2 * 18018 T) > 1e-7 from a half-integer, far beyond the
@@ -3325,9 +3335,9 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
     uint32_t E_lo = 0, E_hi = 0;         // E's words, scalar registers
     uint32_t S = 0;                      // the rational mean's numerator (rows: k_fast_rows rounds it)
     // (the common instantiation holds records of at most 15 reads)
-    bool slow = EXACT ? (exact || R > 16 || DCR_ABL == 4) : false;
+    bool slow = EXACT ? (R > 16 || DCR_ABL == 4) : false;
     if (!slow) {
-        S = (uint32_t)wave_sum((int)fx);
+        S = (uint32_t)wave_sum((int)(fx + (uint32_t)fxd));
         if (EXACT || !DCR_ROWS) {
             // the rational 25 S / (18018 T) in doubles: k = rint, remainder exact
             const int64_t num = 25 * (int64_t)S;
@@ -3590,6 +3600,10 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? DCR_EXACT_OCC : DCR_FAST
     RecMeta m1 = ML[midx(i1)];
     FastStage<RG::kDw> st;
     fast_load<DUPLEX>(a, m0, ML + midx(i2), lane0, st);
+    // EXACT: the queue index of the record after i2, loaded one record ahead
+    // as a vector load (the descriptor load of the prefetch depends on it; a
+    // scalar load issued there stalled the issue for its whole latency)
+    int xv = EXACT ? a.xlist[opaque(nxt(i2))] : 0;
     Stamps sp;
     int pend = 0, npend = 0;           // !EXACT: queued fast-list indices (lane p holds the p-th)
     auto flush = [&](int ln) {         // queue pointers from the LDS cache (no scalar registers held)
@@ -3631,7 +3645,8 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? DCR_EXACT_OCC : DCR_FAST
         // next but one; unconditional (the last record re-loads itself) so the
         // registers have one definition
         const int i3 = nxt(i2);
-        fast_load<DUPLEX>(a, m1, ML + midx(i3), lane, st);
+        fast_load<DUPLEX>(a, m1, ML + (EXACT ? __builtin_amdgcn_readfirstlane(xv) : i3), lane, st);
+        if (EXACT) xv = a.xlist[opaque(nxt(i3))];
         sp.mark(3);                    // [2] prefetch issue
         lds_fence();
         const uint2 rw = *(const uint2 *)(lds + rm_addr + 8 * lane);
@@ -3684,7 +3699,7 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? DCR_EXACT_OCC : DCR_FAST
     }
     if (!EXACT && npend) flush(lane0);
     if (DCR_STAMP && lane0 == 0)
-        for (int k = 0; k < 10; ++k)   // fast ss 0-9, ds 16-25; exact ss 32-41, ds 48-57
+        for (int k = 0; k < 12; ++k)   // fast ss 0-11, ds 16-27; exact ss 32-43, ds 48-59
             atomicAdd(&a.stamps[k + (DUPLEX ? 16 : 0) + (EXACT ? 32 : 0)], (unsigned long long)sp.acc[k]);
 }
 

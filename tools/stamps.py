@@ -41,10 +41,11 @@ for _ in range(K):
     kt = [a + b for a, b in zip(kt, ms)]
 lib.dcr_debug_stamps(ctx, st, 64, 0)
 names = ["prefetch wait", "codes into LDS", "prefetch issue", "trim, fence", "products",
-         "finalize", "depth reductions", "column stores", "mean", "record scalars"]
+         "finalize: rest", "depth reductions", "column stores", "mean", "record scalars",
+         "finalize: exact cols", "finalize: decision"]
 for kind, base, nrec, kidx in (("single-strand fast", 0, 4 * nfam, 1), ("duplex fast", 16, 2 * nfam, 5),
                                ("single-strand exact", 32, 4 * nfam, 2), ("duplex exact", 48, 2 * nfam, 6)):
-    tot = sum(st[base + k] for k in range(10))
+    tot = sum(st[base + k] for k in range(12))
     print(f"{kind}: kernel {kt[kidx] / K:.3f} ms; cycles per record per wave (s_memtime ticks):")
-    for k in range(10):
+    for k in range(12):
         print(f"   {names[k]:18s} {st[base + k] / (K * nrec):10.1f}  ({100.0 * st[base + k] / max(tot, 1):5.1f} %)")
