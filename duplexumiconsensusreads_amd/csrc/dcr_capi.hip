@@ -110,6 +110,7 @@ struct dcr_ctx {
     int direct_r = 3;
     uint16_t *d_llr16 = nullptr;   // device [128]
     uint16_t *d_llr8 = nullptr;    // device [128]
+    uint32_t *d_r2tab = nullptr;   // device [dcr::kR2Entries]: two-read column outcomes (EXACT pass)
     double *d_e1000 = nullptr;     // device [1001]: k / 1000 (the fast kernel's E)
     uint32_t *d_wtab = nullptr;    // device [DCR_LUT_N] (general kernel's decision pass)
     int n_cu = 256;     // compute units (persistent grid size)
@@ -228,6 +229,12 @@ static int upload_fast(dcr_ctx *c, const dcr_params *params) {
         hipMemcpy(c->d_llr8, llr8, sizeof(llr8), hipMemcpyHostToDevice) != hipSuccess ||
         (c->wide_ok && hipMemcpy(c->d_wtab, wtab, sizeof(wtab), hipMemcpyHostToDevice) != hipSuccess))
         return fail(DCR_EHIP, "fast-kernel table upload failed");
+    // the two-read outcomes from the device parameters just uploaded, by the
+    // EXACT pass's own products and posterior (bit-identical by construction)
+    hipLaunchKernelGGL(dcr::k_r2_table, dim3((dcr::kR2Entries + 255) / 256), dim3(256), 0, c->stream, c->d_params,
+                       c->d_r2tab);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)
+        return fail(DCR_EHIP, "two-read table build failed");
     return DCR_OK;
 }
 
@@ -267,6 +274,7 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
         hipMalloc(&c->d_params, sizeof(dcr_params)) != hipSuccess ||
         hipMalloc(&c->d_llr16, 128 * sizeof(uint16_t)) != hipSuccess ||
         hipMalloc(&c->d_llr8, 128 * sizeof(uint16_t)) != hipSuccess ||
+        hipMalloc(&c->d_r2tab, dcr::kR2Entries * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_e1000, 1001 * sizeof(double)) != hipSuccess ||
         hipMalloc(&c->d_wtab, DCR_LUT_N * sizeof(uint32_t)) != hipSuccess) {
         fail(DCR_EHIP, "context allocation failed");
@@ -324,6 +332,7 @@ void dcr_destroy(dcr_ctx *c) {
     if (c->d_params) (void)hipFree(c->d_params);
     if (c->d_llr16) (void)hipFree(c->d_llr16);
     if (c->d_llr8) (void)hipFree(c->d_llr8);
+    if (c->d_r2tab) (void)hipFree(c->d_r2tab);
     if (c->d_e1000) (void)hipFree(c->d_e1000);
     if (c->d_wtab) (void)hipFree(c->d_wtab);
     for (auto &e : c->ev)
@@ -461,6 +470,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
         f.lo_check = duplex || c->host_params.min_base_quality < c->fast_qlo;
         f.llr16 = c->d_llr16;
         f.llr8 = c->d_llr8;
+        f.r2tab = c->d_r2tab;
         f.t8 = c->fast_t8;
         f.narrow = c->fast_narrow;
         f.e1000 = c->d_e1000;

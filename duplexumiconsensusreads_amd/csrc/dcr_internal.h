@@ -102,6 +102,7 @@ struct FastArgs {
     int lo_check;                   // some unmasked quality may lie below fast_qlo: check the bytes
     const uint16_t *llr16;          // [123] per-quality LLR term, 1/16 nat, rounded down (EXACT's wide rows)
     const uint16_t *llr8;           // [123] the same in 1/u nat, u = 16, 8 or 4 (the common instantiation's narrow rows)
+    const uint32_t *r2tab;          // [5 * 128 * 5 * 128] two-read column outcomes (k_r2_table), EXACT
     int t8;                         // decision margin in 1/u nat
     int narrow;                     // llr8 fits the narrow rows (else the common kernel queues every record)
     const double *e1000;            // [1001] k / 1000 correctly rounded (numpy round(x, 3) = rint(1000 x) / 1000)
@@ -118,6 +119,8 @@ template <bool DUPLEX> __global__ void k_recmeta(Args a);
 __global__ void k_prep_big(Args a);
 template <bool DUPLEX, bool EXACT> __global__ void k_consensus_fast(FastArgs a);
 __global__ void k_fast_rows(FastArgs a);
+__global__ void k_r2_table(const dcr_params *P, uint32_t *tab);
+constexpr int kR2Entries = 5 * 128 * 5 * 128;
 template <bool DUPLEX> __global__ void k_consensus_general(Args a);
 template <bool DUPLEX> __global__ void k_decide(Args a);
 __global__ void k_decide_deep(Args a);

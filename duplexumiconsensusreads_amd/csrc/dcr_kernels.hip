@@ -3220,6 +3220,41 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
                     for (int i = 0; i < 4; ++i) L4[i] = L4[i] * (k == (uint32_t)(i + 1) ? f.x : f.y);
                     cn += k ? 1u << (8 * (k - 1)) : 0u;
                 };
+                if (R == 2) {
+                    // two reads: the column's outcome from the table (k_r2_table)
+                    auto kq = [&](int rr, uint32_t &k, uint32_t &q) {
+                        const int cr = readlane(crv, rr);
+                        const int x = readlane((int)rm.x, rr);
+                        const int col = x & 255, len = (x >> 8) & 255;
+                        const uint32_t ad = (uint32_t)(t - col) < (uint32_t)len ? (uint32_t)(cr + 2 * t) : (uint32_t)fk::kSent;
+                        const uint32_t code = *(const uint16_t *)(lds + ad);
+                        const uint32_t kc = code >> 11;
+                        q = (((code >> 4) & 127u) - kc) & 127u;
+                        k = (kc == 0 || (int)q < a.minbq) ? 0u : min(kc, 4u);
+                    };
+                    uint32_t k0, q0, k1, q1;
+                    kq(0, k0, q0);
+                    kq(1, k1, q1);
+                    const uint32_t te = a.r2tab[((k0 * 128u + q0) * 5u + k1) * 128u + q1];
+                    cn = (k0 ? 1u << (8 * (k0 - 1)) : 0u) + (k1 ? 1u << (8 * (k1 - 1)) : 0u);
+                    Posterior po;
+                    po.ch = (int)(te & 255u);
+                    po.q = (int)((te >> 8) & 1023u) - 1;
+                    po.best = (int)((te >> 18) & 7u);
+                    po.masked = (te >> 21) & 1u;
+                    po.overflow = (te >> 22) & 1u;
+                    if (t >= 0) {
+                        fail |= po.overflow || (!po.masked && po.best > 3);
+                        const uint32_t w = *(const uint16_t *)(ov + 2 * t);
+                        const int d = (int)(w & 63u);
+                        const int nb = po.best <= 3 ? (int)((cn >> (8 * po.best)) & 255u) : 0;
+                        const int e = po.masked ? d : R - nb;
+                        fxd += (d == 0 ? 720720 : e * (int)m720[d]) - (int)((w >> 6) & 63u) * (int)m720[d];
+                        *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6));
+                        chq[t] = (uint16_t)((uint32_t)po.ch | ((uint32_t)po.q << 8));
+                    }
+                    continue;
+                }
                 int r = 0;
                 for (; r + 1 < R; r += 2) {
                     uint32_t k0, k1;
@@ -3701,6 +3736,33 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? DCR_EXACT_OCC : DCR_FAST
     if (DCR_STAMP && lane0 == 0)
         for (int k = 0; k < 12; ++k)   // fast ss 0-11, ds 16-27; exact ss 32-43, ds 48-59
             atomicAdd(&a.stamps[k + (DUPLEX ? 16 : 0) + (EXACT ? 32 : 0)], (unsigned long long)sp.acc[k]);
+}
+
+// The outcome of a two-read column per (class after the mask, quality) of
+// each read, index ((k1 * 128 + q1) * 5 + k2) * 128 + q2, packed as the
+// one-read table (character, quality + 1, argmax, masked, overflow): the
+// EXACT pass's products in read order (1.0 * factor of read 1, then * factor
+// of read 2) and posterior(), so a table entry is bit-identical to computing
+// the column.  Two-read columns are the exact pass's most common kind (every
+// duplex record, single-strand records of two reads).
+__global__ __launch_bounds__(256) void k_r2_table(const dcr_params *P, uint32_t *tab) {
+    const int i = (int)(blockIdx.x * 256u + threadIdx.x);
+    if (i >= kR2Entries) return;
+    const uint32_t q2 = (uint32_t)i & 127u, k2 = ((uint32_t)i >> 7) % 5u;
+    const uint32_t q1 = ((uint32_t)i / 640u) & 127u, k1 = (uint32_t)i / (640u * 128u);
+    const double x1 = P->match[q1], y1 = P->mismatch[q1], x2 = P->match[q2], y2 = P->mismatch[q2];
+    double L4[4] = {1.0, 1.0, 1.0, 1.0};
+    double U = 1.0;
+    U = U * y1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) L4[j] = L4[j] * (k1 == (uint32_t)(j + 1) ? x1 : y1);
+    U = U * y2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) L4[j] = L4[j] * (k2 == (uint32_t)(j + 1) ? x2 : y2);
+    const double L[6] = {L4[0], L4[1], L4[2], L4[3], U, U};
+    const Posterior po = posterior(L, false, P, P->qthresh, true);
+    tab[i] = ((uint32_t)po.ch & 255u) | ((uint32_t)(po.q + 1) & 1023u) << 8 | ((uint32_t)po.best & 7u) << 18 |
+             (uint32_t)po.masked << 21 | (uint32_t)po.overflow << 22;
 }
 
 // Expands the rows k_consensus_fast wrote for the records it decided (one
