@@ -484,7 +484,11 @@ def main():
             dom, dom_label = "k_consensus_fast<ss>", ("k_consensus_fast<false, false> + k_fast_rows (single-strand "
                                                       "consensus; the HIP-event slot spans both launches)")
             dom_ms = kavg[dom]
+            # the slot's two launches: the kernel and its row expansion
             traffic, tsrc = load_traffic("k_consensus_fast<false, false>", packed.n_fam)
+            rows_traffic, _ = load_traffic("k_fast_rows", packed.n_fam)
+            if traffic is not None and rows_traffic is not None:
+                traffic += rows_traffic
         else:
             dom_label = "single-strand stage (k_recmeta<ss> + k_consensus_fast<ss> + k_consensus_exact<ss> + k_consensus_general<ss>)"
             dom_ms = sum(kavg[k] for k in _lib.KERNELS[0:4])
