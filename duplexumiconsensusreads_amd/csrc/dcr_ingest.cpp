@@ -400,6 +400,8 @@ struct Chunk {
     std::string err;
     bool indexed = false;           // recs holds every record starting after the first
     std::vector<Rec> recs;          // boundary in this chunk and ending in it (off from buf start)
+    std::vector<size_t> offs;       // the chain's record starts (parse stage input)
+    bool chained = false;           // the chain walked this chunk (its offs are valid)
 };
 
 // Record-index vectors of released chunks, kept for the next ingest of the
@@ -549,6 +551,7 @@ class Inflater {
         }
         th_ = std::thread([this] { loop(); });
         sth_ = std::thread([this] { scan_loop(); });
+        pth_ = std::thread([this] { parse_loop(); });
     }
     ~Inflater() {
         {
@@ -558,6 +561,7 @@ class Inflater {
         cv_.notify_all();
         th_.join();
         sth_.join();
+        pth_.join();
         stop_members_ = true;
         if (mth_.joinable()) mth_.join();
         if (stream_) hook_.stream_close(stream_);          // before the mapping it reads goes away
@@ -705,7 +709,29 @@ class Inflater {
                 c = inflated_.front();
                 inflated_.pop_front();
             }
-            scan(*c);
+            chain(*c);
+            const bool last = c->eof || !c->err.empty();
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                chained_.push_back(c);
+            }
+            cv_.notify_all();
+            if (last) return;
+        }
+    }
+    // the records' fields, on the scanner pool, one chunk behind the chain
+    // (the chain of chunk k + 1 runs while chunk k is parsed)
+    void parse_loop() {
+        for (;;) {
+            Chunk *c;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || !chained_.empty(); });
+                if (stop_) return;
+                c = chained_.front();
+                chained_.pop_front();
+            }
+            parse(*c);
             const bool last = c->eof || !c->err.empty();
             {
                 std::lock_guard<std::mutex> g(mu_);
@@ -718,15 +744,17 @@ class Inflater {
 
     // the block_size chain through c, continuing the stream state of the
     // previous chunk (a field or a skip may straddle the boundary)
-    void scan(Chunk &c) {
+    void chain(Chunk &c) {
         c.recs.clear();
         c.indexed = false;
+        c.chained = false;
+        std::vector<size_t> &offs_ = c.offs;
+        offs_.clear();
         if (dead_ || !c.err.empty()) { dead_ = true; return; }
         const double t0 = prof_ ? now() : 0;
         const uint8_t *d = c.data() + kHead;
         const size_t n = c.len;
         size_t pos = 0;
-        offs_.clear();
         auto field = [&](uint32_t &v) -> bool {      // a 4-byte field, possibly across chunks
             while (nfld_ < 4 && pos < n) fld_[nfld_++] = d[pos++];
             if (nfld_ < 4) return false;
@@ -791,7 +819,13 @@ class Inflater {
                     break;
             }
         }
+        c.chained = true;
+        if (prof_) scan_s += now() - t0;
+    }
+    void parse(Chunk &c) {
+        if (!c.chained) return;
         const double t1 = prof_ ? now() : 0;
+        const std::vector<size_t> &offs_ = c.offs;
         c.recs.resize(offs_.size());
         const uint8_t *base = c.data();
         const size_t chunk = 512;
@@ -802,10 +836,7 @@ class Inflater {
             return true;
         });
         c.indexed = true;
-        if (prof_) {
-            scan_s += t1 - t0;
-            index_parse_s += now() - t1;
-        }
+        if (prof_) index_parse_s += now() - t1;
     }
     static double now() {
         return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -996,12 +1027,12 @@ class Inflater {
     HugeBuf cbuf_;
     size_t cbeg_ = 0, cend_ = 0;
     bool file_eof_ = false;
-    Chunk chunks_[4];
-    std::deque<Chunk *> empty_, inflated_, full_;
+    Chunk chunks_[5];                  // filling, chaining, parsing, walked, one spare
+    std::deque<Chunk *> empty_, inflated_, chained_, full_;
     std::mutex mu_;
     std::condition_variable cv_;
     bool stop_ = false;
-    std::thread th_, sth_;
+    std::thread th_, sth_, pth_;
     // scanner stream state
     enum { kMagic, kLText, kNRef, kLName, kRec } st_ = kMagic;
     uint8_t fld_[4] = {0, 0, 0, 0};
@@ -1009,14 +1040,13 @@ class Inflater {
     uint64_t skip_ = 0;
     int32_t nref_left_ = 0;
     bool dead_ = false;
-    std::vector<size_t> offs_;
     const bool prof_ = std::getenv("DCR_INGEST_PROF") != nullptr;
 };
 
 // DCR_INGEST_PROF=1: seconds per ingest stage, printed to stderr at close
 struct IngestProf {
     bool on = std::getenv("DCR_INGEST_PROF") != nullptr;
-    double wait_chunk = 0, scan = 0, parse = 0, flush = 0, walk_total = 0, complete = 0;
+    double wait_chunk = 0, scan = 0, parse = 0, flush = 0, walk_total = 0, complete = 0, tasks_wait = 0;
     int64_t indexed = 0;
     static double now() {
         return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -1067,8 +1097,10 @@ struct dcr_ingest {
         if (prof.on)
             std::fprintf(stderr,
                          "[ingest] walk %.3f s: chunk wait %.3f, serial scan %.3f, parse %.3f, pack copy %.3f, "
-                         "families %.3f; scanner stage: chain %.3f, parse %.3f; indexed records %lld of %lld\n",
+                         "families %.3f, family tasks wait %.3f; scanner stage: chain %.3f, parse %.3f; indexed "
+                         "records %lld of %lld\n",
                          prof.walk_total, prof.wait_chunk, prof.scan, prof.parse, prof.flush, prof.complete,
+                         prof.tasks_wait,
                          infl ? infl->scan_s : 0.0,
                          infl ? infl->index_parse_s : 0.0, (long long)prof.indexed, (long long)records);
         infl.reset();             // stops the inflate thread before the file closes
@@ -1214,9 +1246,16 @@ struct dcr_ingest {
     // first, :1548-1551) and at the end of a batch; the first task (in input
     // order) that fails truncates the batch to its reservation and stops
     // there, exactly where complete_family would have stopped.
+    // a family's records: a pointer list, or (p null) consecutive records
+    struct RecList {
+        const Rec *const *p;
+        const Rec *base;
+        const Rec *operator[](size_t i) const { return p ? p[i] : base + i; }
+    };
     struct FamTask {
         const uint8_t *w;               // the window its records' offsets refer to
-        uint32_t rb, n;                 // the family's records: pend_recs[rb, rb + n)
+        uint32_t rb, n;                 // the family's records: pend_recs[rb, rb + n), or cbase[0, n)
+        const Rec *cbase = nullptr;     // set when they are consecutive in the record index (no copy)
         int32_t t, f;                   // table entry; processed family (-1: filtered)
         int64_t read_base, base_off[4], cig_off[4];   // per subfamily (split order)
         int64_t filt_off;               // filtered: its bytes in side_filt
@@ -1250,7 +1289,7 @@ struct dcr_ingest {
     static constexpr size_t kTkStep = 256;
 
     void run_task(FamTask &T, const uint8_t *w, dcr_host_batch *b) const {
-        const Rec *const *fr = pend_recs.data() + T.rb;
+        const RecList fr{T.cbase ? nullptr : pend_recs.data() + T.rb, T.cbase};
         std::string umi2;
         T.err_kind = check_family(fr, T.n, w, umi2, T.err);
         if (T.err_kind != DCR_ERR_NONE) return;
@@ -1319,9 +1358,11 @@ struct dcr_ingest {
         if (tasks.empty()) return 1;
         kick_tasks(true);
         {
+            const double tw = prof.on ? IngestProf::now() : 0;
             std::unique_lock<std::mutex> lk(pk_mu);
             pk_cv.wait(lk, [&] { return tk_done == tk_sub; });
             tk_sub = tk_done = 0;
+            if (prof.on) prof.tasks_wait += IngestProf::now() - tw;
         }
         for (const Retired &r : retired) infl->give_back(r.c);
         retired.clear();
@@ -1393,7 +1434,11 @@ struct dcr_ingest {
         // length the deferred UMI check (run_task) has not yet tied to r0's
         const int64_t l_rx0 = first[0] ? first[0]->l_rx : 0, l_rx2 = first[2] ? first[2]->l_rx : 0;
         const int64_t names_need = (int64_t)l_code + 1 + (l_rx0 + 1) + (l_rx2 + 1) + 64 * 2;
-        if (samples || pend_recs.size() + fam.size() > pend_recs.capacity() || tasks.size() == tasks.capacity()) {
+        // the family's records consecutive in the record index (not copies in fam_store)?
+        bool contig = fam.front() < fam_store.data() || fam.front() >= fam_store.data() + fam_store.size();
+        for (size_t j = 1; j < fam.size() && contig; ++j) contig = fam[j] == fam.front() + j;
+        if (samples || (!contig && pend_recs.size() + fam.size() > pend_recs.capacity()) ||
+            tasks.size() == tasks.capacity()) {
             if (flush_tasks() < 0) return -1;
             return complete_family();
         }
@@ -1478,15 +1523,22 @@ struct dcr_ingest {
             ++processed;
         }
         T.w = wb;
-        // records materialized into fam_store move with the next window
-        // (need() rewrites their offsets): the task keeps copies
+        // consecutive records of the record index (the common case): the task
+        // points at them, no per-record copy into pend_recs (whose 8-byte
+        // writes each cost a write-allocate miss: 25 cycles per read).
+        // Otherwise pointers; records materialized into fam_store move with
+        // the next window (need() rewrites their offsets): the task keeps copies
         const Rec *fs0 = fam_store.data(), *fs1 = fs0 + fam_store.size();
-        for (const Rec *r : fam) {
-            if (r >= fs0 && r < fs1) {
-                task_recs.push_back(*r);
-                pend_recs.push_back(&task_recs.back());
-            } else {
-                pend_recs.push_back(r);
+        if (contig) {
+            T.cbase = fam.front();
+        } else {
+            for (const Rec *r : fam) {
+                if (r >= fs0 && r < fs1) {
+                    task_recs.push_back(*r);
+                    pend_recs.push_back(&task_recs.back());
+                } else {
+                    pend_recs.push_back(r);
+                }
             }
         }
         tasks.push_back(std::move(T));
@@ -1650,7 +1702,7 @@ struct dcr_ingest {
     // check_family_UMIs (:100-113), every RX is umi1 or its swapped halves,
     // then check_family_rnames (:116-128), over the family's records fr[0, n)
     // in window w.  Returns DCR_ERR_NONE or the error kind with its message.
-    int check_family(const Rec *const *fr, size_t n, const uint8_t *w, std::string &umi2, std::string &msg) const {
+    int check_family(RecList fr, size_t n, const uint8_t *w, std::string &umi2, std::string &msg) const {
         const Rec &r0 = *fr[0];
         auto rx_at = [&](const Rec &r) { return (const char *)(w + r.off + r.o_rx); };
         auto code_at = [&](const Rec &r) { return r.l_code <= sizeof r.code ? r.code : (const char *)(w + r.off + r.o_mi); };
@@ -1714,7 +1766,7 @@ struct dcr_ingest {
         }
         {
             std::string msg;
-            const int kind = check_family(fam.data(), fam.size(), wb, umi2_, msg);
+            const int kind = check_family(RecList{fam.data(), nullptr}, fam.size(), wb, umi2_, msg);
             if (kind != DCR_ERR_NONE) return stop(kind, msg);
         }
         // split_family (:132-154), the subfamily of each read from parse_at
