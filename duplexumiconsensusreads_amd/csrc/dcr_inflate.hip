@@ -73,7 +73,7 @@ struct IStamp {
 // at 8 KiB / 10 bits) inflate a 4,096-member span in 5.65 ms instead of 9.09
 // (35.2 -> 47.5 GB/s over all members in one launch; profiles/r04e)
 #ifndef DINF_WG_PER_CU
-#define DINF_WG_PER_CU 0  // k_inflate launch grid cap per CU (0: one workgroup per member)
+#define DINF_WG_PER_CU 12 // k_inflate launch grid cap per CU (0: one workgroup per member)
 #endif
 #ifndef DINF_RING
 #define DINF_RING 4096    // LDS output history per member (bytes)
@@ -606,12 +606,14 @@ __device__ __forceinline__ void inflate_one(const Args &a, WaveLds &s, const int
     }
 }
 
-// Wave w takes members w, w + gridDim.x, ...  The grid is one workgroup per
-// member (DINF_WG_PER_CU 0).  A bounded resident grid (4 or 2 waves per CU)
-// lets the batch kernels beside a span start at once (k_recmeta<ss> per batch
-// 864 -> 44 us) but the serial member decode is latency-bound, so fewer waves
-// inflate slower (117 -> 266 / 390 ms of kernel time per pass) and the whole
-// node loses (357 -> 268 / 204 M consensus bases/s, profiles/r05r).
+// Wave w takes members w, w + gridDim.x, ...  The grid is capped at
+// DINF_WG_PER_CU workgroups per CU (12 of the 16 that fit), so a span never
+// holds every wave slot and LDS byte of a CU and the batch kernels beside it
+// find room at once.  The member decode is latency-bound: 4 or 2 waves per CU
+// starved the inflate (117 -> 266 / 390 ms of kernel time per pass) and the
+// whole node lost (357 -> 268 / 204 M consensus bases/s, profiles/r05r); once
+// the host walk stopped waiting for chunks, 12 per CU beat the uncapped grid
+// (profiles/r05ab: 429 vs 419 M at level 1, 470 vs 422 M at level 6).
 __global__ __launch_bounds__(64) void k_inflate(Args a) {
     WaveLds &s = *reinterpret_cast<WaveLds *>(smem);
     const int lane = lane_id();
