@@ -154,6 +154,27 @@ def test_gpu_fast_decision_borderline(ctx, maxq, minbq, qhi, sub):
     assert_same(packed, got, want)
 
 
+@pytest.mark.parametrize("maxq,minbq,qhi,sub,nfrac", [(93, 0, 93, 2, 0.05), (60, 30, 60, 2, 0.02),
+                                                      (60, 13, 45, 1, 0.05), (40, 2, 40, 3, 0.1)])
+def test_gpu_exact_small_records(ctx, maxq, minbq, qhi, sub, nfrac):
+    """Records of one to three reads, qualities over the whole range (masked
+    ones included) and sequenced 'N's: the exact pass's one-read table, its
+    two-read table (single-strand pairs and every duplex record, built by
+    k_r2_table at set_params) and its compacted products must match the
+    oracle bit for bit."""
+    packed = synth.packed_fixed_size(600, sub_size=sub, read_len=150, seed=maxq * 3 + qhi + sub)
+    rng = np.random.default_rng(maxq * 11 + qhi + sub)
+    q = packed.quals
+    q[:] = rng.integers(0, qhi + 1, q.shape, dtype=np.uint8)
+    b = packed.bases
+    b[rng.random(b.shape) < nfrac] = ord("N")
+    params = ConsensusParams(max_base_quality=maxq, min_base_quality=minbq)
+    ctx.set_params(params)
+    got = ctx.run_host(packed)
+    want = dcr_oracle_c.run(packed, params, n_threads=8)
+    assert_same(packed, got, want)
+
+
 @pytest.mark.parametrize("config,families", [("C3", 3000), ("C4", 24), ("C5", 3000)])
 def test_gpu_config_shapes_match_oracle(ctx, config, families):
     """The bench shapes of C3 (skewed sizes, indels, clips), C4 (100..1000
