@@ -262,6 +262,7 @@ def e2e_passes(path, params_args, device, steps, warmup, workdir):
     infl = cli._INFLATERS.get(device)
     if infl is not None:
         infl[0].totals(reset=True)
+    cpu0 = os.times()                   # the process's user + system CPU seconds (every thread)
     for i in range(steps):
         argv = argv_of(warmup + i)
         stats = {"trace": []}
@@ -272,11 +273,13 @@ def e2e_passes(path, params_args, device, steps, warmup, workdir):
         dt_pass = time.perf_counter() - t_pass
         dt += dt_pass
         passes.append(round(dt_pass, 4))
+    cpu1 = os.times()
     trace = stats.pop("trace")
     log("last pass timeline (ms from CLI start): " +
         " ".join(f"{k}[{(a - t_pass) * 1e3:.0f},{(b - t_pass) * 1e3:.0f}]" for k, a, b in trace))
     stats["first_pass_s"] = cold        # the cold first pass (allocations included)
     stats["passes_s"] = passes
+    stats["host_cpu_s_per_pass"] = round(((cpu1.user - cpu0.user) + (cpu1.system - cpu0.system)) / max(steps, 1), 4)
     if infl is not None:                # BGZF inflate on the device (cli.gpu_inflate)
         t = infl[0].totals()
         stats["gpu_inflate"] = {"kernel_ms_per_pass": t["kernel_ms"] / max(steps, 1),
@@ -502,6 +505,7 @@ def main():
             value_kind = "whole node: CLI from BAM open to output close"
         stage = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in stats.items() if k.endswith("_s")}
         stage["gpu_inflate"] = stats.get("gpu_inflate")
+        stage["host_cpu_s_per_pass"] = stats.get("host_cpu_s_per_pass")   # user + sys, every thread
         res = {
             "metric": METRIC, "value": value, "unit": "consensus bases/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,

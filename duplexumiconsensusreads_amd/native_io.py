@@ -16,7 +16,7 @@ import numpy as np
 from .batch import BATCH_FIELDS, BATCH_DTYPES, DcrBatch, PackedBatch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdcr_io.so")
+LIB_PATH = os.environ.get("DCR_IO_LIB", os.path.join(HERE, "libdcr_io.so"))   # DCR_IO_LIB: A/B builds (tools/)
 
 _i32, _i64, _vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p
 
