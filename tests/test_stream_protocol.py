@@ -151,7 +151,7 @@ def _run_raw(exe, bam, env_extra, timeout):
 @pytest.mark.parametrize("kind", ["", "_asan"])
 def test_round3_late_member_scan_is_a_clean_open_error(r3_drivers, bams, kind):
     big, _ = bams
-    r = _run_raw(os.path.join(r3_drivers, "r3_driver" + kind), big, {"DCR_R3_LATE_MS": "5"}, 120)
+    r = _run_raw(os.path.join(r3_drivers, "r3_driver" + kind), big, {"DCR_R3_LATE_MS": "100"}, 120)
     assert r.returncode == 4, (r.returncode, r.stdout[-1000:], r.stderr[-3000:])
     assert r.stderr.strip() == "open: not a BAM file", r.stderr[-3000:]
 
