@@ -19,7 +19,12 @@ with its inputs resident in HBM (K device-only passes, HIP events on the
 context stream): SURVEY.md §8d algorithmic bytes / average launch / 8 TB/s.
 config.device_resident holds that loop's consensus bases/s (kernels only).
 
-cpu_baseline: the C restatement (oracle/, kind "port") on the same batch.
+cpu_baseline: the whole node on the CPU, like for like with value: the same
+CLI over the same C2 BAM with the C restatement (oracle/, kind "port") as the
+consensus backend on the host cores, host BGZF inflate and host record
+writer / deflate (no GPU anywhere), timed from BAM open to output close; the
+cores are the box's CPU quota (cgroup cpu.max).  Its ``kernels_only`` field
+is the restatement alone on the packed batch (no BAM I/O).
 
 --config C3 / C4 / C5 runs the other BASELINE.json shapes (per-GPU shards).
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
@@ -145,6 +150,57 @@ def cpu_baseline(packed, reps):
             "sample": f"the whole bench batch ({packed.n_fam} families, {packed.n_reads} reads), "
                       f"C restatement oracle/dcr_oracle.c on {threads} threads, kernels only (no BAM I/O), "
                       f"best of {reps}: {dt:.2f} s per pass"}
+
+
+def cpu_cores():
+    """(cores of the process's CPU quota or None, os.cpu_count()): the GPU box
+    runs under a cgroup quota (cpu.max 1600000/100000 = 16 cores) on a host
+    with many more CPUs."""
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return quota, os.cpu_count()
+
+
+def cpu_baseline_whole_node(bam_path, params_args, workdir, reps, threads):
+    """The CLI drop-in over the bench BAM with no GPU: the C restatement as
+    the consensus backend (oracle/dcr_oracle_c.run on ``threads`` threads,
+    test infrastructure used here only as the timed CPU leg), the native
+    ingest's host inflate pool and the host record writer / BGZF deflate.
+    Best of ``reps`` passes, each from BAM open to output close."""
+    import contextlib
+    import io
+    import random
+    from duplexumiconsensusreads_amd import cli, native_io
+    from oracle import dcr_oracle_c
+
+    def oracle(packed, params):
+        return dcr_oracle_c.run(packed, params, n_threads=threads)
+
+    hook = native_io._HOOK
+    native_io.set_inflate_hook(None)            # the host inflate pool (no device inflater)
+    dts, st = [], {}
+    try:
+        for i in range(reps):
+            for f in os.listdir(workdir):
+                if f.startswith("cpu"):
+                    os.remove(os.path.join(workdir, f))
+            st = {}
+            random.seed(4)
+            t0 = time.perf_counter()
+            with contextlib.redirect_stdout(io.StringIO()):
+                cli.main(["-i", bam_path, "-o", os.path.join(workdir, f"cpu{i}.bam"), *params_args],
+                         backend=oracle, stats=st)
+            dts.append(time.perf_counter() - t0)
+    finally:
+        native_io.set_inflate_hook(hook)
+    dt = min(dts)
+    return st.get("consensus_bases", 0) / dt, dt, st
 
 
 def load_traffic(kernel, n_fam):
@@ -412,7 +468,7 @@ def main():
         workdir = wd[0]
     else:
         workdir = tempfile.mkdtemp(prefix=f"dcr_bench_r{rank}_", dir=os.environ.get("DCR_BENCH_DIR"))
-    stats, e2e_s, level6 = {}, None, None
+    stats, e2e_s, level6, cpu_whole = {}, None, None, None
     try:
         if not args.kernel_only:
             bam_path = os.path.join(workdir, "in.bam")
@@ -439,6 +495,14 @@ def main():
                 tdist.barrier()
             log(f"[rank {rank}] {args.steps} CLI passes in {e2e_s:.2f} s: "
                 f"{ {k: v for k, v in stats.items() if k != 'ranks'} }")
+            if not args.no_cpu and not dist and not args.sharded:
+                quota, ncpu = cpu_cores()
+                threads = int(quota) if quota else min(16, ncpu or 1)
+                v, dt, st = cpu_baseline_whole_node(bam_path, params_args, workdir, args.cpu_reps, threads)
+                cpu_whole = {"value": v, "pass_s": round(dt, 3), "threads": threads, "quota_cores": quota,
+                             "host_cpus": ncpu, "consensus_bases": st.get("consensus_bases")}
+                log(f"[rank {rank}] CPU whole node (oracle backend, host codecs): {v / 1e6:.1f} M consensus "
+                    f"bases/s, {dt:.2f} s per pass")
             if args.level6_passes > 0 and not dist and not args.sharded and args.in_level != 6:
                 # the same families from a level-6 input (a BAM as aligners
                 # write it): more inflate work per byte, not the headline
@@ -545,7 +609,22 @@ def main():
                          "traffic_source": (f"profiles/traffic.json ({tsrc.get('source', '')})" if tsrc else None)},
         }
         if not args.no_cpu and world == 1:
-            res["cpu_baseline"] = cpu_baseline(packed, args.cpu_reps)
+            ko = cpu_baseline(packed, args.cpu_reps)
+            if cpu_whole is not None:
+                # like for like with value: the whole CLI pass on the CPU
+                res["cpu_baseline"] = {
+                    "value": cpu_whole["value"], "unit": "consensus bases/s",
+                    "cores": cpu_whole["quota_cores"] or cpu_whole["threads"], "kind": "port",
+                    "sample": (f"the whole-node CLI (cli.main, DuplexUMIConsensusReads.py:1426-1650) over the same "
+                               f"{packed.n_reads}-read C2 BAM, best of {args.cpu_reps} passes "
+                               f"({cpu_whole['pass_s']:.2f} s per pass): consensus by the C restatement "
+                               f"oracle/dcr_oracle.c on {cpu_whole['threads']} threads, host BGZF inflate pool, "
+                               f"host record writer and deflate; no GPU"),
+                    "threads": cpu_whole["threads"], "quota_cores": cpu_whole["quota_cores"],
+                    "host_cpus": cpu_whole["host_cpus"], "gpu_over_cpu": value / cpu_whole["value"],
+                    "kernels_only": ko}
+            else:
+                res["cpu_baseline"] = ko
         else:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)

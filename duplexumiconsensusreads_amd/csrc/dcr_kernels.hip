@@ -47,11 +47,23 @@
 #ifndef DCR_ROWS
 #define DCR_ROWS 1    // fast kernel: decided scalars as one 16-byte row per record, expanded by k_fast_rows
 #endif
+#ifndef DCR_DEFER
+#define DCR_DEFER 1   // fast kernel: a record's row stored after the next record's staging (its vmcnt(0) does not wait
+                      // for it; deferring the column stores too held registers across the loop and was slower)
+#endif
+#ifndef DCR_ST4
+#define DCR_ST4 0     // fast kernel (common instantiation): column stores four columns per lane through the free stage
+                      // (4 stores per record instead of 4 per tile: measured level, profiles/r06h)
+#endif
 #ifndef DCR_ABL
 #define DCR_ABL 0   // diagnostic builds only (tools/ablate.py); fast kernel: 1 staging only, 2 +products,
-                    // 4 always the exact pairwise mean, 5 no per-column stores
+                    // 4 always the exact pairwise mean, 5 no per-column stores, 6 every single-strand record
+                    // staged from the fast list's first record's bytes (cache-resident: the kernel without its
+                    // HBM reads)
 #endif
 
+#define DCR_STR_(x) #x
+#define DCR_STR(x) DCR_STR_(x)
 namespace dcr {
 
 constexpr int kStageElems = 2048;        // per-wave LDS staging (16-bit codes)
@@ -2384,7 +2396,6 @@ constexpr int kBlockThreads = kFastBlock;
 constexpr int kRowMax = 122;                               // quality rows 0..122
 constexpr uint32_t kPadCode = 16u * 2u;                    // class N, quality 2 (:509-510, :543-544)
 constexpr uint32_t kPadCode8 = 8u * 2u;                    // the same in the narrow table (common instantiation)
-constexpr int kNMax = 0x800;                               // codes below: class N
 constexpr int kTable = 5 * 0x800;                          // 5 class banks of 2 KiB (narrow: of 1 KiB)
 constexpr int kTable8 = 5 * 0x400;
 constexpr int kPtrs = kTable;                              // u64 [32] pointers (kP* below)
@@ -2452,9 +2463,10 @@ struct FastStage {
 // voffset 4 lane + immediate 256 u, no per-lane address arithmetic, and bytes
 // past the end of the array read as 0 (range-checked) instead of faulting.
 template <bool DUPLEX, int NDW>
-__device__ __forceinline__ void fast_load(const FastArgs &a, const RecMeta &m, const RecMeta *mlater, int lane,
+__device__ __forceinline__ void fast_load(const FastArgs &a, RecMeta m, const RecMeta *mlater, int lane,
                                           FastStage<NDW> &st) {
     const int ndw = (int)(m.w >> 15);
+    if (DCR_ABL == 6 && !DUPLEX) m.base_al = a.meta[0].base_al;   // diagnostic: cache-resident bytes
     // range: the array's last dword read whole (device allocations are padded
     // to at least 16 bytes, as the 16-byte-aligned staging already assumes)
     const int64_t left = ((a.nbytes + 3) & ~(int64_t)3) - m.base_al;
@@ -2471,6 +2483,7 @@ __device__ __forceinline__ void fast_load(const FastArgs &a, const RecMeta &m, c
         }
     }
     const int R = (int)(m.w & 127u);
+    if (DCR_ABL == 6 && !DUPLEX) m.g0 = a.meta[0].g0;
     st.rm = a.rmeta[m.g0 + min(lane, R - 1)];
     st.mv = ((const uint32_t *)mlater)[lane & 7];
 }
@@ -2801,14 +2814,18 @@ template <bool DUPLEX>
 __device__ __forceinline__ void send_to_general_(int rec, int g0, int R, uint32_t rmx, const uint8_t *lds, int lane) {
     if (!DUPLEX && lane < R) {
         const int tl = ((int)rmx >> 8) & 255;
-        uint32_t *norm_cig = lds_ptr<uint32_t>(lds, fk::kPNormCig);
-        const int32_t *cig_off = lds_ptr<const int32_t>(lds, fk::kPCigOff);
+        DCR_G uint32_t *norm_cig = lds_sgptr<uint32_t>(lds, fk::kPNormCig);
+        const DCR_G int32_t *cig_off = lds_sgptr<const int32_t>(lds, fk::kPCigOff);
         if (tl > 0) norm_cig[cig_off[g0 + lane]] = (uint32_t)tl << 4;   // one M run
     }
-    int *ovf = lds_ptr<int>(lds, fk::kPOvf);
-    int *ovf_count = lds_ptr<int>(lds, fk::kPOvfCount);
+    // global (not generic) pointers: a flat store or atomic left pending on
+    // this rare path made the record loop's waitcnt model assume FLAT events
+    // at its header, so the staging's wait for the prefetch was a vmcnt(0)
+    // that also waited for the previous record's stores
+    DCR_G int *ovf = lds_sgptr<int>(lds, fk::kPOvf);
+    DCR_G int *ovf_count = lds_sgptr<int>(lds, fk::kPOvfCount);
     if (lane == 0) {
-        const int idx = atomicAdd(ovf_count, 1);
+        const int idx = __hip_atomic_fetch_add(ovf_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ovf[idx] = rec;
     }
 }
@@ -2973,12 +2990,17 @@ __device__ __forceinline__ double div1000(int k) {
 // a status was written (nothing else to do)
 constexpr int kFinQueue = 0, kFinDone = 1, kFinStatus = 2;
 
+// a decided record's row (lanes 0-3), held until the next record is staged (DCR_DEFER)
+struct Pend {
+    uint32_t v;
+};
+
 template <bool DUPLEX, int NT, bool EXACT>
 __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m, const Staged &sg, uint8_t *lds,
                                              const int stage_addr, const int ov_addr, const int rm_addr, const int list_addr,
                                              const int lane,
                                              Stamps &sp, const double2 *xt, const uint32_t *r1, const double *qt,
-                                             const int fi) {
+                                             const int fi, Pend &pd) {
     const int64_t rec = m.rec;
     const int64_t off = m.off;
     const int R = (int)(m.w & 127u);
@@ -3102,16 +3124,27 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
         if (EXACT) *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (kb << 12));
         if (!EXACT && DCR_ABL != 5) {
             // "ATCG"[call] and maxQ; past T (last tile only) 'N' / 0
-            uint32_t letter = __builtin_amdgcn_perm(0u, 0x47435441u, kb), qv = (uint32_t)a.maxq;
+            // maxQ made where it is stored (opaque): a VGPR copy hoisted out of
+            // the record loop was spilled to scratch, and its reload's
+            // vmcnt(0) waited for the next record's prefetch mid-decision
+            uint32_t letter = __builtin_amdgcn_perm(0u, 0x47435441u, kb), qv = (uint32_t)opaque(a.maxq);
             if (tt == NT - 1) {
                 letter = t < T ? letter : 0x4Eu;
                 qv = t < T ? qv : 0u;
             }
+            if (DCR_ST4) {
+                // the column word (d | e << 6 | sel << 12, sel = the call or
+                // 4: 'N' / quality 0 past T) into the free stage; the stores
+                // go four columns per lane once the record is known decided
+                const uint32_t sel = tt == NT - 1 && t >= T ? 4u : kb;
+                *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (sel << 12));
+            } else {
             // the tile's offset as the scalar offset (no per-tile vector add)
             __builtin_amdgcn_raw_buffer_store_b16((uint16_t)d, DCR_RSRC_D, 2 * lane, 128 * tt, 0);
             __builtin_amdgcn_raw_buffer_store_b16((uint16_t)e, DCR_RSRC_E, 2 * lane, 128 * tt, 0);
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)letter, DCR_RSRC_S, lane, 64 * tt, 0);
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)qv, DCR_RSRC_Q, lane, 64 * tt, 0);
+            }
         }
         fx += live ? __umul24((uint32_t)e, m720[d]) : 0u;
         dmax = max(dmax, live ? d : -1);
@@ -3126,6 +3159,30 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
     sp.mark(12);                         // [11] decision (of [5] finalize)
     const bool exact = __ballot(und) != 0;
     if (!EXACT && exact) return kFinQueue;
+    if (!EXACT && DCR_ST4 && DCR_ABL != 5) {
+        // d / e / seq / qual four columns per lane (8-, 8-, 4- and 4-byte
+        // stores): 4 store instructions per record instead of 4 per tile.
+        // The vector memory path pays per instruction (and per lane), not per
+        // byte: a C2 record's twelve 1- and 2-byte stores cost the kernel
+        // ~20 % (profiles/r06g), range-checked-out ones nothing.
+        lds_fence();
+        const int c0 = 4 * lane;
+        if (c0 < T16) {
+            const uint2 w = *(const uint2 *)(ov + 8 * lane);
+            const uint32_t sel = ((w.x >> 12) & 7u) | ((w.x >> 20) & 0x700u) | ((w.y << 4) & 0x70000u) |
+                                 ((w.y >> 4) & 0x7000000u);
+            const uint32_t letters = __builtin_amdgcn_perm(0x4Eu, 0x47435441u, sel);            // "ATCG"[call] or 'N'
+            const uint32_t quals = __builtin_amdgcn_perm(0u, (uint32_t)a.maxq * 0x01010101u, sel); // maxQ or 0
+            DCR_G uint16_t *pdp = lds_sgptr<uint16_t>(lds, fk::kPD);
+            DCR_G uint16_t *pep = lds_sgptr<uint16_t>(lds, fk::kPE);
+            DCR_G uint8_t *psp = lds_sgptr<uint8_t>(lds, fk::kPSeq);
+            DCR_G uint8_t *pqp = lds_sgptr<uint8_t>(lds, fk::kPQual);
+            *(DCR_G uint2 *)(pdp + off + c0) = make_uint2(w.x & 0x003F003Fu, w.y & 0x003F003Fu);
+            *(DCR_G uint2 *)(pep + off + c0) = make_uint2((w.x >> 6) & 0x003F003Fu, (w.y >> 6) & 0x003F003Fu);
+            *(DCR_G uint32_t *)(psp + off + c0) = letters;
+            *(DCR_G uint32_t *)(pqp + off + c0) = quals;
+        }
+    }
     // exact columns' character | quality << 8, as u16 per column in the wave's
     // read-word LDS (free once the read words are in registers)
     uint16_t *chq = (uint16_t *)(lds + rm_addr);
@@ -3452,8 +3509,10 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
         v = write_lane<3>(v, 1u);
         // lanes 0-3 (a buffer store on the row's 16 bytes: the other lanes'
         // words fall outside it, no branch)
-        __builtin_amdgcn_raw_buffer_store_b32(v, __builtin_amdgcn_make_buffer_rsrc((void *)(a.rows + fi), (short)0, 16,
-                                                                                       0x00020000), 4 * lane, 0, 0);
+        if (DCR_DEFER) pd.v = v;         // the caller stores it after the next record's staging
+        else
+            __builtin_amdgcn_raw_buffer_store_b32(v, __builtin_amdgcn_make_buffer_rsrc((void *)(a.rows + fi), (short)0, 16,
+                                                                                           0x00020000), 4 * lane, 0, 0);
         sp.mark(10);                     // [9] record scalars
         return kFinDone;
     }
@@ -3641,17 +3700,61 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? DCR_EXACT_OCC : DCR_FAST
     int xv = EXACT ? a.xlist[opaque(nxt(i2))] : 0;
     Stamps sp;
     int pend = 0, npend = 0;           // !EXACT: queued fast-list indices (lane p holds the p-th)
+    // DCR_DEFER: the last decided record's row, stored once the next record's
+    // bytes are staged: every VMEM store still in flight at a staging is
+    // waited for there (loads and stores share vmcnt on gfx950, so the wait
+    // for the prefetch is a vmcnt(0)), and the row was the record's last store
+    Pend pd;
+    pd.v = 0;
+    int row_i = -1;                    // the pending record's fast-list index (-1: none)
+    auto store_row = [&](int ln) {
+        if (!EXACT && DCR_ROWS && DCR_DEFER && row_i >= 0) {
+            __builtin_amdgcn_raw_buffer_store_b32(pd.v, __builtin_amdgcn_make_buffer_rsrc((void *)(a.rows + row_i), (short)0,
+                                                                                          16, 0x00020000), 4 * ln, 0, 0);
+            row_i = -1;
+            pd.v = 0;
+        }
+    };
     auto flush = [&](int ln) {         // queue pointers from the LDS cache (no scalar registers held)
         int base = 0;
-        if (ln == 0) base = atomicAdd(lds_ptr<int>(lds, fk::kPXcount), npend);
+        if (ln == 0) base = __hip_atomic_fetch_add(lds_sgptr<int>(lds, fk::kPXcount), npend, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
         base = __builtin_amdgcn_readfirstlane(base);
-        if (ln < npend) lds_ptr<int>(lds, fk::kPXlist)[base + ln] = pend;
+        if (ln < npend) lds_sgptr<int>(lds, fk::kPXlist)[base + ln] = pend;
         npend = 0;
     };
     for (;;) {
         // lane-derived addresses are formed per record, not hoisted out of the
         // record loop into registers held across it
         const int lane = opaque(lane0);
+#if defined(DCR_PADV) && !defined(DCR_NO_PAD)
+        if (!EXACT && !DUPLEX) {        // diagnostic builds only: extra VALU issue per record
+            int dv;
+            asm volatile(".rept " DCR_STR(DCR_PADV) "\n v_mov_b32 %0, 0\n .endr" : "=v"(dv));
+        }
+#endif
+#if defined(DCR_PADM) && !defined(DCR_NO_PAD)
+        if (!EXACT && !DUPLEX) {        // diagnostic builds only: extra VMEM stores per record (range-checked out)
+            const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void *)a.rows, (short)0, 0, 0x00020000);
+#pragma unroll
+            for (int k = 0; k < DCR_PADM; ++k) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)lane, rz, lane, 64 * k, 0);
+        }
+#endif
+#if defined(DCR_PADL) && !defined(DCR_NO_PAD)
+        if (!EXACT && !DUPLEX) {        // diagnostic builds only: extra VMEM loads per record (range-checked out)
+            const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void *)a.rows, (short)0, 0, 0x00020000);
+            uint32_t acc = 0;
+#pragma unroll
+            for (int k = 0; k < DCR_PADL; ++k) acc += __builtin_amdgcn_raw_buffer_load_b32(rz, 4 * lane, 256 * k, 0);
+            asm volatile("" :: "v"(acc));
+        }
+#endif
+#if defined(DCR_PADS) && !defined(DCR_NO_PAD)
+        if (!EXACT && !DUPLEX) {        // diagnostic builds only: extra SALU issue per record
+            int ds;
+            asm volatile(".rept " DCR_STR(DCR_PADS) "\n s_mov_b32 %0, 0\n .endr" : "=s"(ds));
+        }
+#endif
         sp.mark(0);
         if (DCR_STAMP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         sp.mark(1);                    // [0] wait for this record's prefetched bytes
@@ -3682,12 +3785,14 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? DCR_EXACT_OCC : DCR_FAST
         const int i3 = nxt(i2);
         fast_load<DUPLEX>(a, m1, ML + (EXACT ? __builtin_amdgcn_readfirstlane(xv) : i3), lane, st);
         if (EXACT) xv = a.xlist[opaque(nxt(i3))];
+        store_row(lane);
         sp.mark(3);                    // [2] prefetch issue
         lds_fence();
         const uint2 rw = *(const uint2 *)(lds + rm_addr + 8 * lane);
         // the read's word relative to this record: col | len << 8 | mapq << 16, stage offset
-        const uint2 rm = make_uint2((uint32_t)(((int)rw.x >> 16) + (m0.d0 & 0xFFFF)) | (rw.x & 0xFFFFu) << 8,
-                                    rw.y - m0.base_al);
+        const uint2 rm = make_uint2((uint32_t)(((int)rw.x >> 16) + ((DCR_ABL == 6 && !DUPLEX ? a.meta[0].d0 : m0.d0) & 0xFFFF)) |
+                                        (rw.x & 0xFFFFu) << 8,
+                                    rw.y - (DCR_ABL == 6 && !DUPLEX ? a.meta[0].base_al : m0.base_al));
         const RecMeta m2 = meta_from_lanes(*(const uint32_t *)(lds + fk::kMv + 32 * wave + 4 * (lane & 7)));   // record i2
         // a record this kernel does not decide gets an empty row (kind 0:
         // k_fast_rows leaves its scalars to the kernel that finishes it)
@@ -3713,12 +3818,17 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? DCR_EXACT_OCC : DCR_FAST
             send_to_general<DUPLEX>(a, m0, sg.rm, lds, lane);
             no_row();
         } else if (sg.state == 0 || sg.state == 3) {
+            // NT comes from T before a state-3 record's 3' trim (finish_record
+            // runs it): a trim that shrinks T by a whole tile leaves all-'N'
+            // live columns in the earlier tiles, undecided, so such a (rare)
+            // record takes the EXACT queue instead of being decided here
             int fin;
-            if (sg.T <= 64) fin = finish_record<DUPLEX, 1, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, list_addr, lane, sp, s_xt, s_r1, s_qt, i);
-            else if (sg.T <= 128) fin = finish_record<DUPLEX, 2, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, list_addr, lane, sp, s_xt, s_r1, s_qt, i);
-            else if (sg.T <= 192) fin = finish_record<DUPLEX, 3, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, list_addr, lane, sp, s_xt, s_r1, s_qt, i);
-            else fin = finish_record<DUPLEX, 4, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, list_addr, lane, sp, s_xt, s_r1, s_qt, i);
+            if (sg.T <= 64) fin = finish_record<DUPLEX, 1, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, list_addr, lane, sp, s_xt, s_r1, s_qt, i, pd);
+            else if (sg.T <= 128) fin = finish_record<DUPLEX, 2, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, list_addr, lane, sp, s_xt, s_r1, s_qt, i, pd);
+            else if (sg.T <= 192) fin = finish_record<DUPLEX, 3, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, list_addr, lane, sp, s_xt, s_r1, s_qt, i, pd);
+            else fin = finish_record<DUPLEX, 4, EXACT>(a, m0, sg, lds, stage_addr, ov_addr, rm_addr, list_addr, lane, sp, s_xt, s_r1, s_qt, i, pd);
             if (!EXACT && fin != kFinDone) no_row();
+            if (!EXACT && DCR_DEFER && fin == kFinDone) row_i = i;
             if (!EXACT && fin == kFinQueue) {
                 if (lane == npend) pend = i;
                 if (++npend == kWave) flush(lane);
@@ -3732,6 +3842,7 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? DCR_EXACT_OCC : DCR_FAST
         m1 = m2;
         i2 = i3;
     }
+    store_row(lane0);
     if (!EXACT && npend) flush(lane0);
     if (DCR_STAMP && lane0 == 0)
         for (int k = 0; k < 12; ++k)   // fast ss 0-11, ds 16-27; exact ss 32-43, ds 48-59
@@ -3776,6 +3887,7 @@ __global__ __launch_bounds__(256) void k_r2_table(const dcr_params *P, uint32_t 
 // double pairwise walk): the record goes on its queue.  Kind 2 rows carry an
 // E the fast kernel stored itself.
 __global__ __launch_bounds__(256) void k_fast_rows(FastArgs a) {
+    if (!DCR_ROWS) return;                       // rows are written (and zeroed) only by DCR_ROWS builds
     const int i = (int)(blockIdx.x * 256u + threadIdx.x);
     if (i >= *a.fast_count) return;
     const uint4 row = a.rows[i];

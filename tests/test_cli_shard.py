@@ -88,7 +88,14 @@ def compare(tmp_path, in_bam, extra, seed, world, expect_exc=None, expect_rounds
     one = str(tmp_path / "one.bam")
     many = str(tmp_path / "many.bam")
     out1, exc1, st1 = _outcome(["-i", in_bam, "-o", one, *extra], seed)
-    got = run_sharded(["-i", in_bam, "-o", many, *extra], seed, world)
+    # ranks > 0 write their parts here (cli._part_dir), rank 0 the final files
+    part_dir = tmp_path / "parts"
+    part_dir.mkdir(exist_ok=True)
+    os.environ["DCR_PART_DIR"] = str(part_dir)
+    try:
+        got = run_sharded(["-i", in_bam, "-o", many, *extra], seed, world)
+    finally:
+        del os.environ["DCR_PART_DIR"]
     out0, exc0, st0, rounds = got[0]
     assert exc1 == expect_exc
     assert exc0 == exc1
@@ -102,7 +109,7 @@ def compare(tmp_path, in_bam, extra, seed, world, expect_exc=None, expect_rounds
     if expect_rounds is not None:
         assert max(g[3][0] or 0 for g in got.values()) == expect_rounds
     # nothing left behind but the three outputs
-    left = sorted(p.name for p in tmp_path.iterdir() if ".part" in p.name)
+    left = sorted(p.name for p in tmp_path.iterdir() if ".part" in p.name) + sorted(p.name for p in part_dir.iterdir())
     assert left == []
     return got
 

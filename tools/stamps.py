@@ -1,5 +1,5 @@
 """Diagnostic: per-phase s_memtime cycle totals of the fast consensus kernel
-(a DCR_STAMP=1 build of libdcr, tools/build_ablate.sh) on the C2 batch.
+(a DCR_STAMP=1 build of libdcr: tools/build_variant.sh stamp "-DDCR_STAMP=1") on the C2 batch.
 usage: python tools/stamps.py FAMILIES LIB"""
 import ctypes
 import os
