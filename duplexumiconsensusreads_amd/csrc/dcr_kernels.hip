@@ -51,6 +51,18 @@
 #define DCR_DEFER 1   // fast kernel: a record's row stored after the next record's staging (its vmcnt(0) does not wait
                       // for it; deferring the column stores too held registers across the loop and was slower)
 #endif
+#ifndef DCR_LCPOL
+#define DCR_LCPOL 0   // fast kernel: cache policy of the staging loads (gfx950 aux bits: 2 = nt)
+#endif
+#ifndef DCR_SCPOL
+#define DCR_SCPOL 0   // fast kernel: cache policy of the column stores
+#endif
+#ifndef DCR_VMPAD
+#define DCR_VMPAD 0   // fast kernel: range-checked-out stores after the prefetch (see the record loop)
+#endif
+#ifndef DCR_STRIDE
+#define DCR_STRIDE 1  // fast kernel: evenly spaced reads' codes addressed by a stepped VGPR (no per-read readlane)
+#endif
 #ifndef DCR_ST4
 #define DCR_ST4 0     // fast kernel (common instantiation): column stores four columns per lane through the free stage
                       // (4 stores per record instead of 4 per tile: measured level, profiles/r06h)
@@ -59,7 +71,8 @@
 #define DCR_ABL 0   // diagnostic builds only (tools/ablate.py); fast kernel: 1 staging only, 2 +products,
                     // 4 always the exact pairwise mean, 5 no per-column stores, 6 every single-strand record
                     // staged from the fast list's first record's bytes (cache-resident: the kernel without its
-                    // HBM reads)
+                    // HBM reads), 7 column stores cache-resident (DCR_RSRC_*), 8 column stores at
+                    // 64-column-aligned offsets (records overlap: timing only)
 #endif
 
 #define DCR_STR_(x) #x
@@ -2478,8 +2491,8 @@ __device__ __forceinline__ void fast_load(const FastArgs &a, RecMeta m, const Re
 #pragma unroll
     for (int u = 0; u < NDW; ++u) {
         if (u * kWave < ndw) {
-            st.vb[u] = __builtin_amdgcn_raw_buffer_load_b32(rb, 4 * lane + 256 * u, 0, 0);
-            st.vq[u] = __builtin_amdgcn_raw_buffer_load_b32(rq, 4 * lane + 256 * u, 0, 0);
+            st.vb[u] = __builtin_amdgcn_raw_buffer_load_b32(rb, 4 * lane + 256 * u, 0, DCR_LCPOL);
+            st.vq[u] = __builtin_amdgcn_raw_buffer_load_b32(rq, 4 * lane + 256 * u, 0, DCR_LCPOL);
         }
     }
     const int R = (int)(m.w & 127u);
@@ -2546,6 +2559,52 @@ __device__ __forceinline__ void run_evidence8(Evidence8<NT> &ev, const uint8_t *
                                               int lane) {
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) ev.lo[tt] = ev.hi[tt] = 0u;
+    if (FULL && DCR_STRIDE) {
+        // the reads' stage addresses evenly spaced (reads of one length packed
+        // back to back: the C2 shape): a lane's code address is one VGPR
+        // stepped by the stride, with no per-read readlane or scalar clamp.
+        // The last step's codes of reads R, R + 1 are loaded from past the
+        // record and never used (LDS reads past the allocation return 0).
+        const int cr0 = readlane(crv, 0);
+        const int step = R > 1 ? readlane(crv, 1) - cr0 : 0;
+        if (__ballot(lane < R && crv != cr0 + lane * step) == 0) {
+            const uint8_t *p = lds + cr0 + 2 * lane;
+            auto codes_at = [&](const uint8_t *q, uint32_t (&cd)[NT]) {
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt) cd[tt] = *(const uint16_t *)(q + 128 * tt);
+            };
+            uint32_t c0[NT], c1[NT];
+            codes_at(p, c0);
+            codes_at(p + step, c1);
+            p += 2 * step;
+            int r = 0;
+            for (; r + 2 <= R; r += 2) {
+                uint2 f0[NT], f1[NT];
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt) {
+                    f0[tt] = *(const uint2 *)(lds + c0[tt]);
+                    f1[tt] = *(const uint2 *)(lds + c1[tt]);
+                }
+                codes_at(p, c0);
+                codes_at(p + step, c1);
+                p += 2 * step;
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt) {
+                    ev.lo[tt] += f0[tt].x + f1[tt].x;
+                    ev.hi[tt] += f0[tt].y + f1[tt].y;
+                }
+            }
+            if (r < R) {
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt) {
+                    const uint2 f0 = *(const uint2 *)(lds + c0[tt]);
+                    ev.lo[tt] += f0.x;
+                    ev.hi[tt] += f0.y;
+                }
+            }
+            return;
+        }
+    }
     auto codes = [&](int r, uint32_t (&cd)[NT]) {
         const int rr = min(r, R - 1);
         const int cr = readlane(crv, rr);          // stage address of the read's column 0
@@ -3070,10 +3129,13 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
     // branching around them (no exec-mask branch in the loop over tiles)
     // (made where they are used, so their 16 scalar registers are not held
     // across the tile loop; unused in the EXACT instantiation)
-#define DCR_RSRC_D __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.d + off), (short)0, 2 * T16, 0x00020000)
-#define DCR_RSRC_E __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.e + off), (short)0, 2 * T16, 0x00020000)
-#define DCR_RSRC_S __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.seq + off), (short)0, T16, 0x00020000)
-#define DCR_RSRC_Q __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.qual + off), (short)0, T16, 0x00020000)
+// (DCR_ABL 7, diagnostic: every record's columns stored over the first 4,096
+// columns of the arrays, cache-resident: the stores without their HBM traffic)
+#define DCR_OFF_ (DCR_ABL == 7 ? (off & 4095) : DCR_ABL == 8 ? (off & ~(int64_t)63) : off)
+#define DCR_RSRC_D __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.d + DCR_OFF_), (short)0, 2 * T16, 0x00020000)
+#define DCR_RSRC_E __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.e + DCR_OFF_), (short)0, 2 * T16, 0x00020000)
+#define DCR_RSRC_S __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.seq + DCR_OFF_), (short)0, T16, 0x00020000)
+#define DCR_RSRC_Q __builtin_amdgcn_make_buffer_rsrc((void *)(a.O.qual + DCR_OFF_), (short)0, T16, 0x00020000)
     // more reads than r_safe: L_b may underflow (fast_constants), no column is decided here
     const bool force = R > a.r_safe;
     int dmax = -1, dmin = 0x7fffffff;
@@ -3140,10 +3202,10 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
                 *(uint16_t *)(ov + 2 * t) = (uint16_t)((uint32_t)d | ((uint32_t)e << 6) | (sel << 12));
             } else {
             // the tile's offset as the scalar offset (no per-tile vector add)
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)d, DCR_RSRC_D, 2 * lane, 128 * tt, 0);
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)e, DCR_RSRC_E, 2 * lane, 128 * tt, 0);
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)letter, DCR_RSRC_S, lane, 64 * tt, 0);
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)qv, DCR_RSRC_Q, lane, 64 * tt, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)d, DCR_RSRC_D, 2 * lane, 128 * tt, DCR_SCPOL);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)e, DCR_RSRC_E, 2 * lane, 128 * tt, DCR_SCPOL);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)letter, DCR_RSRC_S, lane, 64 * tt, DCR_SCPOL);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)qv, DCR_RSRC_Q, lane, 64 * tt, DCR_SCPOL);
             }
         }
         fx += live ? __umul24((uint32_t)e, m720[d]) : 0u;
@@ -3166,22 +3228,19 @@ __device__ __forceinline__ int finish_record(const FastArgs &a, const RecMeta &m
         // byte: a C2 record's twelve 1- and 2-byte stores cost the kernel
         // ~20 % (profiles/r06g), range-checked-out ones nothing.
         lds_fence();
-        const int c0 = 4 * lane;
-        if (c0 < T16) {
-            const uint2 w = *(const uint2 *)(ov + 8 * lane);
-            const uint32_t sel = ((w.x >> 12) & 7u) | ((w.x >> 20) & 0x700u) | ((w.y << 4) & 0x70000u) |
-                                 ((w.y >> 4) & 0x7000000u);
-            const uint32_t letters = __builtin_amdgcn_perm(0x4Eu, 0x47435441u, sel);            // "ATCG"[call] or 'N'
-            const uint32_t quals = __builtin_amdgcn_perm(0u, (uint32_t)a.maxq * 0x01010101u, sel); // maxQ or 0
-            DCR_G uint16_t *pdp = lds_sgptr<uint16_t>(lds, fk::kPD);
-            DCR_G uint16_t *pep = lds_sgptr<uint16_t>(lds, fk::kPE);
-            DCR_G uint8_t *psp = lds_sgptr<uint8_t>(lds, fk::kPSeq);
-            DCR_G uint8_t *pqp = lds_sgptr<uint8_t>(lds, fk::kPQual);
-            *(DCR_G uint2 *)(pdp + off + c0) = make_uint2(w.x & 0x003F003Fu, w.y & 0x003F003Fu);
-            *(DCR_G uint2 *)(pep + off + c0) = make_uint2((w.x >> 6) & 0x003F003Fu, (w.y >> 6) & 0x003F003Fu);
-            *(DCR_G uint32_t *)(psp + off + c0) = letters;
-            *(DCR_G uint32_t *)(pqp + off + c0) = quals;
-        }
+        // lanes past the region (4 lane >= T16) are dropped by the resources' range checks
+        const uint2 w = *(const uint2 *)(ov + 8 * lane);
+        const uint32_t sel = ((w.x >> 12) & 7u) | ((w.x >> 20) & 0x700u) | ((w.y << 4) & 0x70000u) |
+                             ((w.y >> 4) & 0x7000000u);
+        const uint32_t letters = __builtin_amdgcn_perm(0x4Eu, 0x47435441u, sel);            // "ATCG"[call] or 'N'
+        const uint32_t quals = __builtin_amdgcn_perm(0u, (uint32_t)a.maxq * 0x01010101u, sel); // maxQ or 0
+        typedef int v2i __attribute__((ext_vector_type(2)));
+        const v2i dv = {(int)(w.x & 0x003F003Fu), (int)(w.y & 0x003F003Fu)};
+        const v2i evv = {(int)((w.x >> 6) & 0x003F003Fu), (int)((w.y >> 6) & 0x003F003Fu)};
+        __builtin_amdgcn_raw_buffer_store_b64(dv, DCR_RSRC_D, 8 * lane, 0, DCR_SCPOL);
+        __builtin_amdgcn_raw_buffer_store_b64(evv, DCR_RSRC_E, 8 * lane, 0, DCR_SCPOL);
+        __builtin_amdgcn_raw_buffer_store_b32(letters, DCR_RSRC_S, 4 * lane, 0, DCR_SCPOL);
+        __builtin_amdgcn_raw_buffer_store_b32(quals, DCR_RSRC_Q, 4 * lane, 0, DCR_SCPOL);
     }
     // exact columns' character | quality << 8, as u16 per column in the wave's
     // read-word LDS (free once the read words are in registers)
@@ -3698,6 +3757,11 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? DCR_EXACT_OCC : DCR_FAST
     // as a vector load (the descriptor load of the prefetch depends on it; a
     // scalar load issued there stalled the issue for its whole latency)
     int xv = EXACT ? a.xlist[opaque(nxt(i2))] : 0;
+    if (!EXACT && DCR_VMPAD > 0) {      // the same padding as after every later prefetch (the loop's entry path too)
+        const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void *)a.rows, (short)0, 0, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < DCR_VMPAD; ++k) __builtin_amdgcn_raw_buffer_store_b32(0u, rz, 4 * lane0, 256 * k, 0);
+    }
     Stamps sp;
     int pend = 0, npend = 0;           // !EXACT: queued fast-list indices (lane p holds the p-th)
     // DCR_DEFER: the last decided record's row, stored once the next record's
@@ -3786,6 +3850,17 @@ __global__ __launch_bounds__(fk::kBlockThreads, EXACT ? DCR_EXACT_OCC : DCR_FAST
         fast_load<DUPLEX>(a, m1, ML + (EXACT ? __builtin_amdgcn_readfirstlane(xv) : i3), lane, st);
         if (EXACT) xv = a.xlist[opaque(nxt(i3))];
         store_row(lane);
+        if (!EXACT && DCR_VMPAD > 0) {
+            // DCR_VMPAD stores that the range check drops (no memory access)
+            // right after the prefetch: every path through the record now
+            // issues at least that many VMEM ops after the prefetch's loads,
+            // so the next staging's wait for them (s_waitcnt vmcnt counts
+            // loads and stores in issue order) is vmcnt(DCR_VMPAD) or more,
+            // not a drain of this record's column stores
+            const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void *)a.rows, (short)0, 0, 0x00020000);
+#pragma unroll
+            for (int k = 0; k < DCR_VMPAD; ++k) __builtin_amdgcn_raw_buffer_store_b32(0u, rz, 4 * lane, 256 * k, 0);
+        }
         sp.mark(3);                    // [2] prefetch issue
         lds_fence();
         const uint2 rw = *(const uint2 *)(lds + rm_addr + 8 * lane);
@@ -3896,13 +3971,20 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastArgs a) {
     const int64_t rec = m.rec;
     const uint32_t T = row.y & 255u;
     if (row.w == 1u) {
-        const uint64_t num = 25ull * row.z, den = 18018ull * T;
-        const uint64_t q = num / den, r = num - q * den;
+        // 25 S / (18018 T): num < 2^37, den < 2^23.  The quotient from a
+        // double estimate (within 1 of the truth) fixed up by the integer
+        // remainder: a 64-bit integer division is a ~150-instruction
+        // software loop, the slot's largest cost in this kernel
+        const int64_t num = 25ll * row.z, den = 18018ll * T;
+        int64_t q = (int64_t)((double)num * (1.0 / (double)den));
+        int64_t r = num - q * den;
+        if (r < 0) { --q; r += den; }
+        if (r >= den) { ++q; r -= den; }
         if (2 * r == den) {
             a.xlist[atomicAdd(a.xcount, 1)] = i;
             return;
         }
-        a.O.E[rec] = div1000((int)(q + (2 * r > den ? 1u : 0u)));
+        a.O.E[rec] = div1000((int)(q + (2 * r > den ? 1 : 0)));
     }
     a.O.pos[rec] = (int32_t)row.x;
     a.O.mapq[rec] = (int32_t)(row.y >> 24);

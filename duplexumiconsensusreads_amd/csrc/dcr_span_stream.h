@@ -53,6 +53,17 @@ constexpr int kSlots = 4;
 
 inline int32_t span_members(size_t k) { return k == 0 ? 128 : k == 1 ? 1024 : 4096; }
 
+// Every slot's buffers are sized once, for the largest span, by start() on
+// the opening thread before the producer exists: a span holds at most
+// kSpanMembers members, at most kSpanIn compressed bytes (a span ends early
+// past it) and so at most kSpanMembers * 64 KiB of output (isize <= 65536).
+// The producer's ensure() calls then never allocate or free (on the device:
+// no hipFree / hipHostMalloc on the producer thread while kernels run,
+// DESIGN.md §5, the round-3 exit suspect).
+constexpr int32_t kSpanMembers = 4096;
+constexpr size_t kSpanIn = (size_t)128 << 20;
+constexpr size_t kSpanOut = (size_t)kSpanMembers * 65536;
+
 template <class B>
 struct Stream {
     using Event = typename B::Event;
@@ -81,7 +92,15 @@ struct Stream {
     Stream(B &b, const uint8_t *f) : be(b), file(f) {}
     ~Stream() { close(); }
 
-    void start() { producer = std::thread([this] { produce(); }); }
+    void start() {
+        for (int slot = 0; slot < kSlots; ++slot)
+            if (!be.ensure(slot, kSpanIn, kSpanOut, kSpanMembers)) {
+                be.error("dcr_inflate_stream: slot buffers could not be allocated");
+                err = -1;               // every fetch fails; no producer runs
+                return;
+            }
+        producer = std::thread([this] { produce(); });
+    }
 
     int add(const dcr_bgzf_member *mm, int32_t n, int32_t last) {
         {
@@ -113,9 +132,12 @@ struct Stream {
                 sp.m0 = mnext;
                 sp.m1 = std::min((int32_t)m.size(), mnext + want);
                 // a span ends at a gap in the compressed input (members the
-                // reader inflates on the host): its staging copy is contiguous
+                // reader inflates on the host): its staging copy is
+                // contiguous; and before kSpanIn compressed bytes (the slots'
+                // sized capacity)
                 for (int32_t i = sp.m0 + 1; i < sp.m1; ++i)
-                    if (m[i].in_off > m[i - 1].in_off + (int64_t)m[i - 1].in_len + 64) {
+                    if (m[i].in_off > m[i - 1].in_off + (int64_t)m[i - 1].in_len + 64 ||
+                        m[i].in_off + (int64_t)m[i].in_len - m[sp.m0].in_off > (int64_t)kSpanIn - 16) {
                         sp.m1 = i;
                         break;
                     }
@@ -197,6 +219,7 @@ struct Stream {
                 cv.wait(lk, [&] { return spans.size() > k || produced || err; });
                 if (spans.size() <= k) {
                     if (!err) be.error("dcr_inflate_stream_fetch: range past the stream's members");
+                    else be.error("dcr_inflate_stream_fetch: the stream failed");
                     return leave(-1);
                 }
                 spp = &spans[k];

@@ -18,6 +18,7 @@
 
 extern "C" void dcr_test_stream_hook(dcr_inflate_hook *hook);
 extern "C" void dcr_test_stream_stats(int64_t *out4);
+extern "C" int64_t dcr_test_stream_late_allocs(void) __attribute__((weak));   // stream_host.cpp only
 
 namespace {
 uint64_t fnv(uint64_t h, const void *p, size_t n) {
@@ -133,6 +134,7 @@ int main(int argc, char **argv) {
                 batches, hb.end_kind, (long long)c[4], (long long)c[0], (long long)c[1], (long long)c[2],
                 (long long)c[3], (unsigned long long)h, gpu, (long long)s[0], (long long)s[1], (long long)s[2],
                 (long long)s[3]);
+    if (dcr_test_stream_late_allocs) std::printf("late_allocs %lld\n", (long long)dcr_test_stream_late_allocs());
     std::fflush(stdout);
     }
     return 0;

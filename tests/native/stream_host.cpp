@@ -8,6 +8,7 @@
 // (libdcr_io) through the stream path on inputs of any BGZF block size.
 #include <zlib.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -44,12 +45,18 @@ int inflate_member(const uint8_t *in, uint32_t in_len, uint8_t *out, uint32_t is
     return (uint32_t)crc32(0L, out, isize) == crc ? 0 : 2;
 }
 
-// slot buffers that move when they grow (like hipFree + hipMalloc)
+// slot buffers that move when they grow (like hipFree + hipMalloc); a
+// growth on any thread but the stream's opener is counted: the protocol sizes
+// every slot in start() on the opening thread, so the producer never
+// allocates while spans are in flight (dcr_span_stream.h, kSpanIn / kSpanOut)
+std::atomic<int64_t> g_late_allocs{0};
 struct Buf {
     uint8_t *p = nullptr;
     size_t cap = 0;
+    std::thread::id opener = std::this_thread::get_id();
     bool grow(size_t n) {
         if (n <= cap) return true;
+        if (std::this_thread::get_id() != opener) ++g_late_allocs;
         std::free(p);
         p = (uint8_t *)std::malloc(n);
         cap = p ? n : 0;
@@ -205,6 +212,8 @@ void dcr_test_stream_hook(dcr_inflate_hook *hook) {
     hook->stream_fetch = h_fetch;
     hook->stream_close = h_close;
 }
+// slot-buffer growths away from the opening thread (0: the producer never allocated)
+int64_t dcr_test_stream_late_allocs(void) { return g_late_allocs.load(); }
 // streams opened, spans launched, members checked, bytes fetched (totals)
 void dcr_test_stream_stats(int64_t *out4) {
     std::lock_guard<std::mutex> g(g_mu);

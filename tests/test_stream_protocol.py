@@ -16,7 +16,11 @@ end and hashes every packed batch.  Checked here:
   and pack threads (the pool sizes of the one unexplained bench exit in round
   3): no race report (e.g. the stream's start offset read by the member
   scanner while the reader advanced it, dcr_ingest.cpp open_stream) and no
-  heap error (slot buffers are freed and re-allocated when they grow).
+  heap error;
+* the slot buffers are sized once by the protocol's start() on the opening
+  thread: no buffer grows (a hipFree / hipHostMalloc on the device) on the
+  producer thread while spans are in flight (``late_allocs`` 0, the round-3
+  exit suspect of DESIGN.md §5).
 """
 import os
 import subprocess
@@ -74,6 +78,9 @@ def test_small_blocks_through_the_stream_equal_the_host_pool(drivers, bams):
         got, _ = _run(exe, bam, 1)
         assert got["hooked"] == "1" and got["streams"] == "1", got
         _same(ref, got)
+        # the slots were sized at the stream's start: the producer never
+        # grew (freed / re-allocated) a buffer while spans were in flight
+        assert got["late_allocs"] == "0", got
     assert int(got["spans"]) >= 8                   # the small-block run went through many spans
 
 
@@ -102,6 +109,7 @@ def test_stream_ingest_under_sanitizers_16_16_pools(drivers, bams, kind):
         got, err = _run(exe, bam, 1, env, timeout=600)
         assert "WARNING: ThreadSanitizer" not in err and "ERROR: AddressSanitizer" not in err, err[-4000:]
         _same(ref, got)
+        assert got["late_allocs"] == "0", got
 
 
 # ---- round 3's protocol, for the one unexplained bench exit ------------------
