@@ -21,6 +21,14 @@ nfam = int(sys.argv[1])
 cfg = os.environ.get("ABL_CONFIG", "C2")
 packed = (synth.packed_fixed_size(nfam, seed=3) if cfg == "C2"
           else synth.packed_config(synth.CONFIGS[cfg], nfam, seed=3, max_reads=1000))
+if os.environ.get("ABL_SS_ALIGN"):
+    # diagnostic: single-strand output regions rounded up to ABL_SS_ALIGN
+    # columns instead of 16 (the kernels still write T16 columns of each)
+    import numpy as np
+    al = int(os.environ["ABL_SS_ALIGN"])
+    t = np.diff(packed.ss_col_off)
+    t = (t + al - 1) // al * al
+    packed.ss_col_off[1:] = np.cumsum(t)
 db = DeviceBatch(packed)
 P = build_dcr_params(ConsensusParams())
 handles = []
