@@ -108,6 +108,12 @@ struct dcr_ctx {
     // single-strand records of at most this many reads skip the common fast
     // pass (the exact pass takes them whole); DCR_EXACT_DIRECT_R overrides
     int direct_r = 3;
+    // the largest single-strand subfamily of the batch being submitted, when
+    // the host knows it (dcr_submit / dcr_submit_write: host sub_off), else -1:
+    // the kernels only records that large can need (k_prep_big > 64 reads,
+    // k_decide_deep >= kDeepReads) are not launched for batches without them
+    int max_r_hint = -1;
+    int rm_waves = dcr::kRecmetaWaves;   // k_recmeta block size for light records (DCR_RM_WAVES: A/B runs)
     uint16_t *d_llr16 = nullptr;   // device [128]
     uint16_t *d_llr8 = nullptr;    // device [128]
     uint32_t *d_r2tab = nullptr;   // device [dcr::kR2Entries]: two-read column outcomes (EXACT pass)
@@ -269,6 +275,10 @@ dcr_ctx *dcr_create(int device, const dcr_params *params) {
     dcr_ctx *c = new dcr_ctx();
     c->device = device;
     if (const char *e = std::getenv("DCR_EXACT_DIRECT_R")) c->direct_r = std::atoi(e);   // A/B runs
+    if (const char *e = std::getenv("DCR_RM_WAVES")) {                                  // A/B runs
+        const int w = std::atoi(e);
+        if (w == 4 || w == 8 || w == 16) c->rm_waves = w;
+    }
     if (hipSetDevice(device) != hipSuccess ||
         hi_prio_stream(&c->stream) != hipSuccess ||
         hipMalloc(&c->d_params, sizeof(dcr_params)) != hipSuccess ||
@@ -508,7 +518,7 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
             while (rpw > 1 && (int64_t)rpw * avg > 1024) rpw >>= 1;
         }
         a.rpw = rpw;
-        const int rm_waves = rpw == 64 ? dcr::kRecmetaWaves : 4;   // heavy records: small blocks
+        const int rm_waves = rpw == 64 ? c->rm_waves : 4;           // heavy records: small blocks
         const int64_t rpb = (int64_t)rm_waves * rpw;                // records per k_recmeta block
         const unsigned nb = (unsigned)((a.n_rec + rpb - 1) / rpb);
         const size_t rm_lds = dcr::recmeta_lds_bytes(rm_waves);
@@ -530,7 +540,8 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
                                c->stream, a);
         } else {
             hipLaunchKernelGGL(dcr::k_recmeta<false>, dim3(nb), dim3(rm_waves * dcr::kWave), rm_lds, c->stream, a);
-            hipLaunchKernelGGL(dcr::k_prep_big, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
+            if (c->max_r_hint < 0 || c->max_r_hint > dcr::kWave)
+                hipLaunchKernelGGL(dcr::k_prep_big, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
             HIP_TRY(hipEventRecord(ev[0], c->stream));
             hipLaunchKernelGGL((dcr::k_consensus_fast<false, false>), dim3(fast_grid(a.n_rec, 0)),
                                dim3(dcr::kFastBlock), 0, c->stream, fa);
@@ -539,7 +550,12 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
             hipLaunchKernelGGL((dcr::k_consensus_fast<false, true>), dim3(gx), dim3(dcr::kFastBlock), 0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[2], c->stream));
             hipLaunchKernelGGL(dcr::k_decide<false>, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
-            hipLaunchKernelGGL(dcr::k_decide_deep, dim3(2 * c->n_cu), dim3(dcr::kDeepWaves * dcr::kWave), 0, c->stream, a);
+            // (its 66 KB blocks wait for room beside the inflate waves in the
+            // whole-node pipeline even when they find no deep record: up to
+            // 7 ms per C2 pass, profiles/r06g)
+            if (c->max_r_hint < 0 || c->max_r_hint >= dcr::kDeepReads)
+                hipLaunchKernelGGL(dcr::k_decide_deep, dim3(2 * c->n_cu), dim3(dcr::kDeepWaves * dcr::kWave), 0, c->stream,
+                                   a);
             hipLaunchKernelGGL(dcr::k_consensus_general<false>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
                                c->stream, a);
         }
@@ -760,6 +776,15 @@ void dcr_host_free(void *p) {
     if (p) (void)hipHostFree(p);
 }
 
+// the largest subfamily of a host batch (sub_off is a host array here)
+static int host_max_r(const dcr_batch *h) {
+    int m = 0;
+    const int64_t n = 4 * (int64_t)h->n_fam;
+    if (n > 0 && !h->sub_off) return -1;
+    for (int64_t i = 0; i < n; ++i) m = std::max(m, h->sub_off[i + 1] - h->sub_off[i]);
+    return m;
+}
+
 int dcr_submit(dcr_ctx *c, int slot, const dcr_batch *h, dcr_out *hss, dcr_out *hds, int32_t *read_status) {
     if (!c || !h || !hss || !hds) return fail(DCR_EARG, "NULL argument");
     if (slot < 0 || slot >= DCR_MAX_SLOTS) return fail(DCR_EARG, "slot out of range");
@@ -790,7 +815,9 @@ int dcr_submit(dcr_ctx *c, int slot, const dcr_batch *h, dcr_out *hss, dcr_out *
     HIP_TRY(hipEventRecord(S.ev_h2d, c->s_h2d));
     // kernels on the compute stream
     HIP_TRY(hipStreamWaitEvent(c->stream, S.ev_h2d, 0));
+    c->max_r_hint = host_max_r(h);
     int rc = dcr_run_batch(c, &db, &dout[0], &dout[1]);
+    c->max_r_hint = -1;
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(S.h_err, c->w.err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     if (read_status && h->n_reads > 0)
@@ -899,7 +926,9 @@ int dcr_submit_write(dcr_ctx *c, int slot, const dcr_batch *h, const dcr_wmeta *
     HIP_TRY(hipEventRecord(S.ev_h2d, c->s_h2d));
     // consensus kernels on the compute stream
     HIP_TRY(hipStreamWaitEvent(c->stream, S.ev_h2d, 0));
+    c->max_r_hint = host_max_r(h);
     int rc = dcr_run_batch(c, &db, &dout[0], &dout[1]);
+    c->max_r_hint = -1;
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(S.h_err, c->w.err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     // record writer

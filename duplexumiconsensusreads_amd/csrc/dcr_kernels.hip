@@ -35,6 +35,9 @@
 #ifndef DCR_STAMP
 #define DCR_STAMP 0   // diagnostic builds only (tools/stamps.py): per-phase s_memtime cycle totals
 #endif
+#ifndef DCR_GSTAMP
+#define DCR_GSTAMP 0  // diagnostic builds only (tools/gstamps.py): per-phase s_memtime cycles of the general kernel
+#endif
 #ifndef DCR_FAST_OCC
 #define DCR_FAST_OCC 7   // fast kernel (common instantiation): waves per SIMD the launch bounds ask for
 #endif
@@ -1195,6 +1198,29 @@ struct LaneReads {
     int sn;      // stage offset of its first kept base | runs << 16
 };
 
+// diagnostic phase clock of the general kernel (DCR_GSTAMP builds): cycles per
+// phase and per record class, summed per wave, flushed at the kernel's end
+struct GStamp {
+    uint64_t t = 0, t0 = 0;
+    uint64_t acc[20] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    __device__ __forceinline__ void start() {
+        if (DCR_GSTAMP) t = t0 = __builtin_amdgcn_s_memtime();
+    }
+    __device__ __forceinline__ void mark(int k) {
+        if (DCR_GSTAMP) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            acc[k] += now - t;
+            t = now;
+        }
+    }
+    __device__ __forceinline__ void record(int cls) {     // record class: total cycles, count
+        if (DCR_GSTAMP) {
+            acc[8 + cls] += __builtin_amdgcn_s_memtime() - t0;
+            acc[12 + cls] += 1;
+        }
+    }
+};
+
 // ------------------------------------------------------------ k_consensus
 // One consensus record (single-strand subfamily or duplex pair) on one wave.
 // FAST: only the staged layout (no insertion column, <= 64 reads, bytes fit the
@@ -1203,8 +1229,9 @@ struct LaneReads {
 template <bool DUPLEX, bool FAST>
 __device__ __forceinline__ void process_record(const Args &a, const int64_t rec, WaveLds &W, const double2 *s_lut,
                                                const double *s_qthr, const uint32_t *s_wtab, const bool dec,
-                                               const int lane) {
+                                               const int lane, GStamp &gs) {
     const dcr_params *P = a.P;
+    gs.start();
 
     const dcr_out &O = DUPLEX ? a.ds : a.ss;
     const int64_t *col_off = DUPLEX ? a.in.ds_col_off : a.in.ss_col_off;
@@ -1299,6 +1326,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
         write_status(255);
         return;
     }
+    gs.mark(0);
 
     const bool cols_lds = T <= kColsLds;
     // ordering of the record's scratch between lanes: LDS only (wave-local DS
@@ -1513,6 +1541,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
         }
     };
 
+    gs.mark(1);
     // ---- phases 1+2: column tiles (lane = column)
     const int tw = ins ? kTileIns : kWave;       // insertion layout: 32-column tiles
     for (int c0 = 0; c0 < T; c0 += tw) {
@@ -1546,6 +1575,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
                 return e;
             };
             accumulate(A, R, src, s_lut);
+            gs.mark(4);
         } else if (FAST) {
             // unreachable: the fast kernel only keeps staged records
         } else if (!ins) {
@@ -1560,6 +1590,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
                 return e;
             };
             accumulate(A, R, src, s_lut);
+            gs.mark(4);
         } else if (!big) {
             uint64_t insmask = 0;
             // bytes that do not fit the stage: each read's next 32 bytes (the
@@ -1570,6 +1601,12 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
                 sfence();
                 stage_window(lane < R, myrd.seq_start, is0);
                 sfence();
+            }
+            gs.mark(2);
+            if (DCR_GSTAMP) {
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                gs.mark(17);          // [17] memory operations drained before the steps (diagnostic)
+                gs.acc[16] += ncol;   // [16] column steps
             }
             for (int tt = 0; tt < ncol; ++tt) {
                 const bool isI = lane < R && sim.curop == 1;
@@ -1589,11 +1626,13 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
                 }
             }
             sfence();
+            gs.mark(3);
             ins_col = live && ((insmask >> lane) & 1);
             auto src = [&](int r) -> uint32_t { return live ? (uint32_t)W.tile[r][lane & (kTileIns - 1)] : kPad; };
             tdec = decide_tile(a, R, live, ins_col, src, s_wtab, tco);
             if (!tdec) accumulate(A, R, src, s_lut);
             sfence();
+            gs.mark(4);
         } else if (regbig) {
             // this tile's insertion-column flags, one load per lane
             const uint64_t fm = __ballot(lane < ncol && insflag[c0 + lane] != 0);
@@ -1607,6 +1646,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
                 sfence();
                 stage_window(mine, brd[c].seq_start, is0);
                 sfence();
+                gs.mark(2);
                 if (mine) {
                     const ReadRef rd = slim_ref(brd[c]);
                     for (int tt = 0; tt < ncol; ++tt)
@@ -1615,8 +1655,10 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
                             [&](int is) { return (uint32_t)W.stage[((is - is0) << 6) + lane]; });
                 }
                 sfence();
+                gs.mark(3);
                 auto src = [&](int rr) -> uint32_t { return live ? (uint32_t)W.tile[rr][lane & (kTileIns - 1)] : kPad; };
                 accumulate(A, nr, src, s_lut);
+                gs.mark(4);
             }
             sfence();
         } else {
@@ -1681,6 +1723,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
             if (first < 0) first = c0 + __builtin_ctzll(nn);
             last = c0 + 63 - __builtin_clzll(nn);
         }
+        gs.mark(5);
     }
     if (DCR_ABL == 2 || DCR_ABL == 3) {
         if (lane == 0) O.pos[rec] = cons[0] + n_de + first + last;
@@ -1793,6 +1836,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
         if (i < nruns) ocig[i] = ((nx - (v >> 4)) << 4) | (v & 15);
     }
 
+    gs.mark(6);
     // ---- E = round(mean(e/d), 3) with numpy's pairwise summation (:1015-1018)
     // pairwise_sum(a, n): n < 8 sequential; n <= 128 eight accumulators; else
     // split at n2 = n/2 rounded down to a multiple of 8 and add the halves.
@@ -1880,6 +1924,8 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
         O.M[rec] = Dmin;
         O.E[rec] = E;
     }
+    gs.mark(7);
+    gs.record(!ins ? 0 : !big ? 1 : regbig ? 2 : 3);
 }
 
 
@@ -4031,10 +4077,11 @@ __global__ __launch_bounds__(kBlock, DCR_GEN_OCC) void k_consensus_general(Args 
     // 3.85 -> 3.97 / 4.13 ms at 100 k families, the tail imbalance outweighing
     // the serialised claims)
     const int nw = gridDim.x * kWavesPerBlock;
+    GStamp gs;
     for (int i = blockIdx.x * kWavesPerBlock + wave;;) {
         if (i >= n) break;
         const int v = a.ws.ovf[i];                  // bit 31: k_decide decided every column
-        process_record<DUPLEX, false>(a, v & 0x7fffffff, s_wave[wave], s_lut, s_qthr, s_wtab, v < 0, lane);
+        process_record<DUPLEX, false>(a, v & 0x7fffffff, s_wave[wave], s_lut, s_qthr, s_wtab, v < 0, lane, gs);
         if (nw >= n) break;
         // one claim per wave, by its first active lane (any lane may carry it)
         const uint64_t act = __ballot(1);
@@ -4043,6 +4090,8 @@ __global__ __launch_bounds__(kBlock, DCR_GEN_OCC) void k_consensus_general(Args 
         if (lane == leader) t = atomicAdd(next, 1);
         i = nw + __builtin_amdgcn_readfirstlane(__shfl(t, leader, kWave));
     }
+    if (DCR_GSTAMP && lane == 0)
+        for (int k = 0; k < 20; ++k) atomicAdd(&a.ws.stamps[k + (DUPLEX ? 32 : 0)], (unsigned long long)gs.acc[k]);
 }
 
 // decision pass over the general list (decide_record), one wave per record:
