@@ -391,6 +391,12 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     const size_t o_meta = o; o = align_up(o + sizeof(dcr::RecMeta) * n_rec);
     const size_t o_rm = o;   o = align_up(o + sizeof(uint2) * std::max<size_t>((size_t)s->n_reads, n_rec));
     const size_t o_rows = o; o = align_up(o + sizeof(uint4) * n_rec);
+    // insertion layouts: a row of kLayRow codes per single-strand read and per
+    // duplex input (two per duplex record)
+    const size_t o_lb = o;   o = align_up(o + sizeof(int) * (size_t)std::max<int64_t>(6LL * s->n_fam, 1));
+    const size_t o_lm = o;   o = align_up(o + 4 * sizeof(uint64_t) * (size_t)std::max<int64_t>(6LL * s->n_fam, 1));
+    const size_t o_lay = o;
+    o = align_up(o + sizeof(uint16_t) * (size_t)dcr::kLayRow * (size_t)std::max<int64_t>(s->n_reads + 4LL * s->n_fam, 1));
     if (o > c->ws.cap) {
         HIP_TRY(hipStreamSynchronize(c->stream));
         HIP_TRY(c->ws.ensure(o + o / 8));
@@ -408,6 +414,9 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     c->w.xcount = (int *)(b + o_err) + 5;
     c->w.gen_next = (int *)(b + o_err) + 7;      // [2], in the same block: reset with it per batch
     c->w.deep_count = (int *)(b + o_err) + 9;    // [1], likewise
+    c->w.lay_base = (int *)(b + o_lb);
+    c->w.lay_mask = (uint64_t *)(b + o_lm);
+    c->w.lay = (uint16_t *)(b + o_lay);
     c->w.deep = (int *)(b + o_deep);
     c->w.xlist = (int *)(b + o_xl);
     c->w.stamps = (unsigned long long *)(b + o_stamp);
@@ -536,6 +545,8 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
             hipLaunchKernelGGL((dcr::k_consensus_fast<true, true>), dim3(gx), dim3(dcr::kFastBlock), 0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[2], c->stream));
             hipLaunchKernelGGL(dcr::k_decide<true>, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
+            if (DCR_LAYOUT_KERNEL)
+                hipLaunchKernelGGL(dcr::k_ins_layout<true>, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
             hipLaunchKernelGGL(dcr::k_consensus_general<true>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
                                c->stream, a);
         } else {
@@ -550,6 +561,8 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
             hipLaunchKernelGGL((dcr::k_consensus_fast<false, true>), dim3(gx), dim3(dcr::kFastBlock), 0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[2], c->stream));
             hipLaunchKernelGGL(dcr::k_decide<false>, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
+            if (DCR_LAYOUT_KERNEL)
+                hipLaunchKernelGGL(dcr::k_ins_layout<false>, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
             // (its 66 KB blocks wait for room beside the inflate waves in the
             // whole-node pipeline even when they find no deep record: up to
             // 7 ms per C2 pass, profiles/r06g)

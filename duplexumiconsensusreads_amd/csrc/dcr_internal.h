@@ -37,6 +37,10 @@ struct RecMeta {
 };
 static_assert(sizeof(RecMeta) == 32, "RecMeta is one s_load_dwordx8");
 
+#ifndef DCR_LAYOUT_KERNEL
+#define DCR_LAYOUT_KERNEL 1   // insertion layouts by events in k_ins_layout (0: the general kernel steps columns)
+#endif
+
 struct Workspace {
     dcr_read_info *info;    // [n_reads]
     uint32_t *norm_cig;     // [n_cigar] normalised runs (M/I/D)
@@ -60,7 +64,19 @@ struct Workspace {
                             // or 0, kind), expanded into dcr_out by k_fast_rows; kind 0 = not decided
     uint2 *rmeta;           // [max(n_reads, 4F)] per read: len | mapq << 8 | (pos - pos of the record's
                             // first read) << 16 (int16), seq_start (low 32 bits)
+    // insertion layouts by events (k_ins_layout), per general-list record of
+    // either strand (single-strand 4F, then duplex 2F): 1 when laid out, -1
+    // when the general kernel lays it out itself; its insertion-column mask;
+    // its element codes, kLayRow per read at a fixed place (single-strand:
+    // from sub_off[rec] * kLayRow; duplex record p: from (n_reads + 2p) *
+    // kLayRow; a same-counter atomic per record cost milliseconds), tile-major
+    // ([32-column tile][read][32]): a tile of every read is one contiguous
+    // block, copied into the general kernel's LDS tile with 16-byte loads
+    int *lay_base;          // [6F]
+    uint64_t *lay_mask;     // [6F][4]
+    uint16_t *lay;          // [(n_reads + 4F) * kLayRow]
 };
+constexpr int kLayRow = 256;        // columns per laid-out row (records of T <= 256)
 
 struct Args {
     dcr_batch in;
@@ -123,6 +139,7 @@ __global__ void k_r2_table(const dcr_params *P, uint32_t *tab);
 constexpr int kR2Entries = 5 * 128 * 5 * 128;
 template <bool DUPLEX> __global__ void k_consensus_general(Args a);
 template <bool DUPLEX> __global__ void k_decide(Args a);
+template <bool DUPLEX> __global__ void k_ins_layout(Args a);
 __global__ void k_decide_deep(Args a);
 
 }  // namespace dcr

@@ -418,6 +418,51 @@ __device__ __forceinline__ bool walk_runs(const uint32_t *cig, int ncig, int j, 
     return true;
 }
 
+// ------------------------------------------ insertion layout by events
+// (k_ins_layout; tests/fil_model.py is its host model, checked against the
+// oracle's column-by-column reconstruct_alignment, :430-547).  A column is an
+// insertion column when a read's current op is I (:476-478): only reads that
+// hold an I run make one, and between insertion blocks every started read
+// advances one op per column (:506-535).  So the blocks follow from each I
+// read's run start counted in normal columns (phase A, event by event: reads
+// whose runs start at the same column make one block, as long as its longest
+// run), and a read's element at column t from N(t), the normal columns before
+// t: op index N(t) - N(s_r) (+ its I run once past), then the op and the read's
+// bases before it (phase B, lane = column).
+
+// the op at expanded index j of a read's runs (<= 4; I and M consume bases,
+// D not) and the read's bases before it (all its bases past the last op)
+struct RunPos {
+    int op, is;
+};
+__device__ __forceinline__ RunPos run_at(const uint32_t (&v)[4], int ncig, int j) {
+    int acc = 0, accb = 0, op = -1, is = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int ln = k < ncig ? (int)(v[k] >> 4) : 0;
+        const int o = (int)(v[k] & 15u);
+        const bool here = op < 0 && j < acc + ln;
+        const bool cb = o != 2;
+        is = here ? accb + (cb ? j - acc : 0) : is;
+        op = here ? o : op;
+        acc += ln;
+        accb += cb ? ln : 0;
+    }
+    return RunPos{op, op < 0 ? accb : is};
+}
+
+// insertion columns below column s of a record's mask (T <= 256)
+__device__ __forceinline__ int ins_below(const uint64_t (&im)[4], int s) {
+    int n = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int nb = min(max(s - 64 * w, 0), 64);
+        const uint64_t m = nb == 64 ? im[w] : (im[w] & ((1ull << nb) - 1ull));
+        n += __popcll(m);
+    }
+    return n;
+}
+
 // --------------------------------------------------------------- phase 2
 // Likelihood slots (see header): U = the chain shared by all unseen classes,
 // s[j] = chain of the j-th distinct class seen in the column, k[j] its class,
@@ -1404,7 +1449,19 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
     // within 64-read chunk c): the flags pass walks the runs without touching
     // HBM, and the tiles stage each chunk's next 32 bytes per read
     constexpr int kBigCh = 4;
-    const bool regbig = !FAST && ins && big && !DUPLEX && R <= kBigCh * kWave;
+    // insertion records that k_ins_layout laid out: the tiles load their rows
+    // (no column steps, flag pass or windows here)
+    const int64_t lrec = (DUPLEX ? 4 * (int64_t)a.in.n_fam : 0) + rec;
+    const bool laid = DCR_LAYOUT_KERNEL && !FAST && ins && cols_lds && R <= kBigCh * kWave && a.ws.lay_base[lrec] > 0;
+    uint64_t imask[4] = {0ull, 0ull, 0ull, 0ull};
+    const uint16_t *lrows = nullptr;
+    if (laid) {
+        const uint64_t *mk = a.ws.lay_mask + 4 * lrec;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) imask[w] = mk[w];
+        lrows = a.ws.lay + (DUPLEX ? (int64_t)a.in.n_reads + 2 * rec : (int64_t)a.in.sub_off[rec]) * kLayRow;
+    }
+    const bool regbig = !FAST && ins && big && !DUPLEX && R <= kBigCh * kWave && !laid;
     struct SlimRead {
         int pos, len, ncig;
         const uint32_t *cig;
@@ -1452,7 +1509,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
         }
         wave_fence();
     }
-    if (!FAST && ins && big && !DUPLEX && !regbig) {
+    if (!FAST && ins && big && !DUPLEX && !regbig && !laid) {
         for (int c = 0; c < R; c += kWave) {
             const int r = c + lane;
             if (r < R) {
@@ -1503,7 +1560,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
 
     // small-R insertion layout keeps its state in registers (lane = read)
     Sim sim{0, 0, 0, 0, 0};
-    if (ins && !big && lane < R) sim_load_run(sim, myrd);
+    if (ins && !big && !laid && lane < R) sim_load_run(sim, myrd);
 
     // the next 32 bytes of a read from seq index is0 (the most a 32-column tile
     // consumes) as codes in the stage, [k][lane], from 9 range-checked dword
@@ -1591,6 +1648,39 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
             };
             accumulate(A, R, src, s_lut);
             gs.mark(4);
+        } else if (laid) {
+            // the rows k_ins_layout wrote: two reads per load (lanes 32-63 the
+            // second), every load of a chunk issued before its tile is used
+            const uint64_t mw = c0 < 64 ? imask[0] : c0 < 128 ? imask[1] : c0 < 192 ? imask[2] : imask[3];
+            ins_col = live && ((mw >> (t & 63)) & 1ull) != 0;
+            const int tt = lane & (kTileIns - 1);
+            const int hcol = c0 + tt, hi = lane >> 5;
+            for (int cb = 0; cb < R; cb += kWave) {
+                const int nr = min(kWave, R - cb);
+                // this tile of the chunk's reads: nr rows of 64 bytes, one block
+                const uint4 *src4 = (const uint4 *)(lrows + ((int64_t)(c0 >> 5) * R + cb) * kTileIns);
+                uint4 *dst4 = (uint4 *)&W.tile[0][0];
+                uint4 q[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (u * kWave + lane < 4 * nr) q[u] = src4[u * kWave + lane];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (u * kWave + lane < 4 * nr) dst4[u * kWave + lane] = q[u];
+                (void)hi;
+                (void)hcol;
+                sfence();
+                gs.mark(3);
+                auto src = [&](int rr) -> uint32_t { return live ? (uint32_t)W.tile[rr][lane & (kTileIns - 1)] : kPad; };
+                if (R <= kWave) {
+                    tdec = decide_tile(a, R, live, ins_col, src, s_wtab, tco);
+                    if (!tdec) accumulate(A, R, src, s_lut);
+                } else {
+                    accumulate(A, nr, src, s_lut);
+                }
+                sfence();
+                gs.mark(4);
+            }
         } else if (!big) {
             uint64_t insmask = 0;
             // bytes that do not fit the stage: each read's next 32 bytes (the
@@ -1925,7 +2015,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
         O.E[rec] = E;
     }
     gs.mark(7);
-    gs.record(!ins ? 0 : !big ? 1 : regbig ? 2 : 3);
+    gs.record(!ins ? 0 : laid ? (big ? 2 : 1) : !big ? 1 : regbig ? 2 : 3);
 }
 
 
@@ -4094,6 +4184,239 @@ __global__ __launch_bounds__(kBlock, DCR_GEN_OCC) void k_consensus_general(Args 
         for (int k = 0; k < 20; ++k) atomicAdd(&a.ws.stamps[k + (DUPLEX ? 32 : 0)], (unsigned long long)gs.acc[k]);
 }
 
+// Insertion layouts by events (see run_at): one wave per general-list record
+// with an insertion column, 4-wave blocks, few registers.  Writes the record's
+// block (insertion mask, then every read's row of element codes over the T
+// columns) into ws.lay and its offset into ws.lay_base; -1 for a record it
+// does not take (no insertion, a failing read, T or R > 256, a read outside the
+// model's assumptions -- more than 4 runs or one I run, fewer M + I ops than
+// bases, bases ending inside or before its I run -- or no room left): the
+// general kernel then lays it out column by column, reproducing the
+// reference's IndexErrors.
+template <bool DUPLEX>
+__global__ __launch_bounds__(256) void k_ins_layout(Args a) {
+    __shared__ uint32_t s_scr[kWavesPerBlock][4 * kWave];   // phase A: an I read's r, need, L | bases << 16, start
+    __shared__ uint32_t s_iev[kWavesPerBlock][4 * kWave];   // per read: run start | L << 9 | bases << 16 (511: none)
+    __shared__ __attribute__((aligned(16))) uint32_t s_rt[kWavesPerBlock][16 * kWave];  // phase B: a chunk's read table
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int n = a.ws.ovf_count[DUPLEX ? 1 : 0];
+    const int nw = gridDim.x * kWavesPerBlock;
+    const int64_t lb_off = DUPLEX ? 4 * (int64_t)a.in.n_fam : 0;
+    const int minbq = a.P->min_base_quality;
+    uint32_t *scr = s_scr[wave];
+    uint32_t *iev = s_iev[wave];
+    uint32_t *rt = s_rt[wave];
+    for (int i = blockIdx.x * kWavesPerBlock + wave; i < n; i += nw) {
+        const int vv = a.ws.ovf[i];
+        if (vv < 0) continue;                         // decided by k_decide: no insertion column
+        const int64_t rec = vv;
+        const int R = DUPLEX ? 2 : (a.in.sub_off[rec + 1] - a.in.sub_off[rec]);
+        int lay = -1;
+        if (R > 0 && R <= 4 * kWave) {
+            int minpos = 0x7fffffff, maxend = -0x7fffffff;
+            bool up = false, ins = false;
+            for (int c = 0; c < R; c += kWave) {
+                const int r = c + lane;
+                if (r < R) {
+                    const ReadRef rd = get_read<DUPLEX>(a, rec, r);
+                    up |= rd.status != 0 || rd.len <= 0;
+                    minpos = min(minpos, rd.pos);
+                    maxend = max(maxend, rd.pos + rd.len);
+                    if (!DUPLEX) {
+                        ins |= a.ws.info[a.in.sub_off[rec] + r].has_ins != 0;
+                    } else {
+                        for (int k = 0; k < rd.ncig; ++k) ins |= (rd.cig[k] & 15u) == 1u;
+                    }
+                }
+            }
+            up = __ballot(up) != 0;
+            ins = __ballot(ins) != 0;
+            minpos = wave_min(minpos);
+            const int T = wave_max(maxend) - minpos;
+            const int64_t *col_off = DUPLEX ? a.in.ds_col_off : a.in.ss_col_off;
+            const bool take = !up && ins && T > 0 && T <= kColsLds && T <= col_off[rec + 1] - col_off[rec];
+            // phase A: eligibility, the I reads compacted into lanes
+            int nI = 0;
+            bool bad = !take;
+            for (int c = 0; c < R && !bad; c += kWave) {
+                const int r = c + lane;
+                bool isI = false, b_r = false;
+                uint32_t need = 0, L = 0, bb = 0, sr = 0;
+                if (r < R) {
+                    const ReadRef rd = get_read<DUPLEX>(a, rec, r);
+                    int nIr = 0, acc = 0, accb = 0, mi = 0;
+                    for (int k = 0; k < min(rd.ncig, 4); ++k) {
+                        const uint32_t v = rd.cig[k];
+                        const int o = (int)(v & 15u), ln = (int)(v >> 4);
+                        if (o == 1 && nIr == 0) {
+                            need = (uint32_t)acc;
+                            L = (uint32_t)ln;
+                            bb = (uint32_t)accb;
+                        }
+                        nIr += o == 1;
+                        mi += o != 2 ? ln : 0;
+                        acc += ln;
+                        accb += o != 2 ? ln : 0;
+                    }
+                    isI = nIr == 1;
+                    b_r = rd.ncig > 4 || nIr > 1 || mi < rd.len || (isI && (int)(bb + L) > rd.len) || L > 127 ||
+                          bb > 0xFFFF;
+                    sr = (uint32_t)(rd.pos - minpos);
+                    iev[r] = 511u;
+                }
+                const uint64_t im = __ballot(isI);
+                const int slot = nI + __popcll(im & lanemask_lt(lane));
+                if (isI && slot < kWave) {
+                    scr[4 * slot] = (uint32_t)r;
+                    scr[4 * slot + 1] = need;
+                    scr[4 * slot + 2] = L | bb << 16;
+                    scr[4 * slot + 3] = sr;
+                }
+                nI += __popcll(im);
+                bad = __ballot(b_r) != 0;
+            }
+            uint64_t imask[4] = {0ull, 0ull, 0ull, 0ull};
+            if (!bad && nI <= kWave) {
+                lds_fence();
+                bool pend = lane < nI;
+                int need = 0, L = 0, sr = 0, rj = 0, bj = 0;
+                if (pend) {
+                    rj = (int)scr[4 * lane];
+                    need = (int)scr[4 * lane + 1];
+                    L = (int)(scr[4 * lane + 2] & 0xFFFFu);
+                    bj = (int)(scr[4 * lane + 2] >> 16);
+                    sr = (int)scr[4 * lane + 3];
+                }
+                int t = 0;
+                for (int it = 0; it <= kWave; ++it) {     // each event activates at least one lane
+                    const int cand = pend ? (need == 0 ? t : max(t, sr) + need) : 0x7fffffff;
+                    const int tn = wave_min(cand);
+                    if (tn >= T) break;
+                    if (pend && need > 0) need -= max(0, tn - max(t, sr));
+                    const bool act = pend && need == 0 && cand == tn;
+                    const int B = wave_max(act ? L : 0);
+                    const int hi = min(T, tn + B);
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const int lo2 = max(tn, 64 * w), hi2 = min(hi, 64 * w + 64);
+                        if (lo2 < hi2) {
+                            const int nb = hi2 - lo2;
+                            imask[w] |= (nb == 64 ? ~0ull : ((1ull << nb) - 1ull)) << (lo2 - 64 * w);
+                        }
+                    }
+                    if (act) {
+                        iev[rj] = (uint32_t)tn | (uint32_t)L << 9 | (uint32_t)bj << 16;
+                        pend = false;
+                    }
+                    t = tn + B;
+                }
+                lds_fence();
+                // the record's mask and rows (fixed places: see Workspace::lay)
+                {
+                    lay = 1;
+                    if (lane < 4) {
+                        const uint64_t m = lane == 0 ? imask[0] : lane == 1 ? imask[1] : lane == 2 ? imask[2] : imask[3];
+                        a.ws.lay_mask[4 * (lb_off + rec) + lane] = m;
+                    }
+                    uint16_t *rows = a.ws.lay + (DUPLEX ? (int64_t)a.in.n_reads + 2 * rec : (int64_t)a.in.sub_off[rec]) * kLayRow;
+                    // phase B: lane = column, 64 at a time; per read the
+                    // column-free values computed lane-parallel (lane = read)
+                    int nbase = 0;
+                    for (int c0 = 0; c0 < T; c0 += kWave) {
+                        const int t2 = c0 + lane;
+                        const uint64_t mw = imask[c0 >> 6];
+                        const bool insc = ((mw >> lane) & 1ull) != 0;
+                        const int Nt = nbase + __popcll(~mw & (lane == 0 ? 0ull : (~0ull >> (64 - lane))));
+                        for (int cb = 0; cb < R; cb += kWave) {
+                            const int nr = min(kWave, R - cb);
+                            // lane = read of this chunk: everything per read that
+                            // does not depend on the column, into the wave's read
+                            // table (read back as uniform-address LDS loads: no
+                            // readlane into scalar registers, which spilled)
+                            if (lane < nr) {
+                                const ReadRef rd = get_read<DUPLEX>(a, rec, cb + lane);
+                                const int sr = rd.pos - minpos;
+                                int end = 0, bb = 0, ends[4], bbs[4];
+                                uint32_t dm = 0;
+#pragma unroll
+                                for (int k = 0; k < 4; ++k) {
+                                    const uint32_t v = k < rd.ncig ? rd.cig[k] : 0u;
+                                    const int ln = k < rd.ncig ? (int)(v >> 4) : 0;
+                                    const bool isd = (v & 15u) == 2u;
+                                    bbs[k] = bb;
+                                    end += ln;
+                                    ends[k] = end;
+                                    bb += isd ? 0 : ln;
+                                    dm |= (isd ? 1u : 0u) << k;
+                                }
+                                uint4 *row = (uint4 *)&rt[16 * lane];
+                                row[0] = make_uint4((uint32_t)sr, (uint32_t)rd.len, (uint32_t)(sr - ins_below(imask, sr)),
+                                                    iev[cb + lane]);
+                                row[1] = make_uint4((uint32_t)ends[0] | (uint32_t)ends[1] << 16,
+                                                    (uint32_t)ends[2] | (uint32_t)ends[3] << 16,
+                                                    (uint32_t)bbs[1] | (uint32_t)bbs[2] << 16,
+                                                    (uint32_t)bbs[3] | (uint32_t)bb << 16 | 0u);
+                                rt[16 * lane + 8] = dm;
+                                ((int64_t *)&rt[16 * lane])[5] = rd.seq_start;
+                            }
+                            lds_fence();
+                            const uint8_t *gb = DUPLEX ? a.ss.seq : a.in.bases;
+                            const uint8_t *gq = DUPLEX ? a.ss.qual : a.in.quals;
+                            constexpr int kU = 4;     // reads whose byte loads are in flight together
+                            for (int r0 = 0; r0 < nr; r0 += kU) {
+                                int64_t pu[kU];
+                                uint32_t ku[kU];      // 0 base, 1 '+', 2 pad, 3 '-'
+#pragma unroll
+                                for (int u = 0; u < kU; ++u) {
+                                    const int r = min(r0 + u, nr - 1);
+                                    const uint4 f0 = ((const uint4 *)&rt[16 * r])[0];
+                                    const uint4 f1 = ((const uint4 *)&rt[16 * r])[1];
+                                    const uint32_t dm = rt[16 * r + 8];
+                                    const int64_t ss0 = ((const int64_t *)&rt[16 * r])[5];
+                                    const int sr = (int)f0.x, len = (int)f0.y, Ns = (int)f0.z;
+                                    const uint32_t e0 = f0.w;
+                                    const int E = (int)(e0 & 511u), L2 = (int)((e0 >> 9) & 127u), bI = (int)(e0 >> 16);
+                                    const bool isI = E != 511;
+                                    const bool inI = isI && t2 >= E && t2 < E + L2;
+                                    const int j = Nt - Ns + ((isI && E < t2) ? L2 : 0);
+                                    const int en0 = (int)(f1.x & 0xFFFFu), en1 = (int)(f1.x >> 16);
+                                    const int en2 = (int)(f1.y & 0xFFFFu), en3 = (int)(f1.y >> 16);
+                                    const int k = (j >= en0) + (j >= en1) + (j >= en2) + (j >= en3);
+                                    const int st = k == 0 ? 0 : k == 1 ? en0 : k == 2 ? en1 : en2;
+                                    const int bbk = k == 0 ? 0 : k == 1 ? (int)(f1.z & 0xFFFFu)
+                                                  : k == 2 ? (int)(f1.z >> 16) : (int)(f1.w & 0xFFFFu);
+                                    const bool isd = k < 4 && ((dm >> k) & 1u);
+                                    const int is = k == 4 ? (int)(f1.w >> 16) : bbk + (isd ? 0 : j - st);
+                                    const int cis = insc ? bI + (t2 - E) : is;
+                                    ku[u] = insc ? (inI ? 0u : 1u) : (t2 < sr || is >= len) ? 2u : isd ? 3u : 0u;
+                                    pu[u] = ss0 + min(max(cis, 0), len - 1);
+                                }
+                                uint32_t bu[kU], qu[kU];
+#pragma unroll
+                                for (int u = 0; u < kU; ++u) {
+                                    bu[u] = gb[pu[u]];
+                                    qu[u] = gq[pu[u]];
+                                }
+#pragma unroll
+                                for (int u = 0; u < kU; ++u) {
+                                    const uint32_t e = ku[u] == 0u ? make_code<DUPLEX>(bu[u], qu[u], minbq)
+                                                     : ku[u] == 1u ? kPlus : ku[u] == 2u ? kPad : kDel;
+                                    if (r0 + u < nr && t2 < T)
+                                        rows[((int64_t)(t2 >> 5) * R + cb + r0 + u) * kTileIns + (t2 & 31)] = (uint16_t)e;
+                                }
+                            }
+                            lds_fence();      // the read table is rewritten by the next chunk
+                        }
+                        nbase += __popcll(~mw & (T - c0 >= 64 ? ~0ull : ((1ull << (T - c0)) - 1ull)));
+                    }
+                }
+            }
+        }
+        if (lane == 0) a.ws.lay_base[lb_off + rec] = lay;
+    }
+}
+
 // decision pass over the general list (decide_record), one wave per record:
 // marks the records whose every column it decides (ovf entry | bit 31) and
 // leaves their column words in the workspace column scratch (ws.cons)
@@ -4253,6 +4576,8 @@ template __global__ void k_consensus_fast<true, true>(FastArgs);
 template __global__ void k_consensus_general<false>(Args);
 template __global__ void k_decide<false>(Args);
 template __global__ void k_decide<true>(Args);
+template __global__ void k_ins_layout<false>(Args);
+template __global__ void k_ins_layout<true>(Args);
 template __global__ void k_consensus_general<true>(Args);
 
 }  // namespace dcr

@@ -314,3 +314,56 @@ def test_gpu_insertion_layout_batch_end_tail(ctx, tail):
     got = ctx.run_host(packed)
     want = dcr_oracle_c.run(packed, params)
     assert_same(packed, got, want)
+
+
+def _ins_family(rng, fam):
+    """a family whose four subfamilies hold insertion-heavy reads: shared and
+    staggered insertions, leading insertions, deletions, soft clips, 3' N
+    tails and late-starting reads (the general kernel's insertion layout by
+    events, tests/fil_model.py)"""
+    from tests.golden_io import input_record
+    from tests.test_fil_model import _read
+    L = rng.choice([24, 40, 80, 150])
+    R = rng.choice([1, 2, 3, 6, 12, 30, 70])
+    reads = []
+    for k, (flag, strand) in enumerate(((99, "A"), (163, "B"), (83, "B"), (147, "A"))):
+        for i in range(R):
+            cig, b, q = _read(rng, L)
+            if rng.random() < 0.3:
+                a0, li = rng.randint(0, 5), rng.randint(1, 4)
+                if a0 + li < L:
+                    cig = ([(0, a0)] if a0 else []) + [(1, li), (0, L - a0 - li)]
+            reads.append(input_record({"qname": f"f{fam}_{k}_{i}", "flag": flag, "tid": 0,
+                                       "pos": 5000 + rng.randint(0, 8), "mapq": 40,
+                                       "cigar": [list(x) for x in cig], "seq": b, "qual": q,
+                                       "MI": f"{fam}/{strand}", "RX": "AAAA-CCCC"}))
+    return reads
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_gpu_insertion_layouts_by_events(ctx, seed):
+    """Insertion-heavy families through the GPU and the C oracle: every field
+    of every single-strand and duplex record, and the same raising families"""
+    from tests.harness import pipeline
+    rng = random.Random(seed)
+    fams = [_ins_family(rng, f) for f in range(400)]
+    params = ConsensusParams(max_reads=10_000)
+    ctx.set_params(params)
+    out = []
+    for backend in (_lib.backend(ctx), dcr_oracle_c.run):
+        res = []
+        for reads in fams:
+            try:
+                res.append(pipeline.prepare_family(reads, params, random.Random(0)))
+            except (pipeline.FamilyExit, IndexError) as e:
+                res.append(pipeline.FamilyResult(code="?", reads=reads, crash=type(e).__name__))
+        pipeline.run_batch(res, params, backend)
+        out.append(res)
+    n = 0
+    for a, b in zip(*out):
+        assert a.crash == b.crash and (a.subs is None) == (b.subs is None)
+        if a.crash is None and a.subs is not None:
+            assert [x.to_dict() for x in a.ss] == [x.to_dict() for x in b.ss]
+            assert [x.to_dict() for x in a.ds] == [x.to_dict() for x in b.ds]
+            n += 1
+    assert n > 100
