@@ -561,14 +561,16 @@ int dcr_run_batch(dcr_ctx *c, const dcr_batch *in, dcr_out *ss, dcr_out *ds) {
             hipLaunchKernelGGL((dcr::k_consensus_fast<false, true>), dim3(gx), dim3(dcr::kFastBlock), 0, c->stream, fa);
             HIP_TRY(hipEventRecord(ev[2], c->stream));
             hipLaunchKernelGGL(dcr::k_decide<false>, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
-            if (DCR_LAYOUT_KERNEL)
-                hipLaunchKernelGGL(dcr::k_ins_layout<false>, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
             // (its 66 KB blocks wait for room beside the inflate waves in the
             // whole-node pipeline even when they find no deep record: up to
             // 7 ms per C2 pass, profiles/r06g)
             if (c->max_r_hint < 0 || c->max_r_hint >= dcr::kDeepReads)
                 hipLaunchKernelGGL(dcr::k_decide_deep, dim3(2 * c->n_cu), dim3(dcr::kDeepWaves * dcr::kWave), 0, c->stream,
                                    a);
+            // after k_decide_deep: it reads the general list's entries, which
+            // k_ins_layout marks decided (bit 31) for the records it decides
+            if (DCR_LAYOUT_KERNEL)
+                hipLaunchKernelGGL(dcr::k_ins_layout<false>, dim3(grid_for(a.n_rec, 2048)), dim3(256), 0, c->stream, a);
             hipLaunchKernelGGL(dcr::k_consensus_general<false>, dim3(grid_for(a.n_rec, 1024)), dim3(256), 0,
                                c->stream, a);
         }

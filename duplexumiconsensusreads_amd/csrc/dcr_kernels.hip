@@ -1777,7 +1777,7 @@ __device__ __forceinline__ void process_record(const Args &a, const int64_t rec,
             co = tco;
         } else if (decided) {
             const uint32_t w = live ? (uint32_t)a.ws.cons[off + t] : 0u;
-            co.ch = (int)((0x2D2B47435441ull >> (8 * (w & 7u))) & 0xffu);   // "ATCG+-"
+            co.ch = (int)((0x2D2B47435441ull >> (8 * (w & 7u))) & 0xffu) + (((w >> 27) & 1u) ? 32 : 0);   // "ATCG+-"
             co.q = P->max_base_quality;
             co.d = (int)((w >> 3) & 4095u);
             co.e = (int)((w >> 15) & 4095u);
@@ -4198,6 +4198,10 @@ __global__ __launch_bounds__(256) void k_ins_layout(Args a) {
     __shared__ uint32_t s_scr[kWavesPerBlock][4 * kWave];   // phase A: an I read's r, need, L | bases << 16, start
     __shared__ uint32_t s_iev[kWavesPerBlock][4 * kWave];   // per read: run start | L << 9 | bases << 16 (511: none)
     __shared__ __attribute__((aligned(16))) uint32_t s_rt[kWavesPerBlock][16 * kWave];  // phase B: a chunk's read table
+    __shared__ uint32_t s_wtab[DCR_LUT_N];
+    if (a.t16 >= 0)
+        for (int i = threadIdx.x; i < DCR_LUT_N; i += kBlock) s_wtab[i] = a.wtab[i];
+    __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int n = a.ws.ovf_count[DUPLEX ? 1 : 0];
@@ -4321,13 +4325,25 @@ __global__ __launch_bounds__(256) void k_ins_layout(Args a) {
                     }
                     uint16_t *rows = a.ws.lay + (DUPLEX ? (int64_t)a.in.n_reads + 2 * rec : (int64_t)a.in.sub_off[rec]) * kLayRow;
                     // phase B: lane = column, 64 at a time; per read the
-                    // column-free values computed lane-parallel (lane = read)
+                    // column-free values computed lane-parallel (lane = read).
+                    // The columns' integer decision sums ride along (k_decide's
+                    // bound, decide_end, insertion columns included): a record
+                    // whose every column is decided is marked decided and the
+                    // general kernel forms no product for it
+                    bool all_dec = a.t16 >= 0 && decide_usable(a, R);
+                    int32_t *cw = a.ws.cons + (DUPLEX ? a.in.ds_col_off : a.in.ss_col_off)[rec];
+                    // pass 0 decides (no rows written); the rows only when some
+                    // column stays undecided (pass 1)
+                    for (int pass = all_dec ? 0 : 1; pass < 2; ++pass) {
+                    if (pass == 1 && all_dec) break;
+                    const bool wr = pass == 1;
                     int nbase = 0;
-                    for (int c0 = 0; c0 < T; c0 += kWave) {
+                    for (int c0 = 0; c0 < T && (wr || all_dec); c0 += kWave) {
                         const int t2 = c0 + lane;
                         const uint64_t mw = imask[c0 >> 6];
                         const bool insc = ((mw >> lane) & 1ull) != 0;
                         const int Nt = nbase + __popcll(~mw & (lane == 0 ? 0ull : (~0ull >> (64 - lane))));
+                        DecideSums D;
                         for (int cb = 0; cb < R; cb += kWave) {
                             const int nr = min(kWave, R - cb);
                             // lane = read of this chunk: everything per read that
@@ -4402,14 +4418,31 @@ __global__ __launch_bounds__(256) void k_ins_layout(Args a) {
                                 for (int u = 0; u < kU; ++u) {
                                     const uint32_t e = ku[u] == 0u ? make_code<DUPLEX>(bu[u], qu[u], minbq)
                                                      : ku[u] == 1u ? kPlus : ku[u] == 2u ? kPad : kDel;
-                                    if (r0 + u < nr && t2 < T)
-                                        rows[((int64_t)(t2 >> 5) * R + cb + r0 + u) * kTileIns + (t2 & 31)] = (uint16_t)e;
+                                    if (r0 + u < nr) {
+                                        if (!wr) D.add(e, s_wtab);
+                                        if (wr && t2 < T) rows[((int64_t)(t2 >> 5) * R + cb + r0 + u) * kTileIns + (t2 & 31)] = (uint16_t)e;
+                                    }
                                 }
                             }
                             lds_fence();      // the read table is rewritten by the next chunk
                         }
                         nbase += __popcll(~mw & (T - c0 >= 64 ? ~0ull : ((1ull << (T - c0)) - 1ull)));
+                        if (!wr) {
+                            ColOut co;
+                            if (decide_end(a, R, t2 < T, insc, D, co)) {
+                                const int uc = co.ch >= 'a' ? co.ch - 32 : co.ch;
+                                const uint32_t kb = uc == 'A' ? 0u : uc == 'T' ? 1u : uc == 'C' ? 2u : uc == 'G' ? 3u
+                                                  : uc == '+' ? 4u : 5u;
+                                if (t2 < T)
+                                    cw[t2] = (int32_t)(kb | (uint32_t)co.d << 3 | (uint32_t)co.e << 15 |
+                                                       (co.ch >= 'a' ? 1u : 0u) << 27);
+                            } else {
+                                all_dec = false;
+                            }
+                        }
                     }
+                    }
+                    if (all_dec && lane == 0) a.ws.ovf[i] = (int)rec | (int)0x80000000u;
                 }
             }
         }
