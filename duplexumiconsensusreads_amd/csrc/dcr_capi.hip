@@ -414,6 +414,7 @@ int dcr_reserve(dcr_ctx *c, const dcr_batch *s) {
     c->w.xcount = (int *)(b + o_err) + 5;
     c->w.gen_next = (int *)(b + o_err) + 7;      // [2], in the same block: reset with it per batch
     c->w.deep_count = (int *)(b + o_err) + 9;    // [1], likewise
+    c->w.lay_next = (int *)(b + o_err) + 10;     // [2], likewise
     c->w.lay_base = (int *)(b + o_lb);
     c->w.lay_mask = (uint64_t *)(b + o_lm);
     c->w.lay = (uint16_t *)(b + o_lay);

@@ -56,6 +56,7 @@ struct Workspace {
     int *gen_next;          // [2] next general-list entry to claim (k_consensus_general)
     int *deep;              // [n_rec] general-list indices of deep single-strand records (k_decide_deep)
     int *deep_count;        // [1] their number
+    int *lay_next;          // [2] next general-list entry to claim (k_ins_layout)
     int *xlist;             // [n_rec] exact queue: fast-list indices (k_consensus_fast<., true>)
     unsigned long long *stamps;   // [32] diagnostic phase cycles (DCR_STAMP builds only)
     RecMeta *meta;          // [n_rec] fast list

@@ -38,6 +38,18 @@
 #ifndef DCR_GSTAMP
 #define DCR_GSTAMP 0  // diagnostic builds only (tools/gstamps.py): per-phase s_memtime cycles of the general kernel
 #endif
+#ifndef DCR_LAYHOIST
+#define DCR_LAYHOIST 1  // k_ins_layout: a record of <= 64 reads builds its read table once
+#endif
+#ifndef DCR_LAYU
+#define DCR_LAYU 2    // k_ins_layout: reads whose byte loads are in flight together (2: 5 waves per SIMD; 4: 4, slower)
+#endif
+#ifndef DCR_LAYCLAIM
+#define DCR_LAYCLAIM 1  // k_ins_layout: records claimed one at a time past the first (0: fixed stride)
+#endif
+#ifndef DCR_LAYOCC
+#define DCR_LAYOCC 1  // k_ins_layout: waves per SIMD its launch bounds ask for
+#endif
 #ifndef DCR_FAST_OCC
 #define DCR_FAST_OCC 7   // fast kernel (common instantiation): waves per SIMD the launch bounds ask for
 #endif
@@ -4194,7 +4206,7 @@ __global__ __launch_bounds__(kBlock, DCR_GEN_OCC) void k_consensus_general(Args 
 // general kernel then lays it out column by column, reproducing the
 // reference's IndexErrors.
 template <bool DUPLEX>
-__global__ __launch_bounds__(256) void k_ins_layout(Args a) {
+__global__ __launch_bounds__(256, DCR_LAYOCC) void k_ins_layout(Args a) {
     __shared__ uint32_t s_scr[kWavesPerBlock][4 * kWave];   // phase A: an I read's r, need, L | bases << 16, start
     __shared__ uint32_t s_iev[kWavesPerBlock][4 * kWave];   // per read: run start | L << 9 | bases << 16 (511: none)
     __shared__ __attribute__((aligned(16))) uint32_t s_rt[kWavesPerBlock][16 * kWave];  // phase B: a chunk's read table
@@ -4211,7 +4223,20 @@ __global__ __launch_bounds__(256) void k_ins_layout(Args a) {
     uint32_t *scr = s_scr[wave];
     uint32_t *iev = s_iev[wave];
     uint32_t *rt = s_rt[wave];
-    for (int i = blockIdx.x * kWavesPerBlock + wave; i < n; i += nw) {
+    int *lnext = a.ws.lay_next + (DUPLEX ? 1 : 0);
+    // single-strand: the first record of each wave by position, then one
+    // claim per record (records of up to 256 reads and columns: a fixed
+    // stride left the waves holding the heavy ones as the tail; C3 general
+    // slot 11.98 -> 11.13 ms).  Duplex records (two reads each) keep the
+    // stride: 30 k claims on one counter cost 0.27 ms there.
+    auto claim = [&]() {
+        const uint64_t act = __ballot(1);
+        const int leader = __ffsll((long long)act) - 1;
+        int t = 0;
+        if (lane == leader) t = atomicAdd(lnext, 1);
+        return nw + __builtin_amdgcn_readfirstlane(__shfl(t, leader, kWave));
+    };
+    for (int i = blockIdx.x * kWavesPerBlock + wave; i < n; i = DCR_LAYCLAIM && !DUPLEX ? (nw >= n ? n : claim()) : i + nw) {
         const int vv = a.ws.ovf[i];
         if (vv < 0) continue;                         // decided by k_decide: no insertion column
         const int64_t rec = vv;
@@ -4220,10 +4245,23 @@ __global__ __launch_bounds__(256) void k_ins_layout(Args a) {
         if (R > 0 && R <= 4 * kWave) {
             int minpos = 0x7fffffff, maxend = -0x7fffffff;
             bool up = false, ins = false;
+            // the first 64 reads' references stay in registers (lane = read)
+            // and their first four runs in the read table's last four words
+            // (rt[16 r + 12..15], which the table leaves alone) for phase A
+            // and the table
+            ReadRef rd0{};
             for (int c = 0; c < R; c += kWave) {
                 const int r = c + lane;
                 if (r < R) {
                     const ReadRef rd = get_read<DUPLEX>(a, rec, r);
+                    if (DCR_LAYHOIST && c == 0) {
+                        rd0 = rd;
+                        const int kl = max(rd.ncig - 1, 0);      // every load issued at once, clamped to the read's runs
+                        const uint32_t v0 = rd.cig[0], v1 = rd.cig[min(1, kl)], v2 = rd.cig[min(2, kl)],
+                                       v3 = rd.cig[min(3, kl)];
+                        ((uint4 *)&rt[16 * lane])[3] = make_uint4(rd.ncig > 0 ? v0 : 0u, rd.ncig > 1 ? v1 : 0u,
+                                                                  rd.ncig > 2 ? v2 : 0u, rd.ncig > 3 ? v3 : 0u);
+                    }
                     up |= rd.status != 0 || rd.len <= 0;
                     minpos = min(minpos, rd.pos);
                     maxend = max(maxend, rd.pos + rd.len);
@@ -4248,10 +4286,13 @@ __global__ __launch_bounds__(256) void k_ins_layout(Args a) {
                 bool isI = false, b_r = false;
                 uint32_t need = 0, L = 0, bb = 0, sr = 0;
                 if (r < R) {
-                    const ReadRef rd = get_read<DUPLEX>(a, rec, r);
+                    const bool reg = DCR_LAYHOIST && c == 0;
+                    const ReadRef rd = reg ? rd0 : get_read<DUPLEX>(a, rec, r);
+                    const uint32_t *cg0 = &rt[16 * lane + 12];
                     int nIr = 0, acc = 0, accb = 0, mi = 0;
-                    for (int k = 0; k < min(rd.ncig, 4); ++k) {
-                        const uint32_t v = rd.cig[k];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t v = k >= rd.ncig ? 2u : reg ? cg0[k] : rd.cig[k];   // past the runs: D of length 0
                         const int o = (int)(v & 15u), ln = (int)(v >> 4);
                         if (o == 1 && nIr == 0) {
                             need = (uint32_t)acc;
@@ -4332,6 +4373,45 @@ __global__ __launch_bounds__(256) void k_ins_layout(Args a) {
                     // general kernel forms no product for it
                     bool all_dec = a.t16 >= 0 && decide_usable(a, R);
                     int32_t *cw = a.ws.cons + (DUPLEX ? a.in.ds_col_off : a.in.ss_col_off)[rec];
+                    // lane = read of a chunk: everything per read that does
+                    // not depend on the column, into the wave's read table
+                    // (read back as uniform-address LDS loads: no readlane
+                    // into scalar registers, which spilled); built once for a
+                    // record of at most 64 reads, per chunk and block beyond
+                    auto build_rt = [&](const int cb, const int nr) {
+                    if (lane < nr) {
+                        const bool reg = DCR_LAYHOIST && cb == 0;
+                        const ReadRef rd = reg ? rd0 : get_read<DUPLEX>(a, rec, cb + lane);
+                        const uint4 cq = ((const uint4 *)&rt[16 * lane])[3];
+                        const uint32_t cg0[4] = {cq.x, cq.y, cq.z, cq.w};
+                        const int sr = rd.pos - minpos;
+                        int end = 0, bb = 0, ends[4], bbs[4];
+                        uint32_t dm = 0;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const uint32_t v = k < rd.ncig ? (reg ? cg0[k] : rd.cig[k]) : 0u;
+                            const int ln = k < rd.ncig ? (int)(v >> 4) : 0;
+                            const bool isd = (v & 15u) == 2u;
+                            bbs[k] = bb;
+                            end += ln;
+                            ends[k] = end;
+                            bb += isd ? 0 : ln;
+                            dm |= (isd ? 1u : 0u) << k;
+                        }
+                        uint4 *row = (uint4 *)&rt[16 * lane];
+                        row[0] = make_uint4((uint32_t)sr, (uint32_t)rd.len, (uint32_t)(sr - ins_below(imask, sr)),
+                                            iev[cb + lane]);
+                        row[1] = make_uint4((uint32_t)ends[0] | (uint32_t)ends[1] << 16,
+                                            (uint32_t)ends[2] | (uint32_t)ends[3] << 16,
+                                            (uint32_t)bbs[1] | (uint32_t)bbs[2] << 16,
+                                            (uint32_t)bbs[3] | (uint32_t)bb << 16 | 0u);
+                        rt[16 * lane + 8] = dm;
+                        ((int64_t *)&rt[16 * lane])[5] = rd.seq_start;
+                    }
+                        lds_fence();
+                    };
+                    const bool one = DCR_LAYHOIST && R <= kWave;
+                    if (one) build_rt(0, R);
                     // pass 0 decides (no rows written); the rows only when some
                     // column stays undecided (pass 1)
                     for (int pass = all_dec ? 0 : 1; pass < 2; ++pass) {
@@ -4340,46 +4420,17 @@ __global__ __launch_bounds__(256) void k_ins_layout(Args a) {
                     int nbase = 0;
                     for (int c0 = 0; c0 < T && (wr || all_dec); c0 += kWave) {
                         const int t2 = c0 + lane;
-                        const uint64_t mw = imask[c0 >> 6];
+                        const int wq = c0 >> 6;       // no dynamic index: imask stays in registers
+                        const uint64_t mw = wq == 0 ? imask[0] : wq == 1 ? imask[1] : wq == 2 ? imask[2] : imask[3];
                         const bool insc = ((mw >> lane) & 1ull) != 0;
                         const int Nt = nbase + __popcll(~mw & (lane == 0 ? 0ull : (~0ull >> (64 - lane))));
                         DecideSums D;
                         for (int cb = 0; cb < R; cb += kWave) {
                             const int nr = min(kWave, R - cb);
-                            // lane = read of this chunk: everything per read that
-                            // does not depend on the column, into the wave's read
-                            // table (read back as uniform-address LDS loads: no
-                            // readlane into scalar registers, which spilled)
-                            if (lane < nr) {
-                                const ReadRef rd = get_read<DUPLEX>(a, rec, cb + lane);
-                                const int sr = rd.pos - minpos;
-                                int end = 0, bb = 0, ends[4], bbs[4];
-                                uint32_t dm = 0;
-#pragma unroll
-                                for (int k = 0; k < 4; ++k) {
-                                    const uint32_t v = k < rd.ncig ? rd.cig[k] : 0u;
-                                    const int ln = k < rd.ncig ? (int)(v >> 4) : 0;
-                                    const bool isd = (v & 15u) == 2u;
-                                    bbs[k] = bb;
-                                    end += ln;
-                                    ends[k] = end;
-                                    bb += isd ? 0 : ln;
-                                    dm |= (isd ? 1u : 0u) << k;
-                                }
-                                uint4 *row = (uint4 *)&rt[16 * lane];
-                                row[0] = make_uint4((uint32_t)sr, (uint32_t)rd.len, (uint32_t)(sr - ins_below(imask, sr)),
-                                                    iev[cb + lane]);
-                                row[1] = make_uint4((uint32_t)ends[0] | (uint32_t)ends[1] << 16,
-                                                    (uint32_t)ends[2] | (uint32_t)ends[3] << 16,
-                                                    (uint32_t)bbs[1] | (uint32_t)bbs[2] << 16,
-                                                    (uint32_t)bbs[3] | (uint32_t)bb << 16 | 0u);
-                                rt[16 * lane + 8] = dm;
-                                ((int64_t *)&rt[16 * lane])[5] = rd.seq_start;
-                            }
-                            lds_fence();
+                            if (!one) build_rt(cb, nr);
                             const uint8_t *gb = DUPLEX ? a.ss.seq : a.in.bases;
                             const uint8_t *gq = DUPLEX ? a.ss.qual : a.in.quals;
-                            constexpr int kU = 4;     // reads whose byte loads are in flight together
+                            constexpr int kU = DCR_LAYU;     // reads whose byte loads are in flight together
                             for (int r0 = 0; r0 < nr; r0 += kU) {
                                 int64_t pu[kU];
                                 uint32_t ku[kU];      // 0 base, 1 '+', 2 pad, 3 '-'
@@ -4424,7 +4475,7 @@ __global__ __launch_bounds__(256) void k_ins_layout(Args a) {
                                     }
                                 }
                             }
-                            lds_fence();      // the read table is rewritten by the next chunk
+                            if (!one) lds_fence();      // the read table is rewritten by the next chunk
                         }
                         nbase += __popcll(~mw & (T - c0 >= 64 ? ~0ull : ((1ull << (T - c0)) - 1ull)));
                         if (!wr) {
