@@ -4236,7 +4236,9 @@ __global__ __launch_bounds__(256, DCR_LAYOCC) void k_ins_layout(Args a) {
         if (lane == leader) t = atomicAdd(lnext, 1);
         return nw + __builtin_amdgcn_readfirstlane(__shfl(t, leader, kWave));
     };
+    uint64_t gacc[3] = {0, 0, 0}, gcnt[3] = {0, 0, 0}, gmax = 0;   // DCR_GSTAMP builds: ticks per record class
     for (int i = blockIdx.x * kWavesPerBlock + wave; i < n; i = DCR_LAYCLAIM && !DUPLEX ? (nw >= n ? n : claim()) : i + nw) {
+        const uint64_t g0 = DCR_GSTAMP ? __builtin_amdgcn_s_memtime() : 0;
         const int vv = a.ws.ovf[i];
         if (vv < 0) continue;                         // decided by k_decide: no insertion column
         const int64_t rec = vv;
@@ -4498,6 +4500,24 @@ __global__ __launch_bounds__(256, DCR_LAYOCC) void k_ins_layout(Args a) {
             }
         }
         if (lane == 0) a.ws.lay_base[lb_off + rec] = lay;
+        if (DCR_GSTAMP) {
+            const uint64_t dt = __builtin_amdgcn_s_memtime() - g0;
+            const int cls = lay < 0 ? 0 : R <= kWave ? 1 : 2;
+            gacc[0] += cls == 0 ? dt : 0;
+            gacc[1] += cls == 1 ? dt : 0;
+            gacc[2] += cls == 2 ? dt : 0;
+            gcnt[0] += cls == 0;
+            gcnt[1] += cls == 1;
+            gcnt[2] += cls == 2;
+            gmax = dt > gmax ? dt : gmax;
+        }
+    }
+    if (DCR_GSTAMP && !DUPLEX && lane == 0) {
+        for (int k = 0; k < 3; ++k) {
+            atomicAdd(&a.ws.stamps[20 + k], (unsigned long long)gacc[k]);
+            atomicAdd(&a.ws.stamps[23 + k], (unsigned long long)gcnt[k]);
+        }
+        atomicMax(&a.ws.stamps[26], (unsigned long long)gmax);
     }
 }
 

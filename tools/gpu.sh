@@ -65,7 +65,7 @@ for step in "$@"; do
       find "$O/kt$sfx" -name "*kernel_trace.csv" -exec python3 tools/kt_grid.py {} \; > "$O/kernel_grid$sfx.csv" || exit 1
       find "$O/kt$sfx" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats$sfx.csv" \;
       grep '^{' "$O/kt$sfx.txt" | tail -1 > "$O/bench_kt$sfx.json" ;;
-    traffic) run traffic 600 bash tools/gpu_traffic.sh "$TAG" || exit 1 ;;
+    traffic) run "traffic$val" 600 bash tools/gpu_traffic.sh "$TAG" $val || exit 1 ;;   # traffic=C3: that config
     pmc)
       IFS=: read -r ctrs lib <<< "$val"
       # shellcheck disable=SC2086

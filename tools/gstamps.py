@@ -57,3 +57,9 @@ for kind, base, kidx in (("single-strand", 0, 3), ("duplex", 32, 7)):
         n = st[base + 12 + c] / K
         cyc = st[base + 8 + c] / K
         print(f"   class {classes[c]:38s} records {n:9.0f}  ticks/record {cyc / max(n, 1):10.1f}  share {100.0 * cyc / max(sum(st[base + 8 + j] for j in range(4)) / K, 1):5.1f} %")
+lcls = ["not laid out (no insertion, ineligible)", "laid out, <= 64 reads", "laid out, 65-256 reads"]
+print(f"k_ins_layout<ss>: s_memtime ticks per record per wave (its slot is inside the general slot above); "
+      f"longest record {st[26]} ticks")
+for c in range(3):
+    n = st[23 + c] / K
+    print(f"   {lcls[c]:42s} records {n:9.0f}  ticks/record {st[20 + c] / K / max(n, 1):10.1f}")
