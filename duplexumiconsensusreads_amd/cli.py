@@ -71,7 +71,8 @@ def parse_args(argv):
     ap.add_argument("--deletion_score", required=False, default=30, type=int)
     ap.add_argument("--no_insertion_score", required=False, default=30, type=int)
     # not reference flags: batching and codec knobs (they do not change any record)
-    ap.add_argument("--batch_reads", required=False, default=1 << 19, type=int, help=argparse.SUPPRESS)
+    ap.add_argument("--batch_reads", required=False, default=int(os.environ.get("DCR_BATCH_READS", 1 << 19)), type=int,
+                    help=argparse.SUPPRESS)   # DCR_BATCH_READS: A/B runs of the bench, which calls main() without flags
     ap.add_argument("--threads", required=False, default=0, type=int, help=argparse.SUPPRESS)
     ap.add_argument("--compression_level", required=False, default=6, type=int, help=argparse.SUPPRESS)
     ap.add_argument("--device", required=False, default=0, type=int, help=argparse.SUPPRESS)
