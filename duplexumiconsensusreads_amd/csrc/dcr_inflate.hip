@@ -73,7 +73,7 @@ struct IStamp {
 // at 8 KiB / 10 bits) inflate a 4,096-member span in 5.65 ms instead of 9.09
 // (35.2 -> 47.5 GB/s over all members in one launch; profiles/r04e)
 #ifndef DINF_WG_PER_CU
-#define DINF_WG_PER_CU 12 // k_inflate launch grid cap per CU (0: one workgroup per member)
+#define DINF_WG_PER_CU 16 // k_inflate launch grid cap per CU (0: one workgroup per member)
 #endif
 #ifndef DINF_RING
 #define DINF_RING 4096    // LDS output history per member (bytes)
@@ -607,13 +607,15 @@ __device__ __forceinline__ void inflate_one(const Args &a, WaveLds &s, const int
 }
 
 // Wave w takes members w, w + gridDim.x, ...  The grid is capped at
-// DINF_WG_PER_CU workgroups per CU (12 of the 16 that fit), so a span never
-// holds every wave slot and LDS byte of a CU and the batch kernels beside it
-// find room at once.  The member decode is latency-bound: 4 or 2 waves per CU
-// starved the inflate (117 -> 266 / 390 ms of kernel time per pass) and the
-// whole node lost (357 -> 268 / 204 M consensus bases/s, profiles/r05r); once
-// the host walk stopped waiting for chunks, 12 per CU beat the uncapped grid
-// (profiles/r05ab: 429 vs 419 M at level 1, 470 vs 422 M at level 6).
+// DINF_WG_PER_CU workgroups per CU.  The member decode is latency-bound: 4 or
+// 2 waves per CU starved the inflate (117 -> 266 / 390 ms of kernel time per
+// pass) and the whole node lost (357 -> 268 / 204 M consensus bases/s,
+// profiles/r05r); 12 per CU beat the uncapped grid in round 5 (profiles/r05ab:
+// 429 vs 419 M at level 1, 470 vs 422 M at level 6).  With round 6's pass
+// bound by the batch stream, 16 per CU (every workgroup whose LDS fits)
+// decodes a pass in 92 instead of 120 ms of kernel time and the whole node
+// gains (ten interleaved pairs, profiles/r06wg: 400.8 vs 391.8 M at level 1,
+// 449.6 vs 423.6 M at level 6); 6, 8 and 10 per CU were slower or level.
 __global__ __launch_bounds__(64) void k_inflate(Args a) {
     WaveLds &s = *reinterpret_cast<WaveLds *>(smem);
     const int lane = lane_id();
