@@ -75,6 +75,9 @@ struct IStamp {
 #ifndef DINF_WG_PER_CU
 #define DINF_WG_PER_CU 16 // k_inflate launch grid cap per CU (0: one workgroup per member)
 #endif
+#ifndef DINF_CU_SHARE
+#define DINF_CU_SHARE 0   // diagnostic builds: the streaming inflate on DINF_CU_SHARE of every 8 CUs (0: all)
+#endif
 #ifndef DINF_RING
 #define DINF_RING 4096    // LDS output history per member (bytes)
 #endif
@@ -654,6 +657,7 @@ struct InflSlots {
 struct dcr_inflater {
     int device = 0;
     int grid_cap = 1 << 30;           // k_inflate workgroups per launch (resident waves)
+    int n_cu = 1;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     uint8_t *d_in = nullptr, *d_out = nullptr, *d_st = nullptr;
@@ -712,7 +716,8 @@ dcr_inflater *dcr_inflater_create(int device) {
         return nullptr;
     }
     h->base.x8n_piece = dfl::x8nmodp(dinf::kPiece);
-    if (DINF_WG_PER_CU > 0) h->grid_cap = DINF_WG_PER_CU * std::max(1, prop.multiProcessorCount);
+    h->n_cu = std::max(1, prop.multiProcessorCount);
+    if (DINF_WG_PER_CU > 0) h->grid_cap = DINF_WG_PER_CU * h->n_cu * (DINF_CU_SHARE > 0 ? DINF_CU_SHARE : 8) / 8;
     return h;
 }
 
@@ -949,7 +954,14 @@ extern "C" dcr_inflate_stream *dcr_inflate_stream_open(dcr_inflater *h, const ui
     }
     InflSlots &S = *h->slots;
     (void)hipSetDevice(h->device);
-    if ((!S.s_k && hipStreamCreateWithFlags(&S.s_k, hipStreamNonBlocking) != hipSuccess) ||
+    auto make_k = [&]() {
+        if (DINF_CU_SHARE <= 0) return hipStreamCreateWithFlags(&S.s_k, hipStreamNonBlocking);
+        std::vector<uint32_t> mask((size_t)(h->n_cu + 31) / 32, 0u);
+        for (int i = 0; i < h->n_cu; ++i)
+            if (i % 8 < DINF_CU_SHARE) mask[(size_t)i / 32] |= 1u << (i % 32);
+        return hipExtStreamCreateWithCUMask(&S.s_k, (uint32_t)mask.size(), mask.data());
+    };
+    if ((!S.s_k && make_k() != hipSuccess) ||
         (!S.s_out && hipStreamCreateWithFlags(&S.s_out, hipStreamNonBlocking) != hipSuccess)) {
         std::lock_guard<std::mutex> g(h->mu);
         S.busy = false;
