@@ -60,7 +60,10 @@ inline int32_t span_members(size_t k) { return k == 0 ? 128 : k == 1 ? 1024 : 40
 // The producer's ensure() calls then never allocate or free (on the device:
 // no hipFree / hipHostMalloc on the producer thread while kernels run,
 // DESIGN.md §5, the round-3 exit suspect).
-constexpr int32_t kSpanMembers = 4096;
+#ifndef DCR_SPAN_MEMBERS
+#define DCR_SPAN_MEMBERS 4096   // A/B builds only
+#endif
+constexpr int32_t kSpanMembers = DCR_SPAN_MEMBERS;
 constexpr size_t kSpanIn = (size_t)128 << 20;
 constexpr size_t kSpanOut = (size_t)kSpanMembers * 65536;
 
