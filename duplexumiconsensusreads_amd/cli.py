@@ -892,20 +892,45 @@ def _part_dir(finals):
     return os.path.dirname(os.path.abspath(finals[0]))
 
 
-def _write_part_at(part, final, n, off, threads=4):
-    """``n`` bytes of ``part`` written into ``final`` at ``off``: the part
-    mapped, pwritten from memory in slices by a few threads (page-cache
-    writes from user memory run about twice the rate of copy_file_range
-    between two files, and the slices proceed in parallel)."""
+def _write_part_at(part, final, n, off, threads=4, mapped=False):
+    """``n`` bytes of ``part`` written into ``final`` at ``off`` by a few
+    threads, the part mapped.  ``mapped``: the final file's range is already
+    allocated (rank 0's posix_fallocate before the offsets are broadcast), so
+    the range is mapped too and the slices are plain memory copies (page
+    faults of one file proceed in parallel, buffered writes to it take the
+    inode lock in turn: 200 MB in 0.075 s against 0.15 s by pwrite on ext4).
+    Otherwise the slices are pwritten from the mapped part (page-cache writes
+    from user memory run about twice the rate of copy_file_range between two
+    files)."""
     import mmap
-    fd = os.open(final, os.O_WRONLY)
+    if not n:
+        return
+    fd = os.open(final, os.O_RDWR if mapped else os.O_WRONLY)
     try:
         with open(part, "rb") as f:
-            mm = mmap.mmap(f.fileno(), n, prot=mmap.PROT_READ) if n else None
+            mm = mmap.mmap(f.fileno(), n, prot=mmap.PROT_READ)
+        step = max(1 << 20, -(-n // threads))
+        step = (step + 4095) & ~4095
+        starts = range(0, n, step)
+        # a mapping past the end of the file faults (SIGBUS): map only a range the file holds
+        if mapped and os.fstat(fd).st_size >= off + n:
+            a0 = off & ~(mmap.ALLOCATIONGRANULARITY - 1)
+            dm = mmap.mmap(fd, off + n - a0, offset=a0)
+            try:
+                dst = np.frombuffer(dm, np.uint8)[off - a0:]
+                src = np.frombuffer(mm, np.uint8)
+
+                def copy(a):
+                    np.copyto(dst[a:a + step], src[a:a + step])
+                with ThreadPoolExecutor(threads) as ex:
+                    list(ex.map(copy, starts))
+                del dst, src
+            finally:
+                dm.close()
+                mm.close()
+            return
         try:
-            view = memoryview(mm) if mm is not None else b""
-            step = max(1 << 20, -(-n // threads))
-            step = (step + 4095) & ~4095
+            view = memoryview(mm)
 
             def put(a):
                 b = min(a + step, n)
@@ -915,11 +940,10 @@ def _write_part_at(part, final, n, off, threads=4):
                 put(0)
             else:
                 with ThreadPoolExecutor(threads) as ex:
-                    list(ex.map(put, range(0, n, step)))
+                    list(ex.map(put, starts))
         finally:
-            if mm is not None:
-                view.release()
-                mm.close()
+            view.release()
+            mm.close()
     finally:
         os.close(fd)
 
@@ -929,8 +953,9 @@ def _merge_parallel(dist, rank, finals, header, args, sizes, upto, parts):
     range straight into the final files (header, records, EOF); rank r > 0
     writes its part (without its EOF block) at rank 0's length minus its EOF
     plus the sizes of parts 1..r-1, an exclusive scan of the part sizes every
-    rank holds (``sizes[r][k]``), all ranks at once; rank 0 then puts the
-    BGZF EOF block at the end."""
+    rank holds (``sizes[r][k]``), all ranks at once, into ranges rank 0 has
+    allocated (posix_fallocate) before it broadcasts the offsets; rank 0 then
+    puts the BGZF EOF block at the end."""
     eof = len(_BGZF_EOF)
     if rank == 0:
         for k in range(3):
@@ -938,24 +963,44 @@ def _merge_parallel(dist, rank, finals, header, args, sizes, upto, parts):
                 w = native_io.BgzfWriter(finals[k], header, args.compression_level, args.threads)
                 w.close()
                 sizes[0][k] = os.path.getsize(finals[k])
-    obj = [[sizes[0][k] for k in range(3)]]
+
+    def ends_of(s0):
+        return [s0[k] - eof + sum(max(sizes[r][k] - eof, 0) for r in range(1, upto)) for k in range(3)]
+    mapped = False
+    if rank == 0 and upto > 1:
+        # the finals' whole length allocated before any rank writes: the
+        # ranks then copy into mapped ranges (no fault can meet a missing
+        # block or the end of the file); a file system without fallocate
+        # keeps the pwrite path
+        mapped = True
+        for k, e in enumerate(ends_of([sizes[0][j] for j in range(3)])):
+            fd = os.open(finals[k], os.O_RDWR)
+            try:
+                start = sizes[0][k] - eof
+                if e + eof > start:
+                    os.posix_fallocate(fd, start, e + eof - start)
+            except OSError:
+                mapped = False
+            finally:
+                os.close(fd)
+    obj = [[sizes[0][k] for k in range(3)], mapped]
     dist.broadcast_object_list(obj, src=0)
-    s0 = obj[0]
-    ends = []
+    s0, mapped = obj
+    ends = ends_of(s0)
     for k in range(3):
         off = s0[k] - eof
         for r in range(1, upto):
             n = max(sizes[r][k] - eof, 0)
             if r == rank and n:
-                _write_part_at(parts[k], finals[k], n, off)
+                _write_part_at(parts[k], finals[k], n, off, mapped=mapped)
             off += n
-        ends.append(off)
     if rank == 0:
         for k in range(3):
             fd = os.open(finals[k], os.O_WRONLY)
             try:
                 os.pwrite(fd, _BGZF_EOF, ends[k])
-                os.ftruncate(fd, ends[k] + eof)
+                if os.fstat(fd).st_size != ends[k] + eof:   # already so when the finals were allocated
+                    os.ftruncate(fd, ends[k] + eof)
             finally:
                 os.close(fd)
     dist.barrier()

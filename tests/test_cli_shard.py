@@ -235,3 +235,25 @@ def test_state_exchange_failure_marker():
     want.setstate(s0)
     want.sample(range(10), 3)
     assert r1.gate() == want.getstate()
+
+
+@pytest.mark.parametrize("mapped", [True, False])
+def test_write_part_at_places_the_part_byte_for_byte(tmp_path, mapped):
+    """The merge's part copy (cli._write_part_at): into a preallocated range
+    through a mapping (unaligned offsets, parts larger than one slice) or by
+    pwrite, the final file holds its prefix and then the part's first n bytes."""
+    rng = random.Random(7)
+    for n, off in [(1, 0), (5000, 12345), (3 << 20, 4097), (9 << 20, 65535)]:
+        data = rng.randbytes(n)
+        part, final = tmp_path / "p.part", tmp_path / "f.bam"
+        part.write_bytes(data + b"tail")
+        head = rng.randbytes(off)
+        final.write_bytes(head)
+        if mapped:
+            fd = os.open(final, os.O_RDWR)
+            try:
+                os.posix_fallocate(fd, off, n)
+            finally:
+                os.close(fd)
+        cli._write_part_at(str(part), str(final), n, off, mapped=mapped)
+        assert final.read_bytes() == head + data
