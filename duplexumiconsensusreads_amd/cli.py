@@ -916,16 +916,14 @@ def _write_part_at(part, final, n, off, threads=4, mapped=False):
         if mapped and os.fstat(fd).st_size >= off + n:
             a0 = off & ~(mmap.ALLOCATIONGRANULARITY - 1)
             dm = mmap.mmap(fd, off + n - a0, offset=a0)
+            views = [np.frombuffer(dm, np.uint8)[off - a0:], np.frombuffer(mm, np.uint8)]
             try:
-                dst = np.frombuffer(dm, np.uint8)[off - a0:]
-                src = np.frombuffer(mm, np.uint8)
-
                 def copy(a):
-                    np.copyto(dst[a:a + step], src[a:a + step])
+                    np.copyto(views[0][a:a + step], views[1][a:a + step])
                 with ThreadPoolExecutor(threads) as ex:
                     list(ex.map(copy, starts))
-                del dst, src
             finally:
+                views.clear()                # the arrays export the mappings: released before closing
                 dm.close()
                 mm.close()
             return
