@@ -487,7 +487,10 @@ class Inflater {
   public:
     static constexpr size_t kHead = (size_t)8 << 20;
     static constexpr size_t kWant = (size_t)32 << 20;
-    static constexpr size_t kWantGpu = (size_t)64 << 20;
+#ifndef DCR_WANT_GPU_MIB
+#define DCR_WANT_GPU_MIB 64   // A/B builds only
+#endif
+    static constexpr size_t kWantGpu = (size_t)DCR_WANT_GPU_MIB << 20;
 
     // ranged: start at the BGZF block at file offset start_coff, start_uoff
     // bytes into its data, on a record boundary (no header); end_coff >= 0:
