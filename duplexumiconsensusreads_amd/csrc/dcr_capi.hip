@@ -924,7 +924,8 @@ int dcr_submit_write(dcr_ctx *c, int slot, const dcr_batch *h, const dcr_wmeta *
     const size_t o_scan = take(std::max(scan1, scan2));
     const size_t o_stream = take((size_t)B);
     const size_t o_slots = take((size_t)nbm * dfl::kSlot);
-    const size_t o_bsz = take(8 * (size_t)(nbm + 1)), o_boff = take(8 * (size_t)(nbm + 1));
+    // block sizes (+ the scan's total), then k_deflate's block counter
+    const size_t o_bsz = take(8 * (size_t)(nbm + 2)), o_boff = take(8 * (size_t)(nbm + 1));
     const size_t o_comp = take((size_t)nbm * dfl::kSlot);
     const size_t o_tot = take(8 * 4);
     const unsigned gd = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nbm, (int64_t)c->n_cu * c->dfl_blocks));
@@ -968,7 +969,7 @@ int dcr_submit_write(dcr_ctx *c, int slot, const dcr_batch *h, const dcr_wmeta *
     A.rec_off = (int64_t *)(wb + o_roff);
     A.stream = (uint8_t *)(wb + o_stream);
     HIP_TRY(hipMemsetAsync(rsz, 0, 8 * (size_t)(2 * F + 1), c->stream));
-    HIP_TRY(hipMemsetAsync(wb + o_bsz, 0, 8 * (size_t)(nbm + 1), c->stream));
+    HIP_TRY(hipMemsetAsync(wb + o_bsz, 0, 8 * (size_t)(nbm + 2), c->stream));
     if (F) {
         hipLaunchKernelGGL(dcrw::k_famfail, dim3((unsigned)((F + 255) / 256)), dim3(256), 0, c->stream, A);
         const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((2 * F + 3) / 4, (int64_t)c->n_cu * 8));
@@ -981,7 +982,8 @@ int dcr_submit_write(dcr_ctx *c, int slot, const dcr_batch *h, const dcr_wmeta *
         HIP_TRY(hipMemsetAsync(A.rec_off, 0, 8, c->stream));
     }
     int64_t *bsz = (int64_t *)(wb + o_bsz);
-    dcrw::DflArgs D{A.stream, A.rec_off + 2 * F, (uint8_t *)(wb + o_slots), bsz, (uint32_t *)(wb + o_tok), nullptr};
+    dcrw::DflArgs D{A.stream, A.rec_off + 2 * F, (uint8_t *)(wb + o_slots), bsz, (uint32_t *)(wb + o_tok), nullptr,
+                    DFL_CLAIM ? (unsigned long long *)(bsz + nbm + 1) : nullptr};
     hipLaunchKernelGGL(dcrw::k_deflate, dim3(gd), dim3(dfl::kT), sizeof(dfl::Shared), c->stream, D);
     HIP_TRY(hipGetLastError());
     int64_t *boff = (int64_t *)(wb + o_boff);
@@ -1070,7 +1072,7 @@ int dcr_deflate_probe(dcr_ctx *c, const uint8_t *host, int64_t n, unsigned long 
     HIP_TRY(hipMemcpy(d_in, host, (size_t)n, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(d_n, &n, 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemset(d_st, 0, 96));
-    dcrw::DflArgs D{d_in, d_n, d_slots, d_sizes, d_tok, d_st};
+    dcrw::DflArgs D{d_in, d_n, d_slots, d_sizes, d_tok, d_st, nullptr};
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));

@@ -25,6 +25,9 @@ struct FmtArgs {
     uint8_t *stream;                // formatted records
 };
 
+#ifndef DFL_CLAIM
+#define DFL_CLAIM 1   // pipeline k_deflate: blocks claimed from a counter (0: workgroup w takes w, w + grid, ...)
+#endif
 struct DflArgs {
     const uint8_t *stream;
     const int64_t *stream_bytes;    // device scalar (rec_off[2F])
@@ -32,6 +35,7 @@ struct DflArgs {
     int64_t *sizes;                 // per block (0 past the last block)
     uint32_t *tok;                  // dfl::kTokWords per workgroup of the grid
     unsigned long long *stamps;     // diagnostic (dcr_deflate_probe): s_memtime cycles per phase, or null
+    unsigned long long *claim;      // zeroed block counter: workgroups claim blocks from it (null: a fixed stride)
 };
 
 struct CompactArgs {

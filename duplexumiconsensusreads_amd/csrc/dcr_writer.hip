@@ -488,7 +488,18 @@ __global__ __launch_bounds__(dfl::kT) void k_deflate(DflArgs D) {
             t0 = now;
         }
     };
-    for (int64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    // blocks claimed one at a time when a counter is given: in the pipeline
+    // the grid's workgroups start as inflate workgroups leave their CUs, and
+    // a fixed stride left the late starters' blocks as the launch's tail
+    __shared__ int64_t s_claim;
+    auto claim = [&](int64_t fixed) -> int64_t {
+        if (!D.claim) return fixed;
+        __syncthreads();                 // every lane has read the previous claim
+        if (lane == 0) s_claim = (int64_t)atomicAdd(D.claim, 1ull);
+        __syncthreads();
+        return s_claim;
+    };
+    for (int64_t b = claim(blockIdx.x); b < nb; b = claim(b + gridDim.x)) {
         if (st && lane == 0) t0 = __builtin_amdgcn_s_memtime();
         const int64_t off = b * (int64_t)dfl::kMaxIn;
         const uint32_t n = (uint32_t)((total - off) < (int64_t)dfl::kMaxIn ? (total - off) : dfl::kMaxIn);
